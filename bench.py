@@ -1,0 +1,224 @@
+#!/usr/bin/env python
+"""Benchmark: the reference's headline workload -- one flow-matching train step
+of the hybrid PVConv backbone at B=8, N=20000 points, xyz+rgb (README.md:153,
+BASELINE.json configs[1]) -- on N MI355X GPUs, data parallel.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
+        --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...
+
+Prints ONE JSON line on rank 0.  value = points/s of the whole job
+(world * B * N * K / max-over-ranks wall time of K steps); inputs are resident
+in HBM before the timed region.  Besides the contract fields it carries:
+  roofline      the dominant hot-path kernel (by time inside the step), its
+                algorithmic bytes / its HIP-event time, vs 8 TB/s
+  cpu_baseline  the same train step on the host CPU (torch CPU + the C oracle
+                behind modules.functional), on a bounded sample
+  chamfer       Chamfer-3D fwd+bwd ms at the reference's published shape
+                (32x2000 / 32x1000, 1.4 ms) and at the C2 shape
+Progress goes to stderr.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(REPO, "point-cloud-flow-matching_amd")
+for _p in (REPO, PKG):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "train-step points/sec (B=8, N=20000, xyz+rgb) at 1/2/4/8 MI355X; Chamfer ms"
+HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+H100_DERIVED_PTS = 1.88e6       # 25 s/epoch at <= 293 steps/epoch (derived)
+
+
+def log(*a):
+    print("[bench]", *a, file=sys.stderr, flush=True)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--batch", type=int, default=8)
+    p.add_argument("--points", type=int, default=20000)
+    p.add_argument("--backbone", default="hybrid", choices=["hybrid", "mlp"])
+    p.add_argument("--surface", action="store_true", help="points near the unit sphere")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-batch", type=int, default=2, help="CPU baseline sample batch")
+    p.add_argument("--no-chamfer", action="store_true")
+    p.add_argument("--no-event-timing", action="store_true")
+    return p.parse_args()
+
+
+def chamfer_ms(dev, b, n, m, iters=20):
+    from chamfer3D.dist_chamfer_3D import chamfer_3DDist
+    cham = chamfer_3DDist()
+    g = torch.Generator(device=dev).manual_seed(0)
+    p1 = torch.rand(b, n, 3, device=dev, generator=g)
+    p2 = torch.rand(b, m, 3, device=dev, generator=g)
+
+    def once(fwd_only):
+        x = p1.detach().requires_grad_(not fwd_only)
+        d1, d2, _, _ = cham(x, p2)
+        if not fwd_only:
+            d1.sum().backward()  # unit_test.py:38-61 timings(): loss = sum(dist1)
+
+    res = {}
+    for fwd_only in (True, False):
+        for _ in range(3):
+            once(fwd_only)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            once(fwd_only)
+        torch.cuda.synchronize(dev)
+        res["fwd" if fwd_only else "fwd_bwd"] = (time.perf_counter() - t0) * 1e3 / iters
+    return res
+
+
+def cpu_baseline(args, cfg_kwargs):
+    """The reference's CPU-capable path (torch CPU, PVCNN ops through the C
+    oracle), one train step on a bounded sample after one warm-up step."""
+    from oracle.oracle import TorchBackend
+    import modules.functional.backend as be
+    from pcfm.train import TrainConfig, Trainer, synthetic_batch
+
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    saved = be._backend
+    be._backend = TorchBackend()
+    try:
+        cfg = TrainConfig(**{**cfg_kwargs, "batch_size": args.cpu_batch})
+        tr = Trainer(cfg, "cpu")
+        tr.train_mode()
+        batch = synthetic_batch(cfg, "cpu", surface=args.surface)
+        tr.step(batch, epoch=201)
+        t0 = time.perf_counter()
+        tr.step(batch, epoch=201)
+        dt = time.perf_counter() - t0
+    finally:
+        be._backend = saved
+    pts = cfg.batch_size * cfg.num_points
+    return {"value": pts / dt, "unit": "points/s", "cores": threads, "kind": "port",
+            "sample": f"1 timed train step (after 1 warm-up) at B={cfg.batch_size}, "
+                      f"N={cfg.num_points}, {cfg.pf_backbone} backbone, fp32 torch CPU + C "
+                      f"oracle voxel ops; {dt:.2f} s/step",
+            "seconds_per_step": dt}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    ddp = world > 1
+    if ddp:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", init_method="env://")
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from pcfm import _lib, ops
+    from pcfm.train import TrainConfig, Trainer, synthetic_batch
+    _lib.load()
+
+    cfg_kwargs = dict(batch_size=args.batch, num_points=args.points, pf_backbone=args.backbone)
+    cfg = TrainConfig(**cfg_kwargs)
+    tr = Trainer(cfg, dev, rank=rank, world_size=world, ddp=ddp)
+    tr.train_mode()
+    gen = torch.Generator(device=dev).manual_seed(1234 + rank)
+    batch = synthetic_batch(cfg, dev, generator=gen, surface=args.surface)
+    epoch = cfg.geom_warmup_epochs + 1  # full 6-D loss, CFG drop at its final rate
+
+    t_w = time.perf_counter()
+    for i in range(args.warmup):
+        tr.step(batch, epoch)
+        torch.cuda.synchronize(dev)
+        if rank == 0:
+            log(f"warmup step {i + 1}/{args.warmup} done ({time.perf_counter() - t_w:.1f} s)")
+
+    ops.timer.reset()
+    ops.timer.enabled = not args.no_event_timing
+    if ddp:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    last = None
+    for i in range(args.steps):
+        last = tr.step(batch, epoch)
+        if rank == 0 and (i + 1) % max(1, args.steps // 4) == 0:
+            log(f"timed step {i + 1}/{args.steps} issued")
+    torch.cuda.synchronize(dev)
+    if ddp:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    ops.timer.enabled = False
+    if ddp:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    loss_p, loss_z = float(last["loss_point"]), float(last["loss_latent"])
+
+    if rank == 0:
+        points = world * cfg.batch_size * cfg.num_points * args.steps
+        value = points / elapsed
+        ms = elapsed * 1e3 / args.steps
+        summary = ops.timer.summary()
+        kernels = {k: {"launches_per_step": v["launches"] / args.steps,
+                       "ms_per_step": v["ms"] / args.steps,
+                       "GBps": v["bytes"] / (v["ms"] * 1e-3) / 1e9 if v["ms"] > 0 else None}
+                   for k, v in summary.items()}
+        roofline = None
+        if summary:
+            dom = max(summary, key=lambda k: summary[k]["ms"])
+            d = summary[dom]
+            achieved = d["bytes"] / (d["ms"] * 1e-3) / 1e9
+            roofline = {"kernel": dom, "bound": "hbm", "achieved": achieved,
+                        "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                        "traffic": None,
+                        "algorithmic_bytes_per_launch": d["bytes"] / d["launches"],
+                        "avg_launch_ms": d["ms"] / d["launches"]}
+        log(f"{ms:.2f} ms/step, {value / 1e6:.3f} M points/s; losses {loss_p:.4f} {loss_z:.4f}")
+        cham = None
+        if not args.no_chamfer:
+            cham = {"published_shape_32x2000x1000": chamfer_ms(dev, 32, 2000, 1000),
+                    "published_fwd_bwd_ms": 1.4,
+                    "c2_shape_8x20000x20000": chamfer_ms(dev, 8, 20000, 20000, iters=5)}
+            log(f"chamfer: {cham}")
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            log("cpu baseline: running one warm-up + one timed CPU step ...")
+            cpu = cpu_baseline(args, cfg_kwargs)
+            log(f"cpu baseline: {cpu['seconds_per_step']:.2f} s/step")
+        line = {
+            "metric": METRIC, "value": value, "unit": "points/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "vs_h100_derived_upper_bound": value / H100_DERIVED_PTS,
+            "dtype": "fp32 voxel path + bf16 autocast MLP head (reference AMP config)",
+            "data": "synthetic (randn xyz, U[0,1] rgb, U[0,1] cond; no dataset on the box)",
+            "config": {"workload": "hybrid flow-matching train step, B=8/GPU, N=20000 xyz+rgb, "
+                                   "latent 128, 1 joint, stages (128,256,256)@(32,16,8)",
+                       "global_batch": world * cfg.batch_size, "points_per_cloud": cfg.num_points,
+                       "backbone": cfg.pf_backbone, "parallelism": f"dp{world}"},
+            "roofline": roofline, "kernels": kernels, "cpu_baseline": cpu, "chamfer": cham,
+            "loss_point": loss_p, "loss_latent": loss_z,
+        }
+        print(json.dumps(line), flush=True)
+    if ddp:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,169 @@
+/*
+ * pcfm.h -- C ABI of the MI355X-native point-cloud flow-matching hot path.
+ *
+ * One shared library (point-cloud-flow-matching_amd/csrc/libpcfm_hip.so, built
+ * for gfx950) exports every entry point below.  Conventions:
+ *
+ *   - every pointer is a DEVICE pointer (hipMalloc / torch CUDA tensor storage),
+ *     dense and contiguous in the layout written next to it;
+ *   - sizes are plain ints; `stream` is a hipStream_t passed as void* (NULL =
+ *     the legacy default stream) -- no HIP or torch type appears in this header;
+ *   - functions never allocate; scratch memory is passed as `ws` with the byte
+ *     count returned by the matching *_workspace_bytes() query;
+ *   - return value 0 = success, PCFM_EINVAL = bad argument (nothing launched),
+ *     any other positive value = the hipError_t of the failed launch.  The
+ *     reference backend calls exit(-1) on a launch failure
+ *     (third_party/pvcnn/modules/functional/src/cuda_utils.cuh:28-37); here the
+ *     caller decides (the Python layer raises RuntimeError, like TORCH_CHECK).
+ *     pcfm_last_error() returns a thread-local description of the last failure.
+ *
+ * Each function names the reference entry point it replaces (file:line under
+ * the reference tree).  Output ownership differs from the reference in one
+ * way only: the reference allocates zero-filled outputs inside the binding
+ * (torch::zeros); here the caller passes them in and the function writes every
+ * element (no pre-zeroing needed), except where "ACCUMULATES" is stated.
+ */
+#ifndef PCFM_H
+#define PCFM_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PCFM_OK 0
+#define PCFM_EINVAL -1
+
+/* ABI version: bumped on any signature change. */
+int pcfm_abi_version(void);
+/* Thread-local text of the last non-zero return code. */
+const char* pcfm_last_error(void);
+
+/* ------------------------------------------------------------------------
+ * PVConv voxel path
+ * ---------------------------------------------------------------------- */
+
+/* Scratch bytes pcfm_avg_voxelize_fwd needs for (b, n). */
+size_t pcfm_avg_voxelize_fwd_workspace_bytes(int b, int n);
+
+/* Average-pool voxelization, forward.
+ * Replaces avg_voxelize_forward (third_party/pvcnn/modules/functional/src/
+ * voxelization/vox.cpp:17-43) -> grid_stats_kernel + avg_voxelize_kernel
+ * (vox.cu:18-72).
+ *   feat   f32 [b, c, n]        coords i32 [b, 3, n]   (voxel coords in [0, r))
+ *   out    f32 [b, c, r^3]      out[c, v] = sum_{i: ind[i]=v} feat[c, i] * (1/cnt[v])
+ *   ind    i32 [b, n]           ind[i] = x*r*r + y*r + z
+ *   cnt    i32 [b, r^3]         points per voxel                                  */
+int pcfm_avg_voxelize_fwd(const float* feat, const int* coords, int b, int c, int n,
+                          int r, float* out, int* ind, int* cnt, void* ws,
+                          size_t ws_bytes, void* stream);
+
+/* Average-pool voxelization, backward.
+ * Replaces avg_voxelize_backward (vox.cpp:54-76) -> avg_voxelize_grad_kernel
+ * (vox.cu:86-110).
+ *   grad_y f32 [b, c, s]   ind i32 [b, n]   cnt i32 [b, s]   grad_x f32 [b, c, n]   */
+int pcfm_avg_voxelize_bwd(const float* grad_y, const int* ind, const int* cnt, int b,
+                          int c, int n, int s, float* grad_x, void* stream);
+
+/* Trilinear devoxelization, forward.
+ * Replaces trilinear_devoxelize_forward (src/interpolate/trilinear_devox.cpp:18-55)
+ * -> trilinear_devoxelize_kernel (trilinear_devox.cu:21-105).
+ *   coords f32 [b, 3, n] in [0, r-1]   feat f32 [b, c, r^3]   out f32 [b, c, n]
+ *   training != 0: also writes inds i32 [b, 8, n] and wgts f32 [b, 8, n];
+ *   training == 0: inds/wgts are ignored (may be NULL).                         */
+int pcfm_trilinear_devoxelize_fwd(const float* coords, const float* feat, int b, int c,
+                                  int n, int r, int training, float* out, int* inds,
+                                  float* wgts, void* stream);
+
+/* Trilinear devoxelization, backward.
+ * Replaces trilinear_devoxelize_backward (trilinear_devox.cpp:67-91) ->
+ * trilinear_devoxelize_grad_kernel (trilinear_devox.cu:119-162).
+ *   grad_y f32 [b, c, n]  inds i32 [b, 8, n]  wgts f32 [b, 8, n]
+ *   grad_x f32 [b, c, r^3]                                                      */
+int pcfm_trilinear_devoxelize_bwd(const float* grad_y, const int* inds, const float* wgts,
+                                  int b, int c, int n, int r, float* grad_x, void* stream);
+
+/* Ball query.  Replaces ball_query_forward (src/ball_query/ball_query.cpp:6-30)
+ * -> ball_query_kernel (ball_query.cu:19-50).
+ *   centers f32 [b, 3, m]  points f32 [b, 3, n]  idx i32 [b, m, u]
+ *   idx[j, 0..k) = the first k (<= u) point indices with |c - p|^2 < radius^2 in
+ *   index order; the remaining slots repeat the first hit; all zeros if none.     */
+int pcfm_ball_query(const float* centers, const float* points, int b, int m, int n,
+                    float radius, int u, int* idx, void* stream);
+
+/* Grouping forward.  Replaces grouping_forward (src/grouping/grouping.cpp:6-22)
+ * -> grouping_kernel (grouping.cu:18-36).
+ *   feat f32 [b, c, n]  idx i32 [b, m, u]  out f32 [b, c, m, u]                   */
+int pcfm_grouping_fwd(const float* feat, const int* idx, int b, int c, int n, int m,
+                      int u, float* out, void* stream);
+
+/* Grouping backward.  Replaces grouping_backward (grouping.cpp:24-44) ->
+ * grouping_grad_kernel (grouping.cu:58-77).
+ *   grad_y f32 [b, c, m, u]  idx i32 [b, m, u]  grad_x f32 [b, c, n]              */
+int pcfm_grouping_bwd(const float* grad_y, const int* idx, int b, int c, int n, int m,
+                      int u, float* grad_x, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Chamfer-3D
+ * ---------------------------------------------------------------------- */
+
+size_t pcfm_chamfer_workspace_bytes(int b, int n, int m);
+
+/* Chamfer forward, both directions.  Replaces chamfer_forward
+ * (third_party/ChamferDistancePytorch/chamfer3D/chamfer_cuda.cpp:17-19) ->
+ * chamfer_cuda_forward / NmDistanceKernel (chamfer3D.cu:12-154).
+ *   xyz1 f32 [b, n, 3]  xyz2 f32 [b, m, 3]
+ *   dist1 f32 [b, n], idx1 i32 [b, n]: squared distance / index of the nearest
+ *   point of xyz2 (ties -> lowest index); dist2/idx2 the same from xyz2 to xyz1.
+ *   Squared distance contract: d = fma(dz, dz, fma(dx, dx, dy*dy)), dx = q - p.  */
+int pcfm_chamfer_fwd(const float* xyz1, const float* xyz2, int b, int n, int m,
+                     float* dist1, float* dist2, int* idx1, int* idx2, void* ws,
+                     size_t ws_bytes, void* stream);
+
+/* Chamfer backward.  Replaces chamfer_backward (chamfer_cuda.cpp:22-27) ->
+ * NmDistanceGradKernel (chamfer3D.cu:155-195).  ACCUMULATES into grad_xyz1
+ * [b, n, 3] and grad_xyz2 [b, m, 3] (callers zero them, as the reference's do). */
+int pcfm_chamfer_bwd(const float* xyz1, const float* xyz2, int b, int n, int m,
+                     const float* grad_dist1, const float* grad_dist2, const int* idx1,
+                     const int* idx2, float* grad_xyz1, float* grad_xyz2, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Approximate EMD (approxmatch + matchcost), float and double like the
+ * reference's AT_DISPATCH_FLOATING_TYPES (PyTorchEMD/cuda/emd_kernel.cu).
+ * ---------------------------------------------------------------------- */
+
+/* elem_bytes = 4 (float) or 8 (double). */
+size_t pcfm_emd_workspace_bytes(int b, int n, int m, int elem_bytes);
+
+/* Replaces ApproxMatchForward (emd_kernel.cu:169-191) -> approxmatch (:24-156).
+ *   xyz1 [b, n, 3]  xyz2 [b, m, 3]  match [b, m, n]                              */
+int pcfm_emd_approxmatch_f32(const float* xyz1, const float* xyz2, int b, int n, int m,
+                             float* match, void* ws, size_t ws_bytes, void* stream);
+int pcfm_emd_approxmatch_f64(const double* xyz1, const double* xyz2, int b, int n, int m,
+                             double* match, void* ws, size_t ws_bytes, void* stream);
+
+/* Replaces MatchCostForward (emd_kernel.cu:255-277) -> matchcost (:199-241).
+ *   cost [b] = sum_{k,l} |xyz1[k] - xyz2[l]|^2 * match[l, k]                      */
+int pcfm_emd_matchcost_f32(const float* xyz1, const float* xyz2, const float* match, int b,
+                           int n, int m, float* cost, void* ws, size_t ws_bytes,
+                           void* stream);
+int pcfm_emd_matchcost_f64(const double* xyz1, const double* xyz2, const double* match,
+                           int b, int n, int m, double* cost, void* ws, size_t ws_bytes,
+                           void* stream);
+
+/* Replaces MatchCostBackward (emd_kernel.cu:371-396) -> matchcostgrad1/2
+ * (:285-353).  grad1 [b, n, 3], grad2 [b, m, 3] fully written.                   */
+int pcfm_emd_matchcost_bwd_f32(const float* grad_cost, const float* xyz1, const float* xyz2,
+                               const float* match, int b, int n, int m, float* grad1,
+                               float* grad2, void* ws, size_t ws_bytes, void* stream);
+int pcfm_emd_matchcost_bwd_f64(const double* grad_cost, const double* xyz1,
+                               const double* xyz2, const double* match, int b, int n, int m,
+                               double* grad1, double* grad2, void* ws, size_t ws_bytes,
+                               void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PCFM_H */

@@ -1,0 +1,479 @@
+// Approximate EMD: approxmatch, matchcost and its gradient (include/pcfm.h).
+//
+// Reference: third_party/PyTorchEMD/cuda/emd_kernel.cu.  The reference runs
+// the whole 10-level x 3-pass auction inside one block per batch element
+// (<<<32,512>>>, emd_kernel.cu:186) and read-modify-writes the dense
+// match[b, m, n] matrix once per level (:144).
+//
+// MI355X design:
+//   * every pass of every level is a full-chip launch: lanes own rows, the
+//     inner (column) loop is wave-uniform so the column points arrive through
+//     scalar loads, and the column range is split S ways into a partial-sum
+//     buffer that a small finalize kernel reduces in a fixed order;
+//   * match is NOT accumulated level by level.  Each level only needs the
+//     vectors ratioL (n) and ratioR (m), which are kept per level (10 x (n+m));
+//     match is written once at the end as
+//         match[l, k] = sum_j (exp(level_j * d2) * ratioL_j[k]) * ratioR_j[l]
+//     summed in the reference's level order -- the same per-entry expression
+//     and order as the reference's `match += w` (:143-144), with 1/10th of the
+//     HBM traffic.
+//   * exp is the hardware exp2 on x*log2(e): the reference is built with
+//     --use_fast_math (__expf, backend.py:20), so EMD parity is tolerance-based.
+#include "pcfm_common.hpp"
+
+#include <algorithm>
+
+namespace pcfm {
+namespace {
+
+constexpr int kLevels = 10;
+// level_j = -4^j for j = 7 .. -1, then 0 (emd_kernel.cu:44-48).
+__constant__ float c_levels[kLevels] = {-16384.0f, -4096.0f, -1024.0f, -256.0f, -64.0f,
+                                        -16.0f,    -4.0f,    -1.0f,    -0.25f,  0.0f};
+constexpr float h_levels[kLevels] = {-16384.0f, -4096.0f, -1024.0f, -256.0f, -64.0f,
+                                     -16.0f,    -4.0f,    -1.0f,    -0.25f,  0.0f};
+
+__device__ __forceinline__ float fast_expf(float x) {
+  return __builtin_amdgcn_exp2f(x * 1.4426950408889634f);
+}
+template <typename T>
+__device__ __forceinline__ T emd_exp(T x) {
+  return (T)fast_expf((float)x);
+}
+
+template <typename T>
+__device__ __forceinline__ T fmaT(T a, T b, T c);
+template <>
+__device__ __forceinline__ float fmaT<float>(float a, float b, float c) {
+  return __builtin_fmaf(a, b, c);
+}
+template <>
+__device__ __forceinline__ double fmaT<double>(double a, double b, double c) {
+  return __builtin_fma(a, b, c);
+}
+
+constexpr int kThreads = 256;
+
+// MODE 0: acc += e * coef[c]            (pass 1: coef = remainR, :70-76)
+// MODE 1: acc += e * coef[c]            (pass 2: coef = ratioL,  :102-107)
+// MODE 2: acc += (e * rowscale[i]) * coef[c]  (pass 3: ratioL[k] * ratioR[l], :139-146)
+// grid = (row blocks, S, b); part[s][b*nr + i].
+template <typename T, int MODE>
+__global__ void __launch_bounds__(kThreads)
+    emd_pass_kernel(const T* __restrict__ rows, int nr, const T* __restrict__ cols, int ncol,
+                    int b, T level, const T* __restrict__ coef, const T* __restrict__ rowscale,
+                    int S, T* __restrict__ part) {
+  const int bb = blockIdx.z;
+  const int s = blockIdx.y;
+  const int i = blockIdx.x * kThreads + threadIdx.x;
+  const int ii = i < nr ? i : nr - 1;
+  const T* rp = rows + ((size_t)bb * nr + ii) * 3;
+  const T x1 = rp[0], y1 = rp[1], z1 = rp[2];
+  T rl = (T)0;
+  if constexpr (MODE == 2) rl = rowscale[(size_t)bb * nr + ii];
+  const int c0 = (int)(((long long)ncol * s) / S);
+  const int c1 = (int)(((long long)ncol * (s + 1)) / S);
+  const T* __restrict__ cb = cols + (size_t)bb * ncol * 3;
+  const T* __restrict__ kb = coef + (size_t)bb * ncol;
+  T acc = 0;
+#pragma unroll 4
+  for (int c = c0; c < c1; ++c) {
+    const T d2 = sqdist3(cb[3 * c] - x1, cb[3 * c + 1] - y1, cb[3 * c + 2] - z1);
+    const T e = emd_exp<T>(level * d2);
+    if constexpr (MODE == 2) {
+      acc = fmaT<T>(e * rl, kb[c], acc);
+    } else {
+      acc = fmaT<T>(e, kb[c], acc);
+    }
+  }
+  if (i < nr) part[(size_t)s * b * nr + (size_t)bb * nr + i] = acc;
+}
+
+template <typename T>
+__device__ __forceinline__ T sum_parts(const T* part, int S, size_t stride, size_t i) {
+  T v = 0;
+  for (int s = 0; s < S; ++s) v += part[(size_t)s * stride + i];
+  return v;
+}
+
+template <typename T>
+__global__ void emd_init_kernel(T* remL, size_t nl, T multiL, T* remR, size_t nr, T multiR) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < nl) remL[i] = multiL;
+  if (i < nr) remR[i] = multiR;
+}
+
+// ratioL = remainL / (1e-9 + suml)    (:57, :81)
+template <typename T>
+__global__ void emd_fin1_kernel(const T* __restrict__ part, int S, size_t total,
+                                const T* __restrict__ remL, T* __restrict__ ratL) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  ratL[i] = remL[i] / ((T)1e-9f + sum_parts(part, S, total, i));
+}
+
+// sumr *= remainR; consumption = min(remainR / (sumr + 1e-9), 1);
+// ratioR = consumption * remainR; remainR = max(0, remainR - sumr)   (:111-116)
+// fminf/fmaxf take float arguments in the reference for both dtypes.
+template <typename T>
+__global__ void emd_fin2_kernel(const T* __restrict__ part, int S, size_t total,
+                                T* __restrict__ remR, T* __restrict__ ratR,
+                                T* __restrict__ levR) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const T r = remR[i];
+  T sumr = sum_parts(part, S, total, i);
+  sumr *= r;
+  const T cons = (T)fminf((float)(r / (sumr + (T)1e-9f)), 1.0f);
+  const T rat = cons * r;
+  ratR[i] = rat;
+  levR[i] = rat;
+  remR[i] = (T)fmaxf(0.0f, (float)(r - sumr));
+}
+
+// remainL = max(0, remainL - suml); keep this level's ratioL   (:150-151)
+template <typename T>
+__global__ void emd_fin3_kernel(const T* __restrict__ part, int S, size_t total,
+                                T* __restrict__ remL, const T* __restrict__ ratL,
+                                T* __restrict__ levL) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  remL[i] = (T)fmaxf(0.0f, (float)(remL[i] - sum_parts(part, S, total, i)));
+  levL[i] = ratL[i];
+}
+
+// match[b, l, k] = sum_j (exp(level_j * d2(k,l)) * ratioL_j[k]) * ratioR_j[l].
+// grid = (k blocks, l blocks of kLPer, b); lanes over k -> coalesced rows.
+constexpr int kLPer = 8;
+template <typename T>
+__global__ void __launch_bounds__(kThreads)
+    emd_match_kernel(const T* __restrict__ xyz1, const T* __restrict__ xyz2, int b, int n, int m,
+                     const T* __restrict__ levL, const T* __restrict__ levR,
+                     T* __restrict__ match) {
+  const int bb = blockIdx.z;
+  const int k = blockIdx.x * kThreads + threadIdx.x;
+  if (blockIdx.x * kThreads >= n) return;
+  const int kk = k < n ? k : n - 1;
+  const T* p1 = xyz1 + ((size_t)bb * n + kk) * 3;
+  const T x1 = p1[0], y1 = p1[1], z1 = p1[2];
+  T rl[kLevels];
+#pragma unroll
+  for (int j = 0; j < kLevels; ++j) rl[j] = levL[(size_t)j * b * n + (size_t)bb * n + kk];
+  const int l0 = blockIdx.y * kLPer;
+  const int l1 = min(m, l0 + kLPer);
+  for (int l = l0; l < l1; ++l) {
+    const T* p2 = xyz2 + ((size_t)bb * m + l) * 3;
+    const T d2 = sqdist3(p2[0] - x1, p2[1] - y1, p2[2] - z1);
+    T acc = 0;
+#pragma unroll
+    for (int j = 0; j < kLevels; ++j) {
+      const T rr = levR[(size_t)j * b * m + (size_t)bb * m + l];
+      const T e = emd_exp<T>((T)c_levels[j] * d2);
+      acc += (e * rl[j]) * rr;
+    }
+    if (k < n) match[((size_t)bb * m + l) * n + k] = acc;
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ T block_sum(T v, T* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  __syncthreads();
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  T t = 0;
+  if (threadIdx.x == 0)
+    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) t += red[i];
+  return t;  // valid in thread 0
+}
+
+// cost partials: grid = (k blocks, S, b); part[(bb*S + s)*kblocks + kb].
+template <typename T>
+__global__ void __launch_bounds__(kThreads)
+    emd_cost_kernel(const T* __restrict__ xyz1, const T* __restrict__ xyz2,
+                    const T* __restrict__ match, int b, int n, int m, int S,
+                    T* __restrict__ part) {
+  __shared__ T red[kThreads / 64];
+  const int bb = blockIdx.z, s = blockIdx.y;
+  const int k = blockIdx.x * kThreads + threadIdx.x;
+  const int kk = k < n ? k : n - 1;
+  const T* p1 = xyz1 + ((size_t)bb * n + kk) * 3;
+  const T x1 = p1[0], y1 = p1[1], z1 = p1[2];
+  const int l0 = (int)(((long long)m * s) / S), l1 = (int)(((long long)m * (s + 1)) / S);
+  const T* __restrict__ cb = xyz2 + (size_t)bb * m * 3;
+  T sub = 0;
+  if (k < n) {
+    for (int l = l0; l < l1; ++l) {
+      const T d = sqdist3(cb[3 * l] - x1, cb[3 * l + 1] - y1, cb[3 * l + 2] - z1);
+      sub = fmaT<T>(d, match[((size_t)bb * m + l) * n + k], sub);
+    }
+  }
+  const T t = block_sum(sub, red);
+  if (threadIdx.x == 0) part[((size_t)bb * S + s) * gridDim.x + blockIdx.x] = t;
+}
+
+template <typename T>
+__global__ void emd_cost_fin_kernel(const T* __restrict__ part, int per_b, int b,
+                                    T* __restrict__ cost) {
+  const int bb = blockIdx.x * blockDim.x + threadIdx.x;
+  if (bb >= b) return;
+  T t = 0;
+  for (int i = 0; i < per_b; ++i) t += part[(size_t)bb * per_b + i];
+  cost[bb] = t;
+}
+
+// grad1 partials: lanes over k, l split S ways: part[s][(bb*n + k)*3 + x].
+template <typename T>
+__global__ void __launch_bounds__(kThreads)
+    emd_grad1_kernel(const T* __restrict__ xyz1, const T* __restrict__ xyz2,
+                     const T* __restrict__ match, int b, int n, int m, int S,
+                     T* __restrict__ part) {
+  const int bb = blockIdx.z, s = blockIdx.y;
+  const int k = blockIdx.x * kThreads + threadIdx.x;
+  if (k >= n) return;
+  const T* p1 = xyz1 + ((size_t)bb * n + k) * 3;
+  const T x1 = p1[0], y1 = p1[1], z1 = p1[2];
+  const int l0 = (int)(((long long)m * s) / S), l1 = (int)(((long long)m * (s + 1)) / S);
+  const T* __restrict__ cb = xyz2 + (size_t)bb * m * 3;
+  T dx = 0, dy = 0, dz = 0;
+  for (int l = l0; l < l1; ++l) {
+    const T d = match[((size_t)bb * m + l) * n + k] * (T)2;
+    dx = fmaT<T>(x1 - cb[3 * l], d, dx);
+    dy = fmaT<T>(y1 - cb[3 * l + 1], d, dy);
+    dz = fmaT<T>(z1 - cb[3 * l + 2], d, dz);
+  }
+  T* o = part + (size_t)s * b * n * 3 + ((size_t)bb * n + k) * 3;
+  o[0] = dx;
+  o[1] = dy;
+  o[2] = dz;
+}
+
+template <typename T>
+__global__ void emd_grad1_fin_kernel(const T* __restrict__ part, int S, int b, int n,
+                                     const T* __restrict__ gcost, T* __restrict__ grad1) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t total = (size_t)b * n * 3;
+  if (i >= total) return;
+  const int bb = (int)(i / ((size_t)n * 3));
+  grad1[i] = sum_parts(part, S, total, i) * gcost[bb];
+}
+
+// grad2: one block per (l, b); lanes stride over k, block reduce (:285-323).
+template <typename T>
+__global__ void __launch_bounds__(kThreads)
+    emd_grad2_kernel(const T* __restrict__ xyz1, const T* __restrict__ xyz2,
+                     const T* __restrict__ match, const T* __restrict__ gcost, int n, int m,
+                     T* __restrict__ grad2) {
+  __shared__ T red[kThreads / 64];
+  const int l = blockIdx.x, bb = blockIdx.y;
+  const T* p2 = xyz2 + ((size_t)bb * m + l) * 3;
+  const T x2 = p2[0], y2 = p2[1], z2 = p2[2];
+  const T* __restrict__ row = match + ((size_t)bb * m + l) * n;
+  const T* __restrict__ pb = xyz1 + (size_t)bb * n * 3;
+  T sx = 0, sy = 0, sz = 0;
+  for (int k = threadIdx.x; k < n; k += kThreads) {
+    const T d = row[k] * (T)2;
+    sx = fmaT<T>(x2 - pb[3 * k], d, sx);
+    sy = fmaT<T>(y2 - pb[3 * k + 1], d, sy);
+    sz = fmaT<T>(z2 - pb[3 * k + 2], d, sz);
+  }
+  const T tx = block_sum(sx, red);
+  const T ty = block_sum(sy, red);
+  const T tz = block_sum(sz, red);
+  if (threadIdx.x == 0) {
+    const T g = gcost[bb];
+    T* o = grad2 + ((size_t)bb * m + l) * 3;
+    o[0] = tx * g;
+    o[1] = ty * g;
+    o[2] = tz * g;
+  }
+}
+
+int emd_splits(int b, int n, int m) {
+  const long long rows = (long long)b * std::max(n, m);
+  const long long want_lanes = 4LL * kCUs * 4 * 64;  // ~4 waves per SIMD
+  int s = (int)std::max(1LL, (want_lanes + rows - 1) / std::max(1LL, rows));
+  s = std::min(s, std::max(1, std::min(n, m) / 64));
+  return std::max(1, std::min(s, 32));
+}
+
+template <typename T>
+struct EmdWs {
+  T *remL, *remR, *ratL, *ratR, *levL, *levR, *part;
+};
+
+size_t emd_ws_elems(int b, int n, int m) {
+  const size_t bn = (size_t)b * n, bm = (size_t)b * m;
+  const int S = emd_splits(b, n, m);
+  const size_t part = std::max((size_t)S * b * std::max(n, m) * 3,
+                               (size_t)b * S * ceil_div(std::max(n, 1), kThreads));
+  return 2 * (bn + bm) + kLevels * (bn + bm) + part;
+}
+
+template <typename T>
+EmdWs<T> carve(void* ws, int b, int n, int m) {
+  const size_t bn = (size_t)b * n, bm = (size_t)b * m;
+  T* p = (T*)ws;
+  EmdWs<T> w;
+  w.remL = p;
+  p += bn;
+  w.remR = p;
+  p += bm;
+  w.ratL = p;
+  p += bn;
+  w.ratR = p;
+  p += bm;
+  w.levL = p;
+  p += kLevels * bn;
+  w.levR = p;
+  p += kLevels * bm;
+  w.part = p;
+  return w;
+}
+
+inline dim3 grid1d(size_t total, int threads = 256) {
+  return dim3(ceil_div((long long)std::max<size_t>(total, 1), threads));
+}
+
+template <typename T>
+int approxmatch(const T* xyz1, const T* xyz2, int b, int n, int m, T* match, void* ws,
+                size_t ws_bytes, hipStream_t st) {
+  PCFM_CHECK_ARG(b >= 0 && n >= 0 && m >= 0, "approxmatch: negative size");
+  PCFM_CHECK_ARG(ws_bytes >= emd_ws_elems(b, n, m) * sizeof(T),
+                 "approxmatch: workspace %zu < %zu bytes", ws_bytes,
+                 emd_ws_elems(b, n, m) * sizeof(T));
+  if (b == 0 || n == 0 || m == 0) return PCFM_OK;
+  EmdWs<T> w = carve<T>(ws, b, n, m);
+  const int S = emd_splits(b, n, m);
+  // multiL/multiR: integer ratio of the cloud sizes (:27-33)
+  const T multiL = n >= m ? (T)1 : (T)(m / n);
+  const T multiR = n >= m ? (T)(n / m) : (T)1;
+  const size_t bn = (size_t)b * n, bm = (size_t)b * m;
+  hipLaunchKernelGGL(emd_init_kernel<T>, grid1d(std::max(bn, bm)), dim3(256), 0, st, w.remL, bn,
+                     multiL, w.remR, bm, multiR);
+  const dim3 gL(ceil_div(n, kThreads), S, b), gR(ceil_div(m, kThreads), S, b);
+  for (int j = 0; j < kLevels; ++j) {
+    const T level = (T)h_levels[j];
+    // pass 1: rows = xyz1 (k), cols = xyz2 (l), coef = remainR
+    hipLaunchKernelGGL((emd_pass_kernel<T, 0>), gL, dim3(kThreads), 0, st, xyz1, n, xyz2, m, b,
+                       level, w.remR, (const T*)nullptr, S, w.part);
+    hipLaunchKernelGGL(emd_fin1_kernel<T>, grid1d(bn), dim3(256), 0, st, w.part, S, bn, w.remL,
+                       w.ratL);
+    // pass 2: rows = xyz2 (l), cols = xyz1 (k), coef = ratioL
+    hipLaunchKernelGGL((emd_pass_kernel<T, 1>), gR, dim3(kThreads), 0, st, xyz2, m, xyz1, n, b,
+                       level, w.ratL, (const T*)nullptr, S, w.part);
+    hipLaunchKernelGGL(emd_fin2_kernel<T>, grid1d(bm), dim3(256), 0, st, w.part, S, bm, w.remR,
+                       w.ratR, w.levR + (size_t)j * bm);
+    // pass 3: rows = xyz1 (k), cols = xyz2 (l), coef = ratioR, rowscale = ratioL
+    hipLaunchKernelGGL((emd_pass_kernel<T, 2>), gL, dim3(kThreads), 0, st, xyz1, n, xyz2, m, b,
+                       level, w.ratR, (const T*)w.ratL, S, w.part);
+    hipLaunchKernelGGL(emd_fin3_kernel<T>, grid1d(bn), dim3(256), 0, st, w.part, S, bn, w.remL,
+                       w.ratL, w.levL + (size_t)j * bn);
+  }
+  dim3 gm(ceil_div(n, kThreads), ceil_div(m, kLPer), b);
+  hipLaunchKernelGGL(emd_match_kernel<T>, gm, dim3(kThreads), 0, st, xyz1, xyz2, b, n, m, w.levL,
+                     w.levR, match);
+  return check_launch("approxmatch");
+}
+
+template <typename T>
+int matchcost(const T* xyz1, const T* xyz2, const T* match, int b, int n, int m, T* cost,
+              void* ws, size_t ws_bytes, hipStream_t st) {
+  PCFM_CHECK_ARG(b >= 0 && n >= 0 && m >= 0, "matchcost: negative size");
+  PCFM_CHECK_ARG(ws_bytes >= emd_ws_elems(b, n, m) * sizeof(T),
+                 "matchcost: workspace %zu < %zu bytes", ws_bytes,
+                 emd_ws_elems(b, n, m) * sizeof(T));
+  if (b == 0) return PCFM_OK;
+  if (n == 0 || m == 0) {
+    hipError_t e = hipMemsetAsync(cost, 0, (size_t)b * sizeof(T), st);
+    if (e != hipSuccess) {
+      set_error("matchcost: hipMemsetAsync: %s", hipGetErrorString(e));
+      return (int)e;
+    }
+    return PCFM_OK;
+  }
+  EmdWs<T> w = carve<T>(ws, b, n, m);
+  const int S = emd_splits(b, n, m);
+  dim3 g(ceil_div(n, kThreads), S, b);
+  hipLaunchKernelGGL(emd_cost_kernel<T>, g, dim3(kThreads), 0, st, xyz1, xyz2, match, b, n, m, S,
+                     w.part);
+  const int per_b = S * (int)g.x;
+  hipLaunchKernelGGL(emd_cost_fin_kernel<T>, grid1d(b, 64), dim3(64), 0, st, w.part, per_b, b,
+                     cost);
+  return check_launch("matchcost");
+}
+
+template <typename T>
+int matchcost_bwd(const T* gcost, const T* xyz1, const T* xyz2, const T* match, int b, int n,
+                  int m, T* grad1, T* grad2, void* ws, size_t ws_bytes, hipStream_t st) {
+  PCFM_CHECK_ARG(b >= 0 && n >= 0 && m >= 0, "matchcost_bwd: negative size");
+  PCFM_CHECK_ARG(ws_bytes >= emd_ws_elems(b, n, m) * sizeof(T),
+                 "matchcost_bwd: workspace %zu < %zu bytes", ws_bytes,
+                 emd_ws_elems(b, n, m) * sizeof(T));
+  if (b == 0) return PCFM_OK;
+  if (n == 0 || m == 0) {
+    hipError_t e = hipSuccess;
+    if (n) e = hipMemsetAsync(grad1, 0, (size_t)b * n * 3 * sizeof(T), st);
+    if (m && e == hipSuccess) e = hipMemsetAsync(grad2, 0, (size_t)b * m * 3 * sizeof(T), st);
+    if (e != hipSuccess) {
+      set_error("matchcost_bwd: hipMemsetAsync: %s", hipGetErrorString(e));
+      return (int)e;
+    }
+    return PCFM_OK;
+  }
+  EmdWs<T> w = carve<T>(ws, b, n, m);
+  const int S = emd_splits(b, n, m);
+  hipLaunchKernelGGL(emd_grad1_kernel<T>, dim3(ceil_div(n, kThreads), S, b), dim3(kThreads), 0,
+                     st, xyz1, xyz2, match, b, n, m, S, w.part);
+  hipLaunchKernelGGL(emd_grad1_fin_kernel<T>, grid1d((size_t)b * n * 3), dim3(256), 0, st,
+                     w.part, S, b, n, gcost, grad1);
+  hipLaunchKernelGGL(emd_grad2_kernel<T>, dim3(m, b), dim3(kThreads), 0, st, xyz1, xyz2, match,
+                     gcost, n, m, grad2);
+  return check_launch("matchcost_bwd");
+}
+
+}  // namespace
+}  // namespace pcfm
+
+using namespace pcfm;
+
+extern "C" size_t pcfm_emd_workspace_bytes(int b, int n, int m, int elem_bytes) {
+  if (b < 0 || n < 0 || m < 0 || (elem_bytes != 4 && elem_bytes != 8)) return 0;
+  return emd_ws_elems(b, n, m) * (size_t)elem_bytes;
+}
+
+extern "C" int pcfm_emd_approxmatch_f32(const float* xyz1, const float* xyz2, int b, int n, int m,
+                                        float* match, void* ws, size_t ws_bytes, void* stream) {
+  return approxmatch<float>(xyz1, xyz2, b, n, m, match, ws, ws_bytes, (hipStream_t)stream);
+}
+extern "C" int pcfm_emd_approxmatch_f64(const double* xyz1, const double* xyz2, int b, int n,
+                                        int m, double* match, void* ws, size_t ws_bytes,
+                                        void* stream) {
+  return approxmatch<double>(xyz1, xyz2, b, n, m, match, ws, ws_bytes, (hipStream_t)stream);
+}
+extern "C" int pcfm_emd_matchcost_f32(const float* xyz1, const float* xyz2, const float* match,
+                                      int b, int n, int m, float* cost, void* ws,
+                                      size_t ws_bytes, void* stream) {
+  return matchcost<float>(xyz1, xyz2, match, b, n, m, cost, ws, ws_bytes, (hipStream_t)stream);
+}
+extern "C" int pcfm_emd_matchcost_f64(const double* xyz1, const double* xyz2,
+                                      const double* match, int b, int n, int m, double* cost,
+                                      void* ws, size_t ws_bytes, void* stream) {
+  return matchcost<double>(xyz1, xyz2, match, b, n, m, cost, ws, ws_bytes, (hipStream_t)stream);
+}
+extern "C" int pcfm_emd_matchcost_bwd_f32(const float* grad_cost, const float* xyz1,
+                                          const float* xyz2, const float* match, int b, int n,
+                                          int m, float* grad1, float* grad2, void* ws,
+                                          size_t ws_bytes, void* stream) {
+  return matchcost_bwd<float>(grad_cost, xyz1, xyz2, match, b, n, m, grad1, grad2, ws, ws_bytes,
+                              (hipStream_t)stream);
+}
+extern "C" int pcfm_emd_matchcost_bwd_f64(const double* grad_cost, const double* xyz1,
+                                          const double* xyz2, const double* match, int b, int n,
+                                          int m, double* grad1, double* grad2, void* ws,
+                                          size_t ws_bytes, void* stream) {
+  return matchcost_bwd<double>(grad_cost, xyz1, xyz2, match, b, n, m, grad1, grad2, ws,
+                               ws_bytes, (hipStream_t)stream);
+}

@@ -1,0 +1,51 @@
+// Shared helpers for the gfx950 kernels behind include/pcfm.h.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstddef>
+#include <cstdint>
+#include <cstdio>
+
+#include "../../include/pcfm.h"
+
+namespace pcfm {
+
+// Thread-local last-error text (pcfm_last_error).
+void set_error(const char* fmt, ...);
+
+// Host-side argument check: returns PCFM_EINVAL with a message when !cond.
+#define PCFM_CHECK_ARG(cond, ...)            \
+  do {                                       \
+    if (!(cond)) {                           \
+      ::pcfm::set_error(__VA_ARGS__);        \
+      return PCFM_EINVAL;                    \
+    }                                        \
+  } while (0)
+
+// After a group of launches: map the sticky launch error to a return code.
+int check_launch(const char* what);
+
+// Every 64-bit index computation goes through size_t; kernels take int sizes
+// that fit the reference's own int arithmetic.
+inline int ceil_div(long long a, long long b) { return (int)((a + b - 1) / b); }
+
+constexpr int kCUs = 256;           // MI355X: 8 XCDs x 32 CUs
+constexpr int kLdsBytesMax = 160 * 1024;
+
+// Raise the dynamic-LDS cap of one kernel to the gfx950 maximum once.
+int allow_big_lds(const void* kernel);
+
+// Squared distance contract shared by every nearest-neighbour kernel and the
+// oracle: dx = q - p;  d = fma(dz, dz, fma(dx, dx, dy*dy)).
+// (This is how NVVM contracts the reference's `x*x + y*y + z*z`; pinned here
+// explicitly so the order does not depend on the compiler.)
+__device__ __forceinline__ float sqdist3(float dx, float dy, float dz) {
+  return __builtin_fmaf(dz, dz, __builtin_fmaf(dx, dx, dy * dy));
+}
+__device__ __forceinline__ double sqdist3(double dx, double dy, double dz) {
+  return __builtin_fma(dz, dz, __builtin_fma(dx, dx, dy * dy));
+}
+
+}  // namespace pcfm

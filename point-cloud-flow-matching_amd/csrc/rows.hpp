@@ -1,0 +1,378 @@
+// Row gather / row scatter engines shared by the voxel ops and grouping.
+//
+// Every PVConv scatter/gather in the reference is, for one (batch, channel),
+// a 1-D problem between a "row" of V cells (voxels r^3, or points n) and a list
+// of NI items (points, or grouped neighbours) with TAPS (index, weight) pairs
+// per item:
+//
+//   gather : out[b, c, i]  = sum_k w_k(i) * row[b, c, idx_k(i)]       (devox fwd, vox bwd, grouping fwd)
+//   scatter: row[b, c, v] += sum_{(i,k): idx_k(i)=v} w_k(i) * in[b, c, i]  (vox fwd, devox bwd, grouping bwd)
+//
+// The reference launches one block per batch element and walks points with a
+// channel loop inside (vox.cu:48-72, trilinear_devox.cu:21-162,
+// grouping.cu:18-77): 8 blocks on a 256-CU part, random 4-byte global gathers
+// and float atomics into HBM.  Here one block owns (batch, channel group,
+// cell chunk): the row segment lives in LDS (<= 128 KiB per block), so every
+// random access is an LDS access (ds_read / ds_add_f32), while HBM only sees
+// coalesced streams -- the item stream in, and the whole row out exactly once
+// (no torch::zeros pre-pass, no global atomics unless a row is split).
+#pragma once
+
+#include <algorithm>
+
+#include "pcfm_common.hpp"
+
+namespace pcfm {
+
+// ---------------------------------------------------------------------------
+// Index providers.  get(b, i, primary, id, w) fills TAPS (index, weight) pairs
+// for item i of batch b.  Out-of-range indices come back as (0, 0) so no
+// kernel can address outside its row; `primary` is true for exactly one block
+// column so providers with side outputs write them once.
+// ---------------------------------------------------------------------------
+
+// idx [b, ni] (+ optional weights [b, ni]); rows of length `nrows`.
+struct ProvIdx1 {
+  static constexpr int TAPS = 1;
+  const int* idx;
+  const float* w;  // nullptr -> weight 1
+  int ni;
+  int nrows;
+  __device__ __forceinline__ void get(int b, int i, bool, int (&id)[1], float (&wt)[1]) const {
+    const size_t o = (size_t)b * ni + i;
+    const int v = idx[o];
+    const bool ok = (unsigned)v < (unsigned)nrows;
+    id[0] = ok ? v : 0;
+    wt[0] = ok ? (w ? w[o] : 1.0f) : 0.0f;
+  }
+};
+
+// inds [b, 8, ni], wgts [b, 8, ni] as saved by the devoxelization forward.
+struct ProvIdx8 {
+  static constexpr int TAPS = 8;
+  const int* inds;
+  const float* wgts;
+  int ni;
+  int nrows;
+  __device__ __forceinline__ void get(int b, int i, bool, int (&id)[8], float (&wt)[8]) const {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const size_t o = ((size_t)b * 8 + k) * ni + i;
+      const int v = inds[o];
+      const bool ok = (unsigned)v < (unsigned)nrows;
+      id[k] = ok ? v : 0;
+      wt[k] = ok ? wgts[o] : 0.0f;
+    }
+  }
+};
+
+// Trilinear corners straight from float coords [b, 3, n] (values in [0, r-1]),
+// exactly as trilinear_devox.cu:37-75 computes them: weights are the products
+// dX*dY*dZ in that order, the hi offsets are added only when the fraction is
+// non-zero.  Optionally writes inds/wgts [b, 8, n] (training mode).
+struct ProvDevox {
+  static constexpr int TAPS = 8;
+  const float* coords;
+  int n, r, r2, r3;
+  int* inds_out;    // nullptr in eval mode
+  float* wgts_out;  // nullptr in eval mode
+  __device__ __forceinline__ void get(int b, int i, bool primary, int (&id)[8],
+                                      float (&wt)[8]) const {
+    const float* cb = coords + (size_t)b * 3 * n;
+    const float x = cb[i], y = cb[i + n], z = cb[i + 2 * n];
+    const float xl = floorf(x), yl = floorf(y), zl = floorf(z);
+    const float x1 = x - xl, y1 = y - yl, z1 = z - zl;
+    const float x0 = 1.0f - x1, y0 = 1.0f - y1, z0 = 1.0f - z1;
+    wt[0] = x0 * y0 * z0;
+    wt[1] = x0 * y0 * z1;
+    wt[2] = x0 * y1 * z0;
+    wt[3] = x0 * y1 * z1;
+    wt[4] = x1 * y0 * z0;
+    wt[5] = x1 * y0 * z1;
+    wt[6] = x1 * y1 * z0;
+    wt[7] = x1 * y1 * z1;
+    const int xh = (x1 > 0.0f) ? r2 : 0;
+    const int yh = (y1 > 0.0f) ? r : 0;
+    const int zh = (z1 > 0.0f) ? 1 : 0;
+    const int base = (int)xl * r2 + (int)yl * r + (int)zl;
+    id[0] = base;
+    id[1] = base + zh;
+    id[2] = base + yh;
+    id[3] = base + yh + zh;
+    id[4] = base + xh;
+    id[5] = base + xh + zh;
+    id[6] = base + xh + yh;
+    id[7] = base + xh + yh + zh;
+    if (primary && inds_out != nullptr) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const size_t o = ((size_t)b * 8 + k) * n + i;
+        inds_out[o] = id[k];
+        wgts_out[o] = wt[k];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const bool ok = (unsigned)id[k] < (unsigned)r3;
+      wt[k] = ok ? wt[k] : 0.0f;
+      id[k] = ok ? id[k] : 0;
+    }
+  }
+};
+
+// Voxelization backward: one tap, weight (float)(1.0 / (double)cnt[v]) exactly
+// as vox.cu:104 (the reference divides in double, then rounds to float).
+struct ProvVoxBwd {
+  static constexpr int TAPS = 1;
+  const int* ind;  // [b, n]
+  const int* cnt;  // [b, s]
+  int n, s;
+  __device__ __forceinline__ void get(int b, int i, bool, int (&id)[1], float (&wt)[1]) const {
+    const int v = ind[(size_t)b * n + i];
+    const int c = ((unsigned)v < (unsigned)s) ? cnt[(size_t)b * s + v] : 0;
+    id[0] = c > 0 ? v : 0;
+    wt[0] = c > 0 ? (float)(1.0 / (double)c) : 0.0f;
+  }
+};
+
+// ---------------------------------------------------------------------------
+// Kernels
+// ---------------------------------------------------------------------------
+
+// Sum of TAPS weighted row reads in the reference's contraction order:
+// a = w1*f1; a = fma(w0, f0, a); a = fma(wk, fk, a) for k = 2..TAPS-1.
+template <int T>
+__device__ __forceinline__ float tap_sum(const float* __restrict__ s, const int (&id)[T],
+                                         const float (&w)[T]) {
+  if constexpr (T == 1) {
+    return s[id[0]] * w[0];
+  } else {
+    float a = w[1] * s[id[1]];
+    a = __builtin_fmaf(w[0], s[id[0]], a);
+#pragma unroll
+    for (int k = 2; k < T; ++k) a = __builtin_fmaf(w[k], s[id[k]], a);
+    return a;
+  }
+}
+
+// grid = (item splits, channel groups, b).  USE_LDS stages the block's
+// `cpb` rows (cpb * V floats) in LDS first.
+template <class Prov, bool USE_LDS>
+__global__ void __launch_bounds__(1024)
+    gather_rows_kernel(const float* __restrict__ rows, float* __restrict__ out, int C, int V,
+                       int NI, int cpb, Prov prov) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  constexpr int T = Prov::TAPS;
+  const int b = blockIdx.z;
+  const int c0 = blockIdx.y * cpb;
+  const int nc = min(cpb, C - c0);
+  const float* __restrict__ rb = rows + ((size_t)b * C + c0) * V;
+  if constexpr (USE_LDS) {
+    const int total = nc * V;
+    if ((((uintptr_t)rb) & 15) == 0 && (total & 3) == 0) {
+      const float4* __restrict__ s4 = reinterpret_cast<const float4*>(rb);
+      float4* d4 = reinterpret_cast<float4*>(lds);
+      for (int e = threadIdx.x; e < (total >> 2); e += blockDim.x) d4[e] = s4[e];
+    } else {
+      for (int e = threadIdx.x; e < total; e += blockDim.x) lds[e] = rb[e];
+    }
+    __syncthreads();
+  }
+  float* __restrict__ ob = out + ((size_t)b * C + c0) * NI;
+  const bool primary = blockIdx.y == 0;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < NI; i += gridDim.x * blockDim.x) {
+    int id[T];
+    float w[T];
+    prov.get(b, i, primary, id, w);
+    for (int cc = 0; cc < nc; ++cc) {
+      float acc;
+      if constexpr (USE_LDS) {
+        acc = tap_sum<T>(lds + (size_t)cc * V, id, w);
+      } else {
+        acc = tap_sum<T>(rb + (size_t)cc * V, id, w);
+      }
+      ob[(size_t)cc * NI + i] = acc;
+    }
+  }
+}
+
+// grid = (cell chunks * item splits, channel groups, b).  The block's row
+// segments [v0, v0 + vlen) of `cpb` channels accumulate in LDS (ds_add_f32),
+// then go to HBM once: plain stores when the block owns the whole item range
+// (psplit == 1), global atomics into a zeroed row otherwise.
+template <class Prov>
+__global__ void __launch_bounds__(1024)
+    scatter_rows_kernel(const float* __restrict__ in, float* __restrict__ rows, int C, int V,
+                        int NI, int cpb, int vchunk, int nvchunk, int psplit, Prov prov) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  constexpr int T = Prov::TAPS;
+  const int b = blockIdx.z;
+  const int c0 = blockIdx.y * cpb;
+  const int nc = min(cpb, C - c0);
+  const int vc = blockIdx.x % nvchunk;
+  const int ps = blockIdx.x / nvchunk;
+  const int v0 = vc * vchunk;
+  const int vlen = min(vchunk, V - v0);
+  for (int e = threadIdx.x; e < nc * vchunk; e += blockDim.x) lds[e] = 0.0f;
+  __syncthreads();
+  const int i0 = (int)(((long long)NI * ps) / psplit);
+  const int i1 = (int)(((long long)NI * (ps + 1)) / psplit);
+  const float* __restrict__ ib = in + ((size_t)b * C + c0) * NI;
+  for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+    int id[T];
+    float w[T];
+    prov.get(b, i, false, id, w);
+    unsigned rel[T];
+#pragma unroll
+    for (int k = 0; k < T; ++k) rel[k] = (unsigned)(id[k] - v0);
+    for (int cc = 0; cc < nc; ++cc) {
+      const float g = ib[(size_t)cc * NI + i];
+      float* lrow = lds + cc * vchunk;
+#pragma unroll
+      for (int k = 0; k < T; ++k) {
+        if (rel[k] < (unsigned)vlen) atomicAdd(lrow + rel[k], w[k] * g);
+      }
+    }
+  }
+  __syncthreads();
+  float* __restrict__ ob = rows + ((size_t)b * C + c0) * V + v0;
+  for (int cc = 0; cc < nc; ++cc) {
+    const float* lrow = lds + cc * vchunk;
+    float* orow = ob + (size_t)cc * V;
+    if (psplit == 1) {
+      for (int o = threadIdx.x; o < vlen; o += blockDim.x) orow[o] = lrow[o];
+    } else {
+      for (int o = threadIdx.x; o < vlen; o += blockDim.x) {
+        const float val = lrow[o];
+        if (val != 0.0f) atomicAdd(orow + o, val);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Launch planning
+// ---------------------------------------------------------------------------
+
+struct RowPlan {
+  int threads = 512;
+  int cpb = 1;       // channels per block
+  int groups = 1;    // ceil(C / cpb), at least 1
+  int vchunk = 0;    // scatter: LDS row segment length
+  int nvchunk = 1;   // scatter: segments per row
+  int psplit = 1;    // item splits (grid.x multiplier)
+  bool use_lds = true;
+  size_t lds_bytes = 0;
+};
+
+constexpr int kTargetBlocks = 1024;         // 4 per CU
+constexpr int kLdsFloatsSmall = 16 * 1024;  // 64 KiB: 2 blocks of 512 threads per CU
+constexpr int kLdsFloatsBig = 32 * 1024;    // 128 KiB: 1 block of 1024 threads per CU
+
+inline RowPlan plan_gather(int B, int C, int V, int NI) {
+  RowPlan p;
+  if ((long long)V <= kLdsFloatsSmall) {
+    p.threads = 512;
+    p.cpb = std::max(1, std::min(C, kLdsFloatsSmall / std::max(V, 1)));
+  } else if ((long long)V <= kLdsFloatsBig) {
+    p.threads = 1024;
+    p.cpb = 1;
+  } else {
+    p.use_lds = false;
+    p.threads = 256;
+    p.cpb = std::max(1, std::min(C, 4));
+  }
+  auto groups = [&](int cpb) { return std::max(1, ceil_div(C, cpb)); };
+  while (p.cpb > 1 && (long long)groups(p.cpb) * B < kTargetBlocks) p.cpb = (p.cpb + 1) / 2;
+  p.groups = groups(p.cpb);
+  const long long blocks = (long long)p.groups * B;
+  if (blocks < kTargetBlocks) {
+    const int want = ceil_div(kTargetBlocks, blocks);
+    const int cap = std::max(1, ceil_div(NI, p.threads));
+    p.psplit = std::min(want, cap);
+  }
+  p.lds_bytes = p.use_lds ? (size_t)p.cpb * V * sizeof(float) : 0;
+  return p;
+}
+
+inline RowPlan plan_scatter(int B, int C, int V, int NI) {
+  RowPlan p;
+  if ((long long)V <= kLdsFloatsSmall) {
+    p.threads = 512;
+    p.vchunk = std::max(V, 1);
+    p.cpb = std::max(1, std::min(C, kLdsFloatsSmall / p.vchunk));
+  } else if ((long long)V <= kLdsFloatsBig) {
+    p.threads = 1024;
+    p.vchunk = V;
+    p.cpb = 1;
+  } else {
+    p.threads = 1024;
+    p.vchunk = kLdsFloatsBig;
+    p.cpb = 1;
+  }
+  p.nvchunk = std::max(1, ceil_div(V, p.vchunk));
+  auto groups = [&](int cpb) { return std::max(1, ceil_div(C, cpb)); };
+  while (p.cpb > 1 && (long long)groups(p.cpb) * p.nvchunk * B < kTargetBlocks)
+    p.cpb = (p.cpb + 1) / 2;
+  p.groups = groups(p.cpb);
+  const long long blocks = (long long)p.groups * p.nvchunk * B;
+  if (blocks < kTargetBlocks) {
+    const int want = ceil_div(kTargetBlocks, blocks);
+    const int cap = std::max(1, NI / 2048);
+    p.psplit = std::min(want, cap);
+  }
+  p.lds_bytes = (size_t)p.cpb * p.vchunk * sizeof(float);
+  return p;
+}
+
+template <class Prov>
+inline bool prov_has_side_outputs(const Prov&) { return false; }
+inline bool prov_has_side_outputs(const ProvDevox& p) { return p.inds_out != nullptr; }
+
+template <class Prov>
+inline int launch_gather(const float* rows, float* out, int B, int C, int V, int NI, Prov prov,
+                         hipStream_t st, const char* what) {
+  if (B == 0 || NI == 0) return PCFM_OK;
+  if (V == 0 && C > 0) {  // empty rows: every tap is out of range -> zeros
+    hipError_t e = hipMemsetAsync(out, 0, (size_t)B * C * NI * sizeof(float), st);
+    if (e != hipSuccess) {
+      set_error("%s: hipMemsetAsync: %s", what, hipGetErrorString(e));
+      return (int)e;
+    }
+    if (!prov_has_side_outputs(prov)) return PCFM_OK;
+  }
+  RowPlan p = plan_gather(B, C, V, NI);
+  dim3 grid(p.psplit, p.groups, B);
+  if (p.use_lds) {
+    int e = allow_big_lds((const void*)gather_rows_kernel<Prov, true>);
+    if (e) return e;
+    hipLaunchKernelGGL((gather_rows_kernel<Prov, true>), grid, dim3(p.threads), p.lds_bytes, st,
+                       rows, out, C, V, NI, p.cpb, prov);
+  } else {
+    hipLaunchKernelGGL((gather_rows_kernel<Prov, false>), grid, dim3(p.threads), 0, st, rows,
+                       out, C, V, NI, p.cpb, prov);
+  }
+  return check_launch(what);
+}
+
+template <class Prov>
+inline int launch_scatter(const float* in, float* rows, int B, int C, int V, int NI, Prov prov,
+                          hipStream_t st, const char* what) {
+  if (B == 0 || C == 0 || V == 0) return PCFM_OK;
+  RowPlan p = plan_scatter(B, C, V, NI);
+  if (p.psplit > 1) {
+    hipError_t e = hipMemsetAsync(rows, 0, (size_t)B * C * V * sizeof(float), st);
+    if (e != hipSuccess) {
+      set_error("%s: hipMemsetAsync: %s", what, hipGetErrorString(e));
+      return (int)e;
+    }
+  }
+  int e = allow_big_lds((const void*)scatter_rows_kernel<Prov>);
+  if (e) return e;
+  dim3 grid(p.nvchunk * p.psplit, p.groups, B);
+  hipLaunchKernelGGL((scatter_rows_kernel<Prov>), grid, dim3(p.threads), p.lds_bytes, st, in,
+                     rows, C, V, NI, p.cpb, p.vchunk, p.nvchunk, p.psplit, prov);
+  return check_launch(what);
+}
+
+}  // namespace pcfm

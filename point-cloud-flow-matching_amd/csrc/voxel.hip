@@ -1,0 +1,117 @@
+// PVConv voxel path: average voxelization and trilinear devoxelization,
+// forward and backward (include/pcfm.h).
+//
+// Reference semantics: third_party/pvcnn/modules/functional/src/voxelization/
+// vox.cu:18-126 and src/interpolate/trilinear_devox.cu:21-162.
+#include "rows.hpp"
+
+namespace pcfm {
+namespace {
+
+// ind[b, i] = x*r^2 + y*r + z (vox.cu:31) and the per-voxel histogram (integer
+// atomics: the counts are exact and order-free).  One thread per point, the
+// whole B*N range at once instead of one block per batch element.
+__global__ void __launch_bounds__(256)
+    vox_count_kernel(const int* __restrict__ coords, int n, int r, int s, int* __restrict__ ind,
+                     int* __restrict__ cnt) {
+  const int b = blockIdx.y;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int* cb = coords + (size_t)b * 3 * n;
+  const int v = cb[i] * r * r + cb[i + n] * r + cb[i + 2 * n];
+  ind[(size_t)b * n + i] = v;
+  if ((unsigned)v < (unsigned)s) atomicAdd(cnt + (size_t)b * s + v, 1);
+}
+
+// Per-point scale 1/cnt, computed once per point instead of once per
+// (point, channel block): (float)(1.0 / (double)cnt) as vox.cu:66.
+__global__ void __launch_bounds__(256)
+    vox_inv_kernel(const int* __restrict__ ind, const int* __restrict__ cnt, int n, int s,
+                   float* __restrict__ inv) {
+  const int b = blockIdx.y;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int v = ind[(size_t)b * n + i];
+  const int c = ((unsigned)v < (unsigned)s) ? cnt[(size_t)b * s + v] : 0;
+  inv[(size_t)b * n + i] = c > 0 ? (float)(1.0 / (double)c) : 0.0f;
+}
+
+bool cube_fits(int r, int* s) {
+  if (r < 1) return false;
+  const long long c = (long long)r * r * r;
+  if (c > (1LL << 30)) return false;
+  *s = (int)c;
+  return true;
+}
+
+}  // namespace
+}  // namespace pcfm
+
+using namespace pcfm;
+
+extern "C" size_t pcfm_avg_voxelize_fwd_workspace_bytes(int b, int n) {
+  if (b < 0 || n < 0) return 0;
+  return (size_t)b * n * sizeof(float);
+}
+
+extern "C" int pcfm_avg_voxelize_fwd(const float* feat, const int* coords, int b, int c, int n,
+                                     int r, float* out, int* ind, int* cnt, void* ws,
+                                     size_t ws_bytes, void* stream) {
+  int s = 0;
+  PCFM_CHECK_ARG(b >= 0 && c >= 0 && n >= 0, "avg_voxelize_fwd: negative size b=%d c=%d n=%d",
+                 b, c, n);
+  PCFM_CHECK_ARG(cube_fits(r, &s), "avg_voxelize_fwd: bad resolution %d", r);
+  PCFM_CHECK_ARG(ws_bytes >= pcfm_avg_voxelize_fwd_workspace_bytes(b, n),
+                 "avg_voxelize_fwd: workspace %zu < %zu bytes", ws_bytes,
+                 pcfm_avg_voxelize_fwd_workspace_bytes(b, n));
+  if (b == 0) return PCFM_OK;
+  hipStream_t st = (hipStream_t)stream;
+  hipError_t he = hipMemsetAsync(cnt, 0, (size_t)b * s * sizeof(int), st);
+  if (he != hipSuccess) {
+    set_error("avg_voxelize_fwd: hipMemsetAsync: %s", hipGetErrorString(he));
+    return (int)he;
+  }
+  float* inv = (float*)ws;
+  if (n > 0) {
+    dim3 grid(ceil_div(n, 256), b);
+    hipLaunchKernelGGL(vox_count_kernel, grid, dim3(256), 0, st, coords, n, r, s, ind, cnt);
+    hipLaunchKernelGGL(vox_inv_kernel, grid, dim3(256), 0, st, ind, cnt, n, s, inv);
+    int e = check_launch("avg_voxelize_fwd(count)");
+    if (e) return e;
+  }
+  // out[c, v] = sum_i feat[c, i] * inv[i]   (the reference's per-term product, vox.cu:68)
+  return launch_scatter(feat, out, b, c, s, n, ProvIdx1{ind, inv, n, s}, st,
+                        "avg_voxelize_fwd(scatter)");
+}
+
+extern "C" int pcfm_avg_voxelize_bwd(const float* grad_y, const int* ind, const int* cnt, int b,
+                                     int c, int n, int s, float* grad_x, void* stream) {
+  PCFM_CHECK_ARG(b >= 0 && c >= 0 && n >= 0 && s >= 0,
+                 "avg_voxelize_bwd: negative size b=%d c=%d n=%d s=%d", b, c, n, s);
+  if (c == 0) return PCFM_OK;
+  return launch_gather(grad_y, grad_x, b, c, s, n, ProvVoxBwd{ind, cnt, n, s},
+                       (hipStream_t)stream, "avg_voxelize_bwd");
+}
+
+extern "C" int pcfm_trilinear_devoxelize_fwd(const float* coords, const float* feat, int b, int c,
+                                             int n, int r, int training, float* out, int* inds,
+                                             float* wgts, void* stream) {
+  int s = 0;
+  PCFM_CHECK_ARG(b >= 0 && c >= 0 && n >= 0, "trilinear_devoxelize_fwd: negative size");
+  PCFM_CHECK_ARG(cube_fits(r, &s), "trilinear_devoxelize_fwd: bad resolution %d", r);
+  PCFM_CHECK_ARG(!training || (inds != nullptr && wgts != nullptr),
+                 "trilinear_devoxelize_fwd: training needs inds/wgts buffers");
+  ProvDevox prov{coords, n, r, r * r, s, training ? inds : nullptr, training ? wgts : nullptr};
+  return launch_gather(feat, out, b, c, s, n, prov, (hipStream_t)stream,
+                       "trilinear_devoxelize_fwd");
+}
+
+extern "C" int pcfm_trilinear_devoxelize_bwd(const float* grad_y, const int* inds,
+                                             const float* wgts, int b, int c, int n, int r,
+                                             float* grad_x, void* stream) {
+  int s = 0;
+  PCFM_CHECK_ARG(b >= 0 && c >= 0 && n >= 0, "trilinear_devoxelize_bwd: negative size");
+  PCFM_CHECK_ARG(cube_fits(r, &s), "trilinear_devoxelize_bwd: bad resolution %d", r);
+  return launch_scatter(grad_y, grad_x, b, c, s, n, ProvIdx8{inds, wgts, n, s},
+                        (hipStream_t)stream, "trilinear_devoxelize_bwd");
+}

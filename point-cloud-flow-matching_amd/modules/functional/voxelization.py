@@ -1,0 +1,33 @@
+"""avg_voxelize: autograd wrapper of the voxelization kernels.
+
+Reference: third_party/pvcnn/modules/functional/voxelization.py:8-40.
+"""
+from torch.autograd import Function
+
+from modules.functional import backend as _be
+
+__all__ = ["avg_voxelize"]
+
+
+class AvgVoxelization(Function):
+    """features f32 [B, C, N], coords i32 [B, 3, N] -> f32 [B, C, R, R, R]."""
+
+    @staticmethod
+    def forward(ctx, features, coords, resolution):
+        feats = features.contiguous()
+        vox = coords.int().contiguous()
+        b, c = feats.shape[0], feats.shape[1]
+        r = int(resolution)
+        grid, ind, cnt = _be._backend.avg_voxelize_forward(feats, vox, r)
+        ctx.save_for_backward(ind, cnt)
+        return grid.view(b, c, r, r, r)
+
+    @staticmethod
+    def backward(ctx, grad_output):
+        ind, cnt = ctx.saved_tensors
+        b, c = grad_output.shape[0], grad_output.shape[1]
+        flat = grad_output.contiguous().view(b, c, -1)
+        return _be._backend.avg_voxelize_backward(flat, ind, cnt), None, None
+
+
+avg_voxelize = AvgVoxelization.apply

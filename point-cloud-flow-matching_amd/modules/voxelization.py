@@ -1,0 +1,40 @@
+"""Voxelization module: point coords -> voxel grid of averaged features.
+
+Reference: third_party/pvcnn/modules/voxelization.py:8-28.  The coordinate
+normalisation is the reference's exact sequence of torch ops (mean-centre,
+scale by 2*max radius + eps, shift to [0,1], scale to [0, r-1], round
+half-to-even), so voxel assignment is identical; the pooling itself runs in the
+gfx950 scatter kernel (modules.functional.avg_voxelize).
+"""
+import torch
+import torch.nn as nn
+
+import modules.functional as F
+
+__all__ = ["Voxelization"]
+
+
+class Voxelization(nn.Module):
+    def __init__(self, resolution, normalize=True, eps=0):
+        super().__init__()
+        self.r = int(resolution)
+        self.normalize = normalize
+        self.eps = eps
+
+    def _grid_coords(self, coords: torch.Tensor) -> torch.Tensor:
+        centred = coords - coords.mean(2, keepdim=True)
+        if self.normalize:
+            radius = centred.norm(dim=1, keepdim=True).max(dim=2, keepdim=True).values
+            unit = centred / (radius * 2.0 + self.eps) + 0.5
+        else:
+            unit = (centred + 1) / 2.0
+        return torch.clamp(unit * self.r, 0, self.r - 1)
+
+    def forward(self, features, coords):
+        norm_coords = self._grid_coords(coords.detach())
+        vox_coords = torch.round(norm_coords).to(torch.int32)
+        return F.avg_voxelize(features, vox_coords, self.r), norm_coords
+
+    def extra_repr(self):
+        tail = f", normalized eps = {self.eps}" if self.normalize else ""
+        return f"resolution={self.r}{tail}"

@@ -1,0 +1,91 @@
+"""ctypes binding of the C ABI in include/pcfm.h (libpcfm_hip.so, gfx950).
+
+The library is built in-tree by ``__graft_entry__.build()`` (``make -C
+point-cloud-flow-matching_amd/csrc``).  There is no CPU implementation behind
+this module: if the library is missing, or a tensor is not on a HIP device,
+every op raises -- exactly like the reference backend, which only accepts CUDA
+tensors (third_party/pvcnn/modules/functional/src/utils.hpp:7-18).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "csrc", "libpcfm_hip.so")
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_F = ctypes.c_float
+_Z = ctypes.c_size_t
+
+# name -> (restype, argtypes); must list every symbol of include/pcfm.h.
+SIGNATURES = {
+    "pcfm_abi_version": (_I, []),
+    "pcfm_last_error": (ctypes.c_char_p, []),
+    "pcfm_avg_voxelize_fwd_workspace_bytes": (_Z, [_I, _I]),
+    "pcfm_avg_voxelize_fwd": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _Z, _P]),
+    "pcfm_avg_voxelize_bwd": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P]),
+    "pcfm_trilinear_devoxelize_fwd": (_I, [_P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P]),
+    "pcfm_trilinear_devoxelize_bwd": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P]),
+    "pcfm_ball_query": (_I, [_P, _P, _I, _I, _I, _F, _I, _P, _P]),
+    "pcfm_grouping_fwd": (_I, [_P, _P, _I, _I, _I, _I, _I, _P, _P]),
+    "pcfm_grouping_bwd": (_I, [_P, _P, _I, _I, _I, _I, _I, _P, _P]),
+    "pcfm_chamfer_workspace_bytes": (_Z, [_I, _I, _I]),
+    "pcfm_chamfer_fwd": (_I, [_P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _Z, _P]),
+    "pcfm_chamfer_bwd": (_I, [_P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P]),
+    "pcfm_emd_workspace_bytes": (_Z, [_I, _I, _I, _I]),
+    "pcfm_emd_approxmatch_f32": (_I, [_P, _P, _I, _I, _I, _P, _P, _Z, _P]),
+    "pcfm_emd_approxmatch_f64": (_I, [_P, _P, _I, _I, _I, _P, _P, _Z, _P]),
+    "pcfm_emd_matchcost_f32": (_I, [_P, _P, _P, _I, _I, _I, _P, _P, _Z, _P]),
+    "pcfm_emd_matchcost_f64": (_I, [_P, _P, _P, _I, _I, _I, _P, _P, _Z, _P]),
+    "pcfm_emd_matchcost_bwd_f32": (_I, [_P, _P, _P, _P, _I, _I, _I, _P, _P, _P, _Z, _P]),
+    "pcfm_emd_matchcost_bwd_f64": (_I, [_P, _P, _P, _P, _I, _I, _I, _P, _P, _P, _Z, _P]),
+}
+
+ABI_VERSION = 1
+
+_lock = threading.Lock()
+_lib = None
+
+
+class PcfmError(RuntimeError):
+    """A pcfm_* entry point returned a non-zero status."""
+
+
+def load() -> ctypes.CDLL:
+    """Load libpcfm_hip.so once and declare every signature.  Raises if absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise RuntimeError(
+                    f"pcfm: HIP library {LIB_PATH} is not built; run "
+                    "`python -c 'import __graft_entry__ as g; g.build()'` "
+                    "(there is no CPU fallback)")
+            lib = ctypes.CDLL(LIB_PATH)
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(lib, name)
+                fn.restype = res
+                fn.argtypes = args
+            v = lib.pcfm_abi_version()
+            if v != ABI_VERSION:
+                raise RuntimeError(f"pcfm: ABI version {v} != expected {ABI_VERSION}; rebuild")
+            _lib = lib
+    return _lib
+
+
+def call(name: str, *args) -> None:
+    """Call pcfm_<name>; raise PcfmError with the library's message on failure."""
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    if rc != 0:
+        msg = lib.pcfm_last_error().decode(errors="replace")
+        raise PcfmError(f"{name} failed (status {rc}): {msg}")
+
+
+def query(name: str, *args) -> int:
+    return int(getattr(load(), name)(*args))

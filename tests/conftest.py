@@ -1,0 +1,48 @@
+"""Test configuration.
+
+* `gpu` marker: needs a HIP device (MI355X); everything else runs on the CPU.
+* The package directory point-cloud-flow-matching_amd/ is put on sys.path the
+  way the reference puts third_party/pvcnn on it (models.py:9-13).
+* `oracle_backend` fixture: CPU tests swap the C oracle in behind
+  modules.functional (the product itself has no CPU path).
+"""
+import os
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(REPO, "point-cloud-flow-matching_amd")
+GOLDEN = os.path.join(REPO, "tests", "golden")
+for p in (REPO, PKG):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a HIP GPU (MI355X); run with -m gpu")
+
+
+@pytest.fixture
+def oracle_backend(monkeypatch):
+    from oracle.oracle import TorchBackend
+    import modules.functional.backend as be
+    monkeypatch.setattr(be, "_backend", TorchBackend())
+    return be._backend
+
+
+@pytest.fixture(scope="session")
+def golden():
+    import numpy as np
+
+    def load(name):
+        return np.load(os.path.join(GOLDEN, name), allow_pickle=False)
+    return load
+
+
+def have_gpu():
+    try:
+        import torch
+        return torch.cuda.is_available()
+    except Exception:
+        return False

@@ -1,0 +1,77 @@
+"""The drop-in `modules` package and the flow models against goldens produced by
+the reference's own Python (tests/golden/make_golden.py), on the CPU with the
+oracle swapped in behind modules.functional (fixture `oracle_backend`)."""
+import numpy as np
+import pytest
+import torch
+
+
+def _param_sums(module):
+    return np.array([p.detach().double().sum().item() for _, p in module.named_parameters()])
+
+
+def test_pvconv_matches_reference(oracle_backend, golden):
+    from modules.pvconv import PVConv
+    g = golden("pvconv_r8.npz")
+    torch.set_num_threads(1)
+    torch.manual_seed(int(g["seed"]))
+    blk = PVConv(16, 16, kernel_size=3, resolution=8, with_se=True, normalize=True, eps=1e-6)
+    # same creation order -> same initial weights from the same seed
+    np.testing.assert_array_equal(_param_sums(blk), g["param_sums"])
+    feats = torch.from_numpy(g["feats"]).requires_grad_(True)
+    out, _ = blk((feats, torch.from_numpy(g["coords"])))
+    np.testing.assert_allclose(out.detach().numpy(), g["out"], rtol=1e-5, atol=1e-6)
+    loss = (out * torch.linspace(-1, 1, out.numel()).view_as(out)).sum()
+    loss.backward()
+    np.testing.assert_allclose(feats.grad.numpy(), g["grad_feats"], rtol=1e-4, atol=1e-6)
+    # conv biases feeding a BatchNorm have analytically zero gradient: their sums are
+    # pure rounding noise (|x| < 1e-3), hence the absolute floor
+    got = np.array([p.grad.double().sum().item() for p in blk.parameters()])
+    np.testing.assert_allclose(got, g["grad_sums"], rtol=1e-4, atol=1e-3)
+
+
+def test_state_dict_keys_match_reference_layout():
+    from modules.pvconv import PVConv
+    keys = set(PVConv(8, 8, 3, 4, with_se=True).state_dict())
+    for k in ("voxel_layers.0.weight", "voxel_layers.1.running_mean", "voxel_layers.3.weight",
+              "voxel_layers.4.bias", "voxel_layers.6.fc.0.weight", "voxel_layers.6.fc.2.weight",
+              "point_features.layers.0.weight", "point_features.layers.1.weight"):
+        assert k in keys, k
+
+
+@pytest.mark.parametrize("film_per_point", [True, False])
+def test_hybrid_matches_reference(oracle_backend, golden, film_per_point):
+    from pcfm.models import HybridMLP
+    g = golden("model_hybrid_c1.npz")
+    torch.set_num_threads(1)
+    torch.manual_seed(int(g["seed"]))
+    pf = HybridMLP(cond_dim=129, point_dim=6, film_per_point=film_per_point)
+    pf.train()
+    names = [n for n, _ in pf.named_parameters()]
+    assert names == list(g["param_names"])
+    np.testing.assert_array_equal(_param_sums(pf), g["param_sums"])
+    v = pf(torch.from_numpy(g["x"]), torch.from_numpy(g["t"]), torch.from_numpy(g["cond"]),
+           cond_drop_mask=torch.from_numpy(g["mask"]))
+    np.testing.assert_allclose(v.detach().numpy(), g["v"], rtol=1e-4, atol=1e-5)
+    loss = torch.nn.functional.mse_loss(v, torch.from_numpy(g["target"]))
+    np.testing.assert_allclose(loss.item(), float(g["loss"]), rtol=1e-5)
+    loss.backward()
+    norms = np.array([p.grad.double().norm().item() if p.grad is not None else 0.0
+                      for p in pf.parameters()])
+    np.testing.assert_allclose(norms, g["grad_norms"], rtol=2e-3, atol=1e-6)
+
+
+def test_product_ops_refuse_cpu_tensors():
+    """No CPU path: the product raises like the reference's CHECK_CUDA."""
+    from pcfm import ops
+    x = torch.zeros(1, 4, 10)
+    with pytest.raises(RuntimeError, match="must be a CUDA tensor"):
+        ops.avg_voxelize_forward(x, torch.zeros(1, 3, 10, dtype=torch.int32), 2)
+    with pytest.raises(RuntimeError, match="must be a CUDA tensor"):
+        ops.trilinear_devoxelize_forward(2, True, torch.zeros(1, 3, 10), torch.zeros(1, 4, 8))
+    with pytest.raises(NotImplementedError):
+        ops.backend.furthest_point_sampling(x, 3)
+    from chamfer3D.dist_chamfer_3D import chamfer_3D
+    d = torch.zeros(1, 10)
+    i = torch.zeros(1, 10, dtype=torch.int32)
+    assert chamfer_3D.forward(torch.zeros(1, 10, 3), torch.zeros(1, 10, 3), d, d, i, i) == 0
