@@ -44,8 +44,8 @@ const char* pcfm_last_error(void);
  * PVConv voxel path
  * ---------------------------------------------------------------------- */
 
-/* Scratch bytes pcfm_avg_voxelize_fwd needs for (b, n). */
-size_t pcfm_avg_voxelize_fwd_workspace_bytes(int b, int n);
+/* Scratch bytes pcfm_avg_voxelize_fwd needs for (b, c, n, r). */
+size_t pcfm_avg_voxelize_fwd_workspace_bytes(int b, int c, int n, int r);
 
 /* Average-pool voxelization, forward.
  * Replaces avg_voxelize_forward (third_party/pvcnn/modules/functional/src/
@@ -76,13 +76,16 @@ int pcfm_trilinear_devoxelize_fwd(const float* coords, const float* feat, int b,
                                   int n, int r, int training, float* out, int* inds,
                                   float* wgts, void* stream);
 
+size_t pcfm_trilinear_devoxelize_bwd_workspace_bytes(int b, int c, int n, int r);
+
 /* Trilinear devoxelization, backward.
  * Replaces trilinear_devoxelize_backward (trilinear_devox.cpp:67-91) ->
  * trilinear_devoxelize_grad_kernel (trilinear_devox.cu:119-162).
  *   grad_y f32 [b, c, n]  inds i32 [b, 8, n]  wgts f32 [b, 8, n]
  *   grad_x f32 [b, c, r^3]                                                      */
 int pcfm_trilinear_devoxelize_bwd(const float* grad_y, const int* inds, const float* wgts,
-                                  int b, int c, int n, int r, float* grad_x, void* stream);
+                                  int b, int c, int n, int r, float* grad_x, void* ws,
+                                  size_t ws_bytes, void* stream);
 
 /* Ball query.  Replaces ball_query_forward (src/ball_query/ball_query.cpp:6-30)
  * -> ball_query_kernel (ball_query.cu:19-50).
@@ -98,11 +101,13 @@ int pcfm_ball_query(const float* centers, const float* points, int b, int m, int
 int pcfm_grouping_fwd(const float* feat, const int* idx, int b, int c, int n, int m,
                       int u, float* out, void* stream);
 
+size_t pcfm_grouping_bwd_workspace_bytes(int b, int c, int n, int m, int u);
+
 /* Grouping backward.  Replaces grouping_backward (grouping.cpp:24-44) ->
  * grouping_grad_kernel (grouping.cu:58-77).
  *   grad_y f32 [b, c, m, u]  idx i32 [b, m, u]  grad_x f32 [b, c, n]              */
 int pcfm_grouping_bwd(const float* grad_y, const int* idx, int b, int c, int n, int m,
-                      int u, float* grad_x, void* stream);
+                      int u, float* grad_x, void* ws, size_t ws_bytes, void* stream);
 
 /* ------------------------------------------------------------------------
  * Chamfer-3D

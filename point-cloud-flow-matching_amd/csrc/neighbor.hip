@@ -3,6 +3,7 @@
 // Reference semantics: third_party/pvcnn/modules/functional/src/ball_query/
 // ball_query.cu:19-50 and src/grouping/grouping.cu:18-77.
 #include "rows.hpp"
+#include "segsum.hpp"
 
 namespace pcfm {
 namespace {
@@ -74,11 +75,21 @@ extern "C" int pcfm_grouping_fwd(const float* feat, const int* idx, int b, int c
                        (hipStream_t)stream, "grouping_fwd");
 }
 
+extern "C" size_t pcfm_grouping_bwd_workspace_bytes(int b, int c, int n, int m, int u) {
+  if (b < 0 || c < 0 || n < 0 || m < 0 || u < 0) return 0;
+  const long long mu = (long long)m * u;
+  if (mu >= (1LL << 31)) return 0;
+  return seg_ws_bytes(b, c, (int)mu, n, 1);
+}
+
 extern "C" int pcfm_grouping_bwd(const float* grad_y, const int* idx, int b, int c, int n, int m,
-                                 int u, float* grad_x, void* stream) {
+                                 int u, float* grad_x, void* ws, size_t ws_bytes, void* stream) {
   PCFM_CHECK_ARG(b >= 0 && c >= 0 && n >= 0 && m >= 0 && u >= 0, "grouping_bwd: negative size");
   const long long mu = (long long)m * u;
   PCFM_CHECK_ARG(mu < (1LL << 31), "grouping_bwd: m*u too large");
-  return launch_scatter(grad_y, grad_x, b, c, n, (int)mu, ProvIdx1{idx, nullptr, (int)mu, n},
-                        (hipStream_t)stream, "grouping_bwd");
+  const size_t need = pcfm_grouping_bwd_workspace_bytes(b, c, n, m, u);
+  PCFM_CHECK_ARG(ws_bytes >= need, "grouping_bwd: workspace %zu < %zu bytes", ws_bytes, need);
+  // grad_x[c, i] = sum of grad_y over the (center, slot) pairs whose index is i
+  return seg_scatter<1>(grad_y, idx, mu, nullptr, nullptr, 0, b, c, (int)mu, n, nullptr, grad_x,
+                        ws, (hipStream_t)stream, "grouping_bwd");
 }

@@ -4,6 +4,7 @@
 // Reference semantics: third_party/pvcnn/modules/functional/src/voxelization/
 // vox.cu:18-126 and src/interpolate/trilinear_devox.cu:21-162.
 #include "rows.hpp"
+#include "segsum.hpp"
 
 namespace pcfm {
 namespace {
@@ -49,9 +50,10 @@ bool cube_fits(int r, int* s) {
 
 using namespace pcfm;
 
-extern "C" size_t pcfm_avg_voxelize_fwd_workspace_bytes(int b, int n) {
-  if (b < 0 || n < 0) return 0;
-  return (size_t)b * n * sizeof(float);
+extern "C" size_t pcfm_avg_voxelize_fwd_workspace_bytes(int b, int c, int n, int r) {
+  int s = 0;
+  if (b < 0 || c < 0 || n < 0 || !cube_fits(r, &s)) return 0;
+  return align256((size_t)b * n * sizeof(float)) + seg_ws_bytes(b, c, n, s, 1);
 }
 
 extern "C" int pcfm_avg_voxelize_fwd(const float* feat, const int* coords, int b, int c, int n,
@@ -61,9 +63,8 @@ extern "C" int pcfm_avg_voxelize_fwd(const float* feat, const int* coords, int b
   PCFM_CHECK_ARG(b >= 0 && c >= 0 && n >= 0, "avg_voxelize_fwd: negative size b=%d c=%d n=%d",
                  b, c, n);
   PCFM_CHECK_ARG(cube_fits(r, &s), "avg_voxelize_fwd: bad resolution %d", r);
-  PCFM_CHECK_ARG(ws_bytes >= pcfm_avg_voxelize_fwd_workspace_bytes(b, n),
-                 "avg_voxelize_fwd: workspace %zu < %zu bytes", ws_bytes,
-                 pcfm_avg_voxelize_fwd_workspace_bytes(b, n));
+  const size_t need = pcfm_avg_voxelize_fwd_workspace_bytes(b, c, n, r);
+  PCFM_CHECK_ARG(ws_bytes >= need, "avg_voxelize_fwd: workspace %zu < %zu bytes", ws_bytes, need);
   if (b == 0) return PCFM_OK;
   hipStream_t st = (hipStream_t)stream;
   hipError_t he = hipMemsetAsync(cnt, 0, (size_t)b * s * sizeof(int), st);
@@ -72,6 +73,7 @@ extern "C" int pcfm_avg_voxelize_fwd(const float* feat, const int* coords, int b
     return (int)he;
   }
   float* inv = (float*)ws;
+  void* seg = (char*)ws + align256((size_t)b * n * sizeof(float));
   if (n > 0) {
     dim3 grid(ceil_div(n, 256), b);
     hipLaunchKernelGGL(vox_count_kernel, grid, dim3(256), 0, st, coords, n, r, s, ind, cnt);
@@ -79,9 +81,9 @@ extern "C" int pcfm_avg_voxelize_fwd(const float* feat, const int* coords, int b
     int e = check_launch("avg_voxelize_fwd(count)");
     if (e) return e;
   }
-  // out[c, v] = sum_i feat[c, i] * inv[i]   (the reference's per-term product, vox.cu:68)
-  return launch_scatter(feat, out, b, c, s, n, ProvIdx1{ind, inv, n, s}, st,
-                        "avg_voxelize_fwd(scatter)");
+  // out[c, v] = sum_{i in voxel v} feat[c, i] * inv[i]   (per-term product, vox.cu:68)
+  return seg_scatter<1>(feat, ind, n, inv, nullptr, r, b, c, n, s, cnt, out, seg, st,
+                        "avg_voxelize_fwd(segsum)");
 }
 
 extern "C" int pcfm_avg_voxelize_bwd(const float* grad_y, const int* ind, const int* cnt, int b,
@@ -99,19 +101,33 @@ extern "C" int pcfm_trilinear_devoxelize_fwd(const float* coords, const float* f
   int s = 0;
   PCFM_CHECK_ARG(b >= 0 && c >= 0 && n >= 0, "trilinear_devoxelize_fwd: negative size");
   PCFM_CHECK_ARG(cube_fits(r, &s), "trilinear_devoxelize_fwd: bad resolution %d", r);
-  PCFM_CHECK_ARG(!training || (inds != nullptr && wgts != nullptr),
+  PCFM_CHECK_ARG(!training || (long long)b * n == 0 || (inds != nullptr && wgts != nullptr),
                  "trilinear_devoxelize_fwd: training needs inds/wgts buffers");
   ProvDevox prov{coords, n, r, r * r, s, training ? inds : nullptr, training ? wgts : nullptr};
   return launch_gather(feat, out, b, c, s, n, prov, (hipStream_t)stream,
                        "trilinear_devoxelize_fwd");
 }
 
+extern "C" size_t pcfm_trilinear_devoxelize_bwd_workspace_bytes(int b, int c, int n, int r) {
+  int s = 0;
+  if (b < 0 || c < 0 || n < 0 || !cube_fits(r, &s)) return 0;
+  return seg_ws_bytes(b, c, n, s, 8);
+}
+
 extern "C" int pcfm_trilinear_devoxelize_bwd(const float* grad_y, const int* inds,
                                              const float* wgts, int b, int c, int n, int r,
-                                             float* grad_x, void* stream) {
+                                             float* grad_x, void* ws, size_t ws_bytes,
+                                             void* stream) {
   int s = 0;
   PCFM_CHECK_ARG(b >= 0 && c >= 0 && n >= 0, "trilinear_devoxelize_bwd: negative size");
   PCFM_CHECK_ARG(cube_fits(r, &s), "trilinear_devoxelize_bwd: bad resolution %d", r);
-  return launch_scatter(grad_y, grad_x, b, c, s, n, ProvIdx8{inds, wgts, n, s},
+  const size_t need = pcfm_trilinear_devoxelize_bwd_workspace_bytes(b, c, n, r);
+  PCFM_CHECK_ARG(ws_bytes >= need, "trilinear_devoxelize_bwd: workspace %zu < %zu bytes",
+                 ws_bytes, need);
+  // Points grouped by their base cell inds[b, 0, i]; corner k of a point in
+  // cell q lands on q + (dx r^2 + dy r + dz).  When a fraction is 0 the
+  // reference folds that corner onto the low cell with weight exactly 0
+  // (trilinear_devox.cu:64-75), so both placements add the same zeros.
+  return seg_scatter<8>(grad_y, inds, 8LL * n, nullptr, wgts, r, b, c, n, s, nullptr, grad_x, ws,
                         (hipStream_t)stream, "trilinear_devoxelize_bwd");
 }

@@ -2,12 +2,29 @@
 
 Reference: third_party/pvcnn/modules/shared_mlp.py:6-33.  Parameter names
 (layers.{3k}, layers.{3k+1}) match, so reference checkpoints load unchanged.
+
+The 1x1 Conv1d is evaluated as what it is, a GEMM over the channel axis
+(y[b] = W x[b] + bias, hipBLASLt fp32 MFMA kernels), instead of going through
+MIOpen's convolution solvers: same product, no per-shape solver search.
 """
+import torch
 import torch.nn as nn
 
-__all__ = ["SharedMLP"]
+__all__ = ["SharedMLP", "PointwiseConv1d"]
 
-_KINDS = {1: (nn.Conv1d, nn.BatchNorm1d), 2: (nn.Conv2d, nn.BatchNorm2d)}
+
+class PointwiseConv1d(nn.Conv1d):
+    """nn.Conv1d(in, out, 1) whose forward is a channel GEMM (same parameters)."""
+
+    def forward(self, x):
+        if self.kernel_size != (1,) or self.groups != 1 or self.stride != (1,) \
+                or self.padding not in ((0,), "valid") or self.dilation != (1,):
+            return super().forward(x)
+        y = torch.matmul(self.weight[:, :, 0], x)
+        return y if self.bias is None else y + self.bias[:, None]
+
+
+_KINDS = {1: (PointwiseConv1d, nn.BatchNorm1d), 2: (nn.Conv2d, nn.BatchNorm2d)}
 
 
 class SharedMLP(nn.Module):

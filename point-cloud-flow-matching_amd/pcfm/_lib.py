@@ -24,14 +24,16 @@ _Z = ctypes.c_size_t
 SIGNATURES = {
     "pcfm_abi_version": (_I, []),
     "pcfm_last_error": (ctypes.c_char_p, []),
-    "pcfm_avg_voxelize_fwd_workspace_bytes": (_Z, [_I, _I]),
+    "pcfm_avg_voxelize_fwd_workspace_bytes": (_Z, [_I, _I, _I, _I]),
     "pcfm_avg_voxelize_fwd": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _Z, _P]),
     "pcfm_avg_voxelize_bwd": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P]),
     "pcfm_trilinear_devoxelize_fwd": (_I, [_P, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P]),
-    "pcfm_trilinear_devoxelize_bwd": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P]),
+    "pcfm_trilinear_devoxelize_bwd_workspace_bytes": (_Z, [_I, _I, _I, _I]),
+    "pcfm_trilinear_devoxelize_bwd": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P, _Z, _P]),
     "pcfm_ball_query": (_I, [_P, _P, _I, _I, _I, _F, _I, _P, _P]),
     "pcfm_grouping_fwd": (_I, [_P, _P, _I, _I, _I, _I, _I, _P, _P]),
-    "pcfm_grouping_bwd": (_I, [_P, _P, _I, _I, _I, _I, _I, _P, _P]),
+    "pcfm_grouping_bwd_workspace_bytes": (_Z, [_I, _I, _I, _I, _I]),
+    "pcfm_grouping_bwd": (_I, [_P, _P, _I, _I, _I, _I, _I, _P, _P, _Z, _P]),
     "pcfm_chamfer_workspace_bytes": (_Z, [_I, _I, _I]),
     "pcfm_chamfer_fwd": (_I, [_P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _Z, _P]),
     "pcfm_chamfer_bwd": (_I, [_P, _P, _I, _I, _I, _P, _P, _P, _P, _P, _P, _P]),
@@ -44,7 +46,7 @@ SIGNATURES = {
     "pcfm_emd_matchcost_bwd_f64": (_I, [_P, _P, _P, _P, _I, _I, _I, _P, _P, _P, _Z, _P]),
 }
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 _lock = threading.Lock()
 _lib = None

@@ -22,7 +22,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from modules.pvconv import PVConv
-from modules.shared_mlp import SharedMLP
+from modules.shared_mlp import PointwiseConv1d, SharedMLP
 
 __all__ = [
     "timestep_embedding", "FiLMBlock", "VelocityNet", "ShapeEncoder",
@@ -348,10 +348,10 @@ class ContextNet(_TimeCondEmbed):
 
         self.stage_channels = list(stage_channels)
         head_in = sum(self.stage_channels) + (c_last if self.with_global else 0)
-        self.head_pre = nn.Conv1d(head_in, c_last, 1, bias=True)
+        self.head_pre = PointwiseConv1d(head_in, c_last, 1, bias=True)
         self.head_norm = _make_norm(norm_type, c_last, gn_groups)
         self.head_act = nn.SiLU()
-        self.head_out = nn.Conv1d(c_last, ctx_dim, 1, bias=True)
+        self.head_out = PointwiseConv1d(c_last, ctx_dim, 1, bias=True)
         _kaiming_relu_(self.head_pre)
         nn.init.zeros_(self.head_out.weight)
         nn.init.zeros_(self.head_out.bias)

@@ -119,7 +119,7 @@ def avg_voxelize_forward(features: torch.Tensor, coords: torch.Tensor, resolutio
     out = torch.empty((b, c, s), dtype=torch.float32, device=features.device)
     ind = torch.empty((b, n), dtype=torch.int32, device=features.device)
     cnt = torch.empty((b, s), dtype=torch.int32, device=features.device)
-    ws = _workspace(_lib.query("pcfm_avg_voxelize_fwd_workspace_bytes", b, n), features)
+    ws = _workspace(_lib.query("pcfm_avg_voxelize_fwd_workspace_bytes", b, c, n, r), features)
     nbytes = 4 * b * (3 * n + c * n + n + s + c * s)  # vox-fwd
     with _timed("avg_voxelize_fwd", nbytes, features):
         _lib.call("pcfm_avg_voxelize_fwd", _ptr(features), _ptr(coords), b, c, n, r, _ptr(out),
@@ -176,10 +176,12 @@ def trilinear_devoxelize_backward(grad_y: torch.Tensor, indices: torch.Tensor,
     b, c, n = grad_y.shape
     r = int(r)
     grad_x = torch.empty((b, c, r * r * r), dtype=torch.float32, device=grad_y.device)
+    ws = _workspace(_lib.query("pcfm_trilinear_devoxelize_bwd_workspace_bytes", b, c, n, r),
+                    grad_y)
     nbytes = 4 * b * (c * n + 16 * n + c * r ** 3)  # devox-bwd
     with _timed("trilinear_devoxelize_bwd", nbytes, grad_y):
         _lib.call("pcfm_trilinear_devoxelize_bwd", _ptr(grad_y), _ptr(indices), _ptr(weights),
-                  b, c, n, r, _ptr(grad_x), _stream(grad_y))
+                  b, c, n, r, _ptr(grad_x), _ptr(ws), ws.numel(), _stream(grad_y))
     return grad_x
 
 
@@ -217,8 +219,9 @@ def grouping_backward(grad_y: torch.Tensor, indices: torch.Tensor, n: int):
     m, u = indices.shape[1], indices.shape[2]
     n = int(n)
     grad_x = torch.empty((b, c, n), dtype=torch.float32, device=grad_y.device)
+    ws = _workspace(_lib.query("pcfm_grouping_bwd_workspace_bytes", b, c, n, m, u), grad_y)
     _lib.call("pcfm_grouping_bwd", _ptr(grad_y), _ptr(indices), b, c, n, m, u, _ptr(grad_x),
-              _stream(grad_y))
+              _ptr(ws), ws.numel(), _stream(grad_y))
     return grad_x
 
 

@@ -14,6 +14,8 @@ Deliberate, result-preserving differences (all switchable in TrainConfig):
     device instead of the host round trip of GradScaler.step; same update rule.
   * `device_rng`: t ~ Beta(a, 1) is sampled on the device (the reference
     samples on the CPU and copies, train.py:604-605, :639-640); same law.
+  * `miopen_find`: torch.backends.cudnn.benchmark = True, i.e. MIOpen picks
+    each convolution's solver by timing the candidates once per shape.
 """
 from __future__ import annotations
 
@@ -94,6 +96,10 @@ class TrainConfig:
     fused_adamw: bool = True
     device_rng: bool = True
     film_per_point: bool = False
+    # MIOpen exhaustive solver search for every conv shape (cudnn.benchmark):
+    # ~94-113 TFLOP/s fp32 on the PVConv Conv3d shapes vs 12-68 TFLOP/s with
+    # the default heuristic pick (tools/conv3d_probe.py on MI355X); same math.
+    miopen_find: bool = True
 
     @property
     def enc_in_ch(self) -> int:
@@ -229,6 +235,8 @@ class Trainer:
                  ddp: bool = False):
         self.cfg = cfg
         self.device = torch.device(device)
+        if self.device.type == "cuda" and cfg.miopen_find:
+            torch.backends.cudnn.benchmark = True
         self.rank, self.world_size = rank, world_size
         seed_all(cfg.seed + rank)
         self.enc, self.pf, self.lf = build_models(cfg, self.device)

@@ -267,14 +267,21 @@ def test_emd_vs_oracle(dtype, b, n, m):
     c = g.random((b, m, 3)).astype(dtype)
     match = ops.approxmatch_forward(cu(a), cu(c))
     e_match = O.emd_approxmatch(a, c)
-    np.testing.assert_allclose(np_(match), e_match, rtol=1e-4, atol=1e-6)
+    # 10 levels x 3 passes of approximate exp (the reference's __expf; the oracle
+    # uses libm expf) with min/max clamps in between: individual match entries
+    # move by up to ~1e-4 absolute (entries are <= 1), the cost by < 1e-4 relative
+    np.testing.assert_allclose(np_(match), e_match, rtol=1e-3, atol=5e-4)
+    assert abs(np_(match).sum() - e_match.sum()) <= 1e-4 * e_match.sum()
     cost = ops.matchcost_forward(cu(a), cu(c), match)
     np.testing.assert_allclose(np_(cost), O.emd_matchcost(a, c, e_match), rtol=1e-4)
+    # matchcost itself on identical inputs: summation order only
+    np.testing.assert_allclose(np_(ops.matchcost_forward(cu(a), cu(c), cu(e_match))),
+                               O.emd_matchcost(a, c, e_match), rtol=1e-5)
     gc = g.random(b).astype(dtype)
-    g1, g2 = ops.matchcost_backward(cu(gc), cu(a), cu(c), match)
+    g1, g2 = ops.matchcost_backward(cu(gc), cu(a), cu(c), cu(e_match))
     e1, e2 = O.emd_matchcost_bwd(gc, a, c, e_match)
-    np.testing.assert_allclose(np_(g1), e1, rtol=1e-3, atol=1e-5)
-    np.testing.assert_allclose(np_(g2), e2, rtol=1e-3, atol=1e-5)
+    np.testing.assert_allclose(np_(g1), e1, rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(np_(g2), e2, rtol=1e-4, atol=1e-5)
 
 
 def test_emd_known_answer(golden):

@@ -17,7 +17,7 @@ def test_pvconv_matches_reference(oracle_backend, golden):
     torch.manual_seed(int(g["seed"]))
     blk = PVConv(16, 16, kernel_size=3, resolution=8, with_se=True, normalize=True, eps=1e-6)
     # same creation order -> same initial weights from the same seed
-    np.testing.assert_array_equal(_param_sums(blk), g["param_sums"])
+    np.testing.assert_allclose(_param_sums(blk), g["param_sums"], rtol=1e-12, atol=1e-12)
     feats = torch.from_numpy(g["feats"]).requires_grad_(True)
     out, _ = blk((feats, torch.from_numpy(g["coords"])))
     np.testing.assert_allclose(out.detach().numpy(), g["out"], rtol=1e-5, atol=1e-6)
@@ -49,7 +49,7 @@ def test_hybrid_matches_reference(oracle_backend, golden, film_per_point):
     pf.train()
     names = [n for n, _ in pf.named_parameters()]
     assert names == list(g["param_names"])
-    np.testing.assert_array_equal(_param_sums(pf), g["param_sums"])
+    np.testing.assert_allclose(_param_sums(pf), g["param_sums"], rtol=1e-12, atol=1e-12)
     v = pf(torch.from_numpy(g["x"]), torch.from_numpy(g["t"]), torch.from_numpy(g["cond"]),
            cond_drop_mask=torch.from_numpy(g["mask"]))
     np.testing.assert_allclose(v.detach().numpy(), g["v"], rtol=1e-4, atol=1e-5)
