@@ -90,6 +90,6 @@ extern "C" int pcfm_grouping_bwd(const float* grad_y, const int* idx, int b, int
   const size_t need = pcfm_grouping_bwd_workspace_bytes(b, c, n, m, u);
   PCFM_CHECK_ARG(ws_bytes >= need, "grouping_bwd: workspace %zu < %zu bytes", ws_bytes, need);
   // grad_x[c, i] = sum of grad_y over the (center, slot) pairs whose index is i
-  return seg_scatter<1>(grad_y, idx, mu, nullptr, nullptr, 0, b, c, (int)mu, n, nullptr, grad_x,
+  return seg_scatter<1>(grad_y, idx, mu, false, nullptr, 0, b, c, (int)mu, n, nullptr, grad_x,
                         ws, (hipStream_t)stream, "grouping_bwd");
 }

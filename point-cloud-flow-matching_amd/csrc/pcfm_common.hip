@@ -29,8 +29,10 @@ int allow_big_lds(const void* kernel) {
   static std::unordered_set<const void*> done;
   std::lock_guard<std::mutex> lock(mu);
   if (done.count(kernel)) return PCFM_OK;
+  // leave 1 KiB for the kernels' small static __shared__ arrays: the cap
+  // counts dynamic bytes, the hardware limit counts both
   hipError_t e = hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     kLdsBytesMax);
+                                     kLdsBytesMax - 1024);
   if (e != hipSuccess) {
     set_error("hipFuncSetAttribute(MaxDynamicSharedMemorySize): %s", hipGetErrorString(e));
     return (int)e;

@@ -1,25 +1,32 @@
 // Sorted, atomic-free scatter ("segment sum") for the PVConv path.
 //
 // Measured on MI355X (tools/voxel_probe.py): an LDS float atomic (ds_add_f32)
-// costs ~200 cycles per wave instruction whatever the address pattern, so the
-// LDS-privatised scatter of rows.hpp runs at 0.15-0.9 TB/s.  The scatters are
-// therefore recast as gathers over points sorted by their target cell:
+// costs ~200 cycles per wave instruction whatever the address pattern, so an
+// LDS-privatised scatter with one atomic per (item, channel, tap) runs at
+// 0.15-0.9 TB/s.  The scatters are recast as gathers over items sorted by
+// their target cell:
 //
-//   1. count   cnt[b, key]              integer atomics (exact)
-//   2. scan    start[b, 0..V]           exclusive prefix sums, one block per b
-//   3. place   perm[b, start[key] + r]  points grouped by key
-//   4. gather-transpose  XS[b, j, c] = in[b, c, perm[j]] * scale[perm[j]]
-//                        (channels-last rows, 256 B per point per 64 channels)
-//   5. tap sum out[b, c, v] = sum_k sum_{j in run(v - off_k)} w_k(j) * XS[b, j, c]
-//      lanes = 64 channels, one wave per tap (8 waves for the trilinear
-//      stencil, 4 voxel-interleaved waves for 1 tap), partials reduced in a
-//      fixed tap order in LDS, rows written out coalesced.  No atomics.
+//   1-3. counting sort, one block per batch element, histogram in LDS:
+//      start[b, 0..V] (exclusive prefix of the counts) and perm / skey at
+//      start[key] + rank
+//   4. transpose  xt[b, i, c] = in[b, c, i]       channels-last rows, item order
+//   5. range gather, output-stationary per voxel tile, lanes = 64 channels.
+//      The items feeding a tile [v0, v0+TV) through stencil column (dx, dy)
+//      are ONE contiguous sorted range (cells v0-off-1 .. v0+TV-off-1 are
+//      consecutive keys), so a wave streams that range, keeps one register
+//      accumulator per dz tap for the current run of equal keys, and flushes
+//      it into its own LDS partial tile when the key changes.  Ranges are cut
+//      into chunks shared round robin by the block's waves and, for crowded
+//      tiles, by up to P blocks (a dense r=8 cell holds thousands of points);
+//      partial tiles are summed in a fixed order and leave as coalesced rows.
+//      No atomics in the data path.
 //
-// Used by avg_voxelize forward (key = voxel, scale = 1/cnt), trilinear
-// devoxelize backward (key = base cell inds[b,0,:], 8 taps with wgts) and
-// grouping backward (key = neighbour index).  The order of points inside one
-// key comes from step 3's atomics, so float sums are order-nondeterministic
-// at the last bit -- exactly like the reference's float atomics.
+// Used by avg_voxelize forward (key = voxel, term = feat * (1/cnt)),
+// trilinear devoxelize backward (key = base cell inds[b,0,:], term = wgt * g
+// for the 8 corners) and grouping backward (key = neighbour index, term = g).
+// The order of items inside one key comes from step 3's atomics, so float sums
+// are order-nondeterministic at the last bit -- exactly like the reference's
+// float atomics.
 #pragma once
 
 #include <algorithm>
@@ -30,206 +37,325 @@ namespace pcfm {
 namespace {  // kernels get internal linkage: this header is included by several .hip files
 
 // --------------------------------------------------------------------------
-// 1-3: sort items by key
+// 1-3: counting sort by key, one block (1024 threads) per batch element.
+// The key histogram lives in LDS (kSortKeys ints = 128 KiB; larger key spaces
+// take several passes over the keys), so counting and ranking use LDS atomics
+// only -- device-scope global atomics cost ~5 G/s on this part (measured:
+// 160K of them took ~30 us), an LDS atomic a few hundred cycles per wave.
+//   start[b, 0..V]  exclusive prefix of the counts (start[b, V] = total)
+//   cnt_out[b, v]   the counts (optional: the voxelization's `cnt` output)
+//   vinv[b, v]      (float)(1.0 / (double)cnt) (optional, vox.cu:66)
+//   perm/skey[b, pos]  item and key at pos = start[key] + (arrival rank)
 // --------------------------------------------------------------------------
-__global__ void __launch_bounds__(256)
-    seg_count_kernel(const int* __restrict__ key, long long key_bstride, int n, int V,
-                     int* __restrict__ cnt) {
-  const int b = blockIdx.y;
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const int k = key[(size_t)b * key_bstride + i];
-  if ((unsigned)k < (unsigned)V) atomicAdd(cnt + (size_t)b * V + k, 1);
-}
+constexpr int kSortKeys = 32768;
+constexpr int kSortBatch = 8;  // keys per thread in flight
 
-// One block (1024 threads) per batch element: start[b, v] = sum_{u<v} cnt[b, u],
-// start[b, V] = total; cursor = start[0..V).
 __global__ void __launch_bounds__(1024)
-    seg_scan_kernel(const int* __restrict__ cnt, int V, int* __restrict__ start,
-                    int* __restrict__ cursor) {
+    seg_sort_kernel(const int* __restrict__ key, long long key_bstride, int n, int V,
+                    int* __restrict__ start, int* __restrict__ cnt_out, float* __restrict__ vinv,
+                    int* __restrict__ perm, int* __restrict__ skey) {
+  extern __shared__ int hist[];  // [min(V, kSortKeys)]
   __shared__ int wsum[16];
   const int b = blockIdx.x;
-  const int t = threadIdx.x;
-  const int per = (V + 1023) / 1024;
-  const int lo = min(V, t * per), hi = min(V, lo + per);
-  const int* cb = cnt + (size_t)b * V;
-  int local = 0;
-  for (int v = lo; v < hi; ++v) local += cb[v];
-  // inclusive scan of `local` across the block
-  int x = local;
-  const int lane = t & 63, w = t >> 6;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int* __restrict__ kb = key + (size_t)b * key_bstride;
+  int* __restrict__ sb = start + (size_t)b * (V + 1);
+  int carry = 0;
+  for (int k0 = 0; k0 < V; k0 += kSortKeys) {
+    const int len = min(kSortKeys, V - k0);
+    for (int e = t; e < len; e += 1024) hist[e] = 0;
+    __syncthreads();
+    for (int i0 = 0; i0 < n; i0 += 1024 * kSortBatch) {
+      int kk[kSortBatch];  // keys first (independent loads), then the LDS atomics
 #pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int y = __shfl_up(x, o, 64);
-    if (lane >= o) x += y;
-  }
-  if (lane == 63) wsum[w] = x;
-  __syncthreads();
-  if (t < 64) {
-    int s = (t < 16) ? wsum[t] : 0;
+      for (int q = 0; q < kSortBatch; ++q) {
+        const int i = i0 + q * 1024 + t;
+        kk[q] = i < n ? kb[i] - k0 : -1;
+      }
 #pragma unroll
-    for (int o = 1; o < 16; o <<= 1) {
-      const int y = __shfl_up(s, o, 64);
-      if (lane >= o) s += y;
+      for (int q = 0; q < kSortBatch; ++q)
+        if ((unsigned)kk[q] < (unsigned)len) atomicAdd(hist + kk[q], 1);
+    }    __syncthreads();
+    // exclusive scan: wave w owns the 64-aligned segment [lo, hi)
+    const int seg = ((len + 15) / 16 + 63) & ~63;
+    const int lo = min(len, w * seg), hi = min(len, lo + seg);
+    int part = 0;
+    for (int e = lo + lane; e < hi; e += 64) part += hist[e];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
+    if (lane == 0) wsum[w] = part;
+    __syncthreads();
+    int run = carry, total = 0;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      const int x = wsum[g];
+      run += g < w ? x : 0;
+      total += x;
     }
-    if (t < 16) wsum[t] = s;
+    for (int e0 = lo; e0 < hi; e0 += 64) {
+      const int e = e0 + lane;
+      const int c = e < hi ? hist[e] : 0;
+      int x = c;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+      }
+      if (e < hi) {
+        const int pos = run + x - c;
+        hist[e] = pos;
+        sb[k0 + e] = pos;
+        if (cnt_out != nullptr) cnt_out[(size_t)b * V + k0 + e] = c;
+        if (vinv != nullptr) vinv[(size_t)b * V + k0 + e] = c > 0 ? (float)(1.0 / (double)c) : 0.0f;
+      }
+      run += __shfl(x, 63, 64);
+    }
+    __syncthreads();
+    for (int i0 = 0; i0 < n; i0 += 1024 * kSortBatch) {
+      int kk[kSortBatch];
+#pragma unroll
+      for (int q = 0; q < kSortBatch; ++q) {
+        const int i = i0 + q * 1024 + t;
+        kk[q] = i < n ? kb[i] - k0 : -1;
+      }
+#pragma unroll
+      for (int q = 0; q < kSortBatch; ++q) {
+        if ((unsigned)kk[q] < (unsigned)len) {
+          const int pos = atomicAdd(hist + kk[q], 1);
+          const size_t o = (size_t)b * n + pos;
+          perm[o] = i0 + q * 1024 + t;
+          skey[o] = kk[q] + k0;
+        }
+      }
+    }
+    carry += total;
+    __syncthreads();
   }
-  __syncthreads();
-  int run = x - local + (w > 0 ? wsum[w - 1] : 0);  // exclusive prefix of this thread
-  int* sb = start + (size_t)b * (V + 1);
-  int* kb = cursor + (size_t)b * V;
-  for (int v = lo; v < hi; ++v) {
-    sb[v] = run;
-    kb[v] = run;
-    run += cb[v];
-  }
-  if (t == 1023) sb[V] = wsum[15];
-}
-
-__global__ void __launch_bounds__(256)
-    seg_place_kernel(const int* __restrict__ key, long long key_bstride, int n, int V,
-                     int* __restrict__ cursor, int* __restrict__ perm) {
-  const int b = blockIdx.y;
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const int k = key[(size_t)b * key_bstride + i];
-  if ((unsigned)k < (unsigned)V) {
-    const int pos = atomicAdd(cursor + (size_t)b * V + k, 1);
-    perm[(size_t)b * n + pos] = i;
-  }
+  if (t == 0) sb[V] = carry;
 }
 
 // --------------------------------------------------------------------------
-// 4: gather-transpose into sorted channels-last rows
-// grid = (ceil(n/64), ceil(C/64), B), 256 threads.  perm entries past the
-// valid count are -1 (pre-filled) and produce zero rows.
+// 4: transpose the item features to channels-last rows, ORIGINAL item order:
+//    xt[b, i, c] = in[b, c, i]   (64x64 LDS tiles; 256-B reads and writes)
+// grid = (ceil(n/64), ceil(C/64), B), 256 threads.
 // --------------------------------------------------------------------------
 __global__ void __launch_bounds__(256)
-    seg_gather_t_kernel(const float* __restrict__ in, const int* __restrict__ perm,
-                        const float* __restrict__ scale, const float* __restrict__ tapw,
-                        int C, int n, float* __restrict__ xs, float* __restrict__ ws8) {
+    seg_transpose_kernel(const float* __restrict__ in, int C, int n, float* __restrict__ xt) {
   __shared__ float tile[64][65];
   const int b = blockIdx.z;
   const int j0 = blockIdx.x * 64, c0 = blockIdx.y * 64;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int jj = j0 + lane;
-  const int p = jj < n ? perm[(size_t)b * n + jj] : -1;
-  const float sc = (scale != nullptr && p >= 0) ? scale[(size_t)b * n + p] : 1.0f;
+  const int j = j0 + lane;
   for (int cc = w; cc < 64; cc += 4) {
     const int c = c0 + cc;
-    float v = 0.0f;
-    if (c < C && p >= 0) {
-      v = in[((size_t)b * C + c) * n + p];
-      if (scale != nullptr) v = v * sc;  // the reference's per-term product (vox.cu:68)
-    }
-    tile[cc][lane] = v;
-  }
-  if (tapw != nullptr && blockIdx.y == 0 && w == 0 && jj < n) {
-    float4 lo, hi;  // WS[b, j, 0..7] = wgts[b, 0..7, perm[j]]
-    const float* tb = tapw + (size_t)b * 8 * n + (p >= 0 ? p : 0);
-    lo.x = p >= 0 ? tb[0] : 0.0f;
-    lo.y = p >= 0 ? tb[(size_t)n] : 0.0f;
-    lo.z = p >= 0 ? tb[(size_t)2 * n] : 0.0f;
-    lo.w = p >= 0 ? tb[(size_t)3 * n] : 0.0f;
-    hi.x = p >= 0 ? tb[(size_t)4 * n] : 0.0f;
-    hi.y = p >= 0 ? tb[(size_t)5 * n] : 0.0f;
-    hi.z = p >= 0 ? tb[(size_t)6 * n] : 0.0f;
-    hi.w = p >= 0 ? tb[(size_t)7 * n] : 0.0f;
-    float4* o = reinterpret_cast<float4*>(ws8 + ((size_t)b * n + jj) * 8);
-    o[0] = lo;
-    o[1] = hi;
+    tile[cc][lane] = (c < C && j < n) ? in[((size_t)b * C + c) * n + j] : 0.0f;
   }
   __syncthreads();
   const int c = c0 + lane;
   if (c < C) {
     for (int jr = w; jr < 64; jr += 4) {
-      const int j = j0 + jr;
-      if (j < n) xs[((size_t)b * n + j) * C + c] = tile[lane][jr];
+      const int jj = j0 + jr;
+      if (jj < n) xt[((size_t)b * n + jj) * C + c] = tile[lane][jr];
     }
   }
 }
 
 // --------------------------------------------------------------------------
-// 5: tap sums, output-stationary
-// grid = (ceil(V/TV), ceil(C/64), B).  TAPS == 8: 8 waves, wave k = corner k
-// (dx,dy,dz) = (k>>2, (k>>1)&1, k&1) of the trilinear stencil (the reference's
-// wgt000..wgt111 order, trilinear_devox.cu:178-185).  TAPS == 1: 4 waves share
-// the tile's voxels round robin.
+// 5: range gather
+//   TAPS == 8: column g = (dx, dy) in 0..3, off = dx r^2 + dy r.  A point of
+//     cell q adds w[dx,dy,0] * x to voxel q + off and w[dx,dy,1] * x to voxel
+//     q + off + 1; the column's source cells are [v0 - off - 1, v0 + TV - off).
+//     (When a fraction is 0 the reference folds that corner onto the low cell
+//     with weight exactly 0, trilinear_devox.cu:64-75, so both placements add
+//     the same zeros.)
+//   TAPS == 1: one range [v0, v0 + TV); a point of cell q adds x * vscale[q]
+//     (or x) to voxel q.
+// A tile's ranges are cut into chunks of kChunk sorted items.  Chunk t goes
+// to part t / kWaves mod P (one block per part) and to wave t mod kWaves in
+// it, so a crowded tile (the centre cells of a Gaussian cloud hold thousands
+// of points at r = 8) is spread over up to P blocks.  Part 0 writes the tile
+// to `out` (zeros if empty); parts 1.. that received chunks write partial
+// tiles that seg_part_sum_kernel adds in part order.  No atomics.
+// grid = (ceil(V/TV) * P, ceil(C/64), B), kWaves waves; LDS = kWaves partial tiles.
 // --------------------------------------------------------------------------
+constexpr int kWaves = 4;
+constexpr int kChunk = 128;
+constexpr int kInFlight = 16;  // row loads issued back to back per wave
+
 template <int TAPS>
-__global__ void __launch_bounds__(512)
-    seg_tap_sum_kernel(const float* __restrict__ xs, const float* __restrict__ ws8,
-                       const int* __restrict__ start, int C, int n, int V, int r, int TV,
-                       float* __restrict__ out) {
-  extern __shared__ __attribute__((aligned(16))) float part[];  // [TAPS][TV][65]
-  const int b = blockIdx.z;
-  const int v0 = blockIdx.x * TV, c0 = blockIdx.y * 64;
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int c = c0 + lane;
-  const bool cok = c < C;
-  const int* sb = start + (size_t)b * (V + 1);
-  const float* xb = xs + (size_t)b * n * C + (cok ? c : 0);
-  const int r2 = r * r;
-  if constexpr (TAPS == 8) {
-    const int k = w;
-    const int dx = k >> 2, dy = (k >> 1) & 1, dz = k & 1;
-    const int off = dx * r2 + dy * r + dz;
-    const float* wb = ws8 + (size_t)b * n * 8 + k;
-    for (int vi = 0; vi < TV; ++vi) {
-      const int v = v0 + vi;
-      float acc = 0.0f;
-      if (v < V) {
-        const int X = v / r2, Y = (v / r) % r, Z = v % r;
-        if (X >= dx && Y >= dy && Z >= dz) {
-          const int q = v - off;
-          int j = sb[q];
-          const int e = sb[q + 1];
-          for (; j + 4 <= e; j += 4) {
-            const float x0 = xb[(size_t)j * C], x1 = xb[(size_t)(j + 1) * C];
-            const float x2 = xb[(size_t)(j + 2) * C], x3 = xb[(size_t)(j + 3) * C];
-            const float w0 = wb[(size_t)j * 8], w1 = wb[(size_t)(j + 1) * 8];
-            const float w2 = wb[(size_t)(j + 2) * 8], w3 = wb[(size_t)(j + 3) * 8];
-            acc = acc + w0 * x0;
-            acc = acc + w1 * x1;
-            acc = acc + w2 * x2;
-            acc = acc + w3 * x3;
-          }
-          for (; j < e; ++j) acc = acc + wb[(size_t)j * 8] * xb[(size_t)j * C];
-        }
+struct TileRanges {
+  static constexpr int NR = TAPS == 8 ? 4 : 1;
+  int rs[NR], re[NR], nch[NR];
+  int total;
+  // every lane of the wave ends with the same (wave-uniform) values
+  __device__ __forceinline__ TileRanges(const int* sb, int v0, int TV, int V, int r, int lane) {
+    int bnd = 0;
+    if (lane < 2 * NR) {
+      const int g = lane >> 1;
+      int lo = v0, hi = v0 + TV;
+      if constexpr (TAPS == 8) {
+        const int off = (g >> 1) * r * r + (g & 1) * r;
+        lo = v0 - off - 1;
+        hi = v0 + TV - off;
       }
-      part[(k * TV + vi) * 65 + lane] = acc;
+      bnd = sb[min(max((lane & 1) ? hi : lo, 0), V)];
     }
-  } else {
-    for (int vi = w; vi < TV; vi += (int)(blockDim.x >> 6)) {
-      const int v = v0 + vi;
-      float acc = 0.0f;
-      if (v < V) {
-        int j = sb[v];
-        const int e = sb[v + 1];
-        for (; j + 4 <= e; j += 4) {
-          const float x0 = xb[(size_t)j * C], x1 = xb[(size_t)(j + 1) * C];
-          const float x2 = xb[(size_t)(j + 2) * C], x3 = xb[(size_t)(j + 3) * C];
-          acc = acc + x0;
-          acc = acc + x1;
-          acc = acc + x2;
-          acc = acc + x3;
-        }
-        for (; j < e; ++j) acc = acc + xb[(size_t)j * C];
-      }
-      part[vi * 65 + lane] = acc;
+    total = 0;
+#pragma unroll
+    for (int g = 0; g < NR; ++g) {
+      rs[g] = __builtin_amdgcn_readlane(bnd, 2 * g);
+      re[g] = __builtin_amdgcn_readlane(bnd, 2 * g + 1);
+      nch[g] = (re[g] - rs[g] + kChunk - 1) / kChunk;
+      total += nch[g];
     }
   }
+  __device__ __forceinline__ int parts_used(int P) const {
+    return min(P, (total + kWaves - 1) / kWaves);
+  }
+};
+
+template <int TAPS>
+__device__ __forceinline__ void seg_flush(float* part, int slot0, int TV, int lane, float a0,
+                                          float a1) {
+  if ((unsigned)slot0 < (unsigned)TV) part[slot0 * 65 + lane] += a0;
+  if constexpr (TAPS == 8) {
+    if ((unsigned)(slot0 + 1) < (unsigned)TV) part[(slot0 + 1) * 65 + lane] += a1;
+  }
+}
+
+__device__ __forceinline__ float rl_f(float v, int l) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+}
+
+template <int TAPS>
+__global__ void __launch_bounds__(kWaves * 64)
+    seg_range_gather_kernel(const float* __restrict__ xt, const int* __restrict__ perm,
+                            const int* __restrict__ skey, const float* __restrict__ tapw,
+                            const int* __restrict__ start, const float* __restrict__ vscale,
+                            int C, int n, int V, int r, int TV, int P, float* __restrict__ out,
+                            float* __restrict__ partial) {
+  extern __shared__ __attribute__((aligned(16))) float part[];  // [kWaves][TV][65]
+  constexpr int NR = TileRanges<TAPS>::NR;
+  const int b = blockIdx.z;
+  const int tile = blockIdx.x / P, pp = blockIdx.x - tile * P;
+  const int v0 = tile * TV, c0 = blockIdx.y * 64;
+  // readfirstlane: tells the compiler the wave index is uniform, so the whole
+  // chunk walk below stays scalar (no exec-mask branches, no vmcnt(0) stalls
+  // between the row loads)
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int c = c0 + lane;
+  const bool cok = c < C;
+  const int* __restrict__ sb = start + (size_t)b * (V + 1);
+  const TileRanges<TAPS> tr(sb, v0, TV, V, r, lane);
+  if (pp > 0 && pp >= tr.parts_used(P)) return;  // block-uniform
+  const int* __restrict__ pb = perm + (size_t)b * n;
+  const int* __restrict__ kb = skey + (size_t)b * n;
+  const float* __restrict__ xb = xt + (size_t)b * n * C + (cok ? c : 0);
+  const float* __restrict__ wb = TAPS == 8 ? tapw + (size_t)b * 8 * n : nullptr;
+  const float* __restrict__ vb = vscale != nullptr ? vscale + (size_t)b * V : nullptr;
+
+  for (int e = threadIdx.x; e < kWaves * TV * 65; e += kWaves * 64) part[e] = 0.0f;
   __syncthreads();
-  // out[b, c0 + cc, v0 + vi] = sum_k part[k][vi][cc], k in order
-  const int nthreads = blockDim.x;
-  for (int e = threadIdx.x; e < 64 * TV; e += nthreads) {
+  float* mypart = part + w * TV * 65;
+  for (int t = pp * kWaves + w; t < tr.total; t += P * kWaves) {
+    // chunk t -> (range g, chunk tt within it)
+    int g = 0, tt = t;
+#pragma unroll
+    for (int q = 0; q < NR - 1; ++q) {
+      if (g == q && tt >= tr.nch[q]) {
+        tt -= tr.nch[q];
+        g = q + 1;
+      }
+    }
+    int s = 0, e = 0, off = 0;
+#pragma unroll
+    for (int q = 0; q < NR; ++q) {
+      if (g == q) {
+        s = tr.rs[q] + tt * kChunk;
+        e = min(tr.re[q], s + kChunk);
+        if constexpr (TAPS == 8) off = (q >> 1) * r * r + (q & 1) * r;
+      }
+    }
+    const int slot_base = off - v0;
+    int cur = -1;
+    float a0 = 0.0f, a1 = 0.0f, sc = 1.0f;
+    for (int base = s; base < e; base += 64) {
+      const int m = min(64, e - base);
+      const bool act = lane < m;
+      const int pv = act ? pb[base + lane] : 0;
+      const int kv = act ? kb[base + lane] : -1;
+      float w0v = 0.0f, w1v = 0.0f;
+      if constexpr (TAPS == 8) {
+        if (act) {  // taps k = 4dx + 2dy + dz = 2g + dz of wgts [b, 8, n]
+          w0v = wb[(size_t)(2 * g) * n + pv];
+          w1v = wb[(size_t)(2 * g + 1) * n + pv];
+        }
+      }
+      for (int u0 = 0; u0 < m; u0 += kInFlight) {
+        const int cnt = min(kInFlight, m - u0);
+        float x[kInFlight];
+        // unconditional: lanes >= m hold pv = 0, a valid row
+#pragma unroll
+        for (int q = 0; q < kInFlight; ++q)
+          x[q] = xb[(size_t)__builtin_amdgcn_readlane(pv, u0 + q) * C];
+#pragma unroll
+        for (int q = 0; q < kInFlight; ++q) {
+          if (q < cnt) {
+            const int key = __builtin_amdgcn_readlane(kv, u0 + q);
+            if (key != cur) {
+              if (cur >= 0) seg_flush<TAPS>(mypart, cur + slot_base, TV, lane, a0, a1);
+              cur = key;
+              a0 = 0.0f;
+              a1 = 0.0f;
+              if constexpr (TAPS == 1) sc = vb != nullptr ? vb[key] : 1.0f;
+            }
+            if constexpr (TAPS == 8) {
+              a0 = a0 + rl_f(w0v, u0 + q) * x[q];
+              a1 = a1 + rl_f(w1v, u0 + q) * x[q];
+            } else {
+              a0 = vb != nullptr ? a0 + x[q] * sc : a0 + x[q];
+            }
+          }
+        }
+      }
+    }
+    if (cur >= 0) seg_flush<TAPS>(mypart, cur + slot_base, TV, lane, a0, a1);
+  }
+  __syncthreads();
+  float* dst = pp == 0 ? out : partial + (size_t)(pp - 1) * gridDim.z * C * V;
+  for (int e = threadIdx.x; e < 64 * TV; e += kWaves * 64) {
     const int cc = e / TV, vi = e - cc * TV;
     const int cg = c0 + cc, v = v0 + vi;
     if (cg < C && v < V) {
-      float s = part[vi * 65 + cc];
+      float sum = part[vi * 65 + cc];
 #pragma unroll
-      for (int k = 1; k < TAPS; ++k) s = s + part[(k * TV + vi) * 65 + cc];
-      out[((size_t)b * C + cg) * V + v] = s;
+      for (int q = 1; q < kWaves; ++q) sum = sum + part[(q * TV + vi) * 65 + cc];
+      dst[((size_t)b * C + cg) * V + v] = sum;
+    }
+  }
+}
+
+// out += partial[0 .. used-2] for the tiles that were split over several parts.
+// grid = (ceil(V/TV), ceil(C/64), B), 256 threads.
+template <int TAPS>
+__global__ void __launch_bounds__(256)
+    seg_part_sum_kernel(const int* __restrict__ start, const float* __restrict__ partial, int C,
+                        int V, int r, int TV, int P, float* __restrict__ out) {
+  const int b = blockIdx.z;
+  const int v0 = blockIdx.x * TV, c0 = blockIdx.y * 64;
+  const TileRanges<TAPS> tr(start + (size_t)b * (V + 1), v0, TV, V, r, threadIdx.x & 63);
+  const int used = tr.parts_used(P);
+  if (used <= 1) return;
+  const size_t pstride = (size_t)gridDim.z * C * V;
+  for (int e = threadIdx.x; e < 64 * TV; e += 256) {
+    const int cc = e / TV, vi = e - cc * TV;
+    const int cg = c0 + cc, v = v0 + vi;
+    if (cg < C && v < V) {
+      const size_t o = ((size_t)b * C + cg) * V + v;
+      float sum = out[o];
+      for (int q = 0; q < used - 1; ++q) sum = sum + partial[q * pstride + o];
+      out[o] = sum;
     }
   }
 }
@@ -239,83 +365,75 @@ __global__ void __launch_bounds__(512)
 // --------------------------------------------------------------------------
 // host driver
 // --------------------------------------------------------------------------
-struct SegWs {
-  int* start;   // B*(V+1)
-  int* cursor;  // B*V
-  int* perm;    // B*n
-  int* cnt;     // B*V (when the caller does not own one)
-  float* xs;    // B*n*C
-  float* ws8;   // B*n*8 (TAPS == 8)
-};
-
 inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
+inline int seg_tile_voxels(int V) { return V >= 4096 ? 32 : 16; }
+// parts per tile: small grids (coarse voxel grids hold the dense cells) split more
+inline int seg_parts(int V) { return V <= 4096 ? 16 : 4; }
+
+struct SegWs {
+  int* start;      // B*(V+1)
+  float* vinv;     // B*V (per-voxel 1/cnt)
+  int* perm;       // B*n
+  int* skey;       // B*n
+  float* xt;       // B*n*C
+  float* partial;  // (P-1)*B*C*V
+};
+
 inline size_t seg_ws_bytes(int B, int C, int n, int V, int taps) {
-  size_t s = 0;
-  s += align256((size_t)B * (V + 1) * 4);
+  size_t s = align256((size_t)B * (V + 1) * 4);
   s += align256((size_t)B * V * 4);
-  s += align256((size_t)B * n * 4);
-  s += align256((size_t)B * V * 4);
+  s += 2 * align256((size_t)B * n * 4);
   s += align256((size_t)B * n * std::max(C, 1) * 4);
-  if (taps == 8) s += align256((size_t)B * n * 8 * 4);
+  s += align256((size_t)(seg_parts(V) - 1) * B * C * V * 4);
   return s;
 }
 
 inline SegWs seg_ws_carve(void* ws, int B, int C, int n, int V, int taps) {
   char* p = (char*)ws;
+  auto take = [&p](size_t bytes) {
+    char* q = p;
+    p += align256(bytes);
+    return q;
+  };
   SegWs w;
-  w.start = (int*)p;
-  p += align256((size_t)B * (V + 1) * 4);
-  w.cursor = (int*)p;
-  p += align256((size_t)B * V * 4);
-  w.perm = (int*)p;
-  p += align256((size_t)B * n * 4);
-  w.cnt = (int*)p;
-  p += align256((size_t)B * V * 4);
-  w.xs = (float*)p;
-  p += align256((size_t)B * n * std::max(C, 1) * 4);
-  w.ws8 = taps == 8 ? (float*)p : nullptr;
+  w.start = (int*)take((size_t)B * (V + 1) * 4);
+  w.vinv = (float*)take((size_t)B * V * 4);
+  w.perm = (int*)take((size_t)B * n * 4);
+  w.skey = (int*)take((size_t)B * n * 4);
+  w.xt = (float*)take((size_t)B * n * std::max(C, 1) * 4);
+  w.partial = (float*)take((size_t)(seg_parts(V) - 1) * B * C * V * 4);
   return w;
 }
 
-inline int seg_tile_voxels(int V) { return V >= 32768 ? 32 : (V >= 4096 ? 16 : 8); }
-
-// out[b, c, v] = sum over items i with key(i) (+ stencil offset) = v of w * in[b, c, i].
-//   key: [b, key_bstride] ints (first n used); cnt: [b, V] counts if already
-//   computed by the caller (nullptr: computed here into the workspace).
+// out[b, c, v] = sum over items i whose key (+ stencil offset) is v of the tap term.
+//   key: ints at key + b*key_bstride (first n used); cnt_out: [b, V] counts are
+//   written there when non-null; avg: scale by 1/cnt[v] (average pooling);
+//   tapw: [b, 8, n] trilinear weights (TAPS == 8).
 template <int TAPS>
-inline int seg_scatter(const float* in, const int* key, long long key_bstride,
-                       const float* scale, const float* tapw, int r, int B, int C, int n, int V,
-                       const int* cnt, float* out, void* ws, hipStream_t st, const char* what) {
-  if (B == 0 || C == 0 || V == 0) return PCFM_OK;
+inline int seg_scatter(const float* in, const int* key, long long key_bstride, bool avg,
+                       const float* tapw, int r, int B, int C, int n, int V, int* cnt_out,
+                       float* out, void* ws, hipStream_t st, const char* what) {
+  if (B == 0 || V == 0) return PCFM_OK;
   SegWs w = seg_ws_carve(ws, B, C, n, V, TAPS);
-  hipError_t he = hipSuccess;
-  if (cnt == nullptr) {
-    he = hipMemsetAsync(w.cnt, 0, (size_t)B * V * 4, st);
-    if (he == hipSuccess && n > 0)
-      hipLaunchKernelGGL(seg_count_kernel, dim3(ceil_div(n, 256), B), dim3(256), 0, st, key,
-                         key_bstride, n, V, w.cnt);
-    cnt = w.cnt;
-  }
-  if (he == hipSuccess && n > 0) he = hipMemsetAsync(w.perm, 0xff, (size_t)B * n * 4, st);
-  if (he != hipSuccess) {
-    set_error("%s: hipMemsetAsync: %s", what, hipGetErrorString(he));
-    return (int)he;
-  }
-  hipLaunchKernelGGL(seg_scan_kernel, dim3(B), dim3(1024), 0, st, cnt, V, w.start, w.cursor);
-  if (n > 0) {
-    hipLaunchKernelGGL(seg_place_kernel, dim3(ceil_div(n, 256), B), dim3(256), 0, st, key,
-                       key_bstride, n, V, w.cursor, w.perm);
-    hipLaunchKernelGGL(seg_gather_t_kernel, dim3(ceil_div(n, 64), ceil_div(C, 64), B),
-                       dim3(256), 0, st, in, w.perm, scale, tapw, C, n, w.xs, w.ws8);
-  }
-  const int TV = seg_tile_voxels(V);
-  const size_t lds = (size_t)TAPS * TV * 65 * sizeof(float);
-  const int threads = TAPS == 8 ? 512 : 256;
-  int e = allow_big_lds((const void*)seg_tap_sum_kernel<TAPS>);
+  const size_t sort_lds = (size_t)std::min(V, kSortKeys) * sizeof(int);
+  int e = allow_big_lds((const void*)seg_sort_kernel);
   if (e) return e;
-  hipLaunchKernelGGL(seg_tap_sum_kernel<TAPS>, dim3(ceil_div(V, TV), ceil_div(C, 64), B),
-                     dim3(threads), lds, st, w.xs, w.ws8, w.start, C, n, V, r, TV, out);
+  hipLaunchKernelGGL(seg_sort_kernel, dim3(B), dim3(1024), sort_lds, st, key, key_bstride, n, V,
+                     w.start, cnt_out, avg ? w.vinv : nullptr, w.perm, w.skey);
+  if (C == 0) return check_launch(what);
+  if (n > 0)
+    hipLaunchKernelGGL(seg_transpose_kernel, dim3(ceil_div(n, 64), ceil_div(C, 64), B),
+                       dim3(256), 0, st, in, C, n, w.xt);
+  const int TV = seg_tile_voxels(V), P = seg_parts(V);
+  const int tiles = ceil_div(V, TV);
+  const size_t lds = (size_t)kWaves * TV * 65 * sizeof(float);
+  hipLaunchKernelGGL(seg_range_gather_kernel<TAPS>, dim3(tiles * P, ceil_div(C, 64), B),
+                     dim3(kWaves * 64), lds, st, w.xt, w.perm, w.skey, tapw, w.start,
+                     avg ? w.vinv : nullptr, C, n, V, r, TV, P, out, w.partial);
+  if (P > 1)
+    hipLaunchKernelGGL(seg_part_sum_kernel<TAPS>, dim3(tiles, ceil_div(C, 64), B), dim3(256), 0,
+                       st, w.start, w.partial, C, V, r, TV, P, out);
   return check_launch(what);
 }
 

@@ -9,32 +9,14 @@
 namespace pcfm {
 namespace {
 
-// ind[b, i] = x*r^2 + y*r + z (vox.cu:31) and the per-voxel histogram (integer
-// atomics: the counts are exact and order-free).  One thread per point, the
-// whole B*N range at once instead of one block per batch element.
+// ind[b, i] = x*r^2 + y*r + z (vox.cu:31); the histogram is built by the sort.
 __global__ void __launch_bounds__(256)
-    vox_count_kernel(const int* __restrict__ coords, int n, int r, int s, int* __restrict__ ind,
-                     int* __restrict__ cnt) {
+    vox_ind_kernel(const int* __restrict__ coords, int n, int r, int* __restrict__ ind) {
   const int b = blockIdx.y;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const int* cb = coords + (size_t)b * 3 * n;
-  const int v = cb[i] * r * r + cb[i + n] * r + cb[i + 2 * n];
-  ind[(size_t)b * n + i] = v;
-  if ((unsigned)v < (unsigned)s) atomicAdd(cnt + (size_t)b * s + v, 1);
-}
-
-// Per-point scale 1/cnt, computed once per point instead of once per
-// (point, channel block): (float)(1.0 / (double)cnt) as vox.cu:66.
-__global__ void __launch_bounds__(256)
-    vox_inv_kernel(const int* __restrict__ ind, const int* __restrict__ cnt, int n, int s,
-                   float* __restrict__ inv) {
-  const int b = blockIdx.y;
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const int v = ind[(size_t)b * n + i];
-  const int c = ((unsigned)v < (unsigned)s) ? cnt[(size_t)b * s + v] : 0;
-  inv[(size_t)b * n + i] = c > 0 ? (float)(1.0 / (double)c) : 0.0f;
+  ind[(size_t)b * n + i] = cb[i] * r * r + cb[i + n] * r + cb[i + 2 * n];
 }
 
 bool cube_fits(int r, int* s) {
@@ -53,7 +35,7 @@ using namespace pcfm;
 extern "C" size_t pcfm_avg_voxelize_fwd_workspace_bytes(int b, int c, int n, int r) {
   int s = 0;
   if (b < 0 || c < 0 || n < 0 || !cube_fits(r, &s)) return 0;
-  return align256((size_t)b * n * sizeof(float)) + seg_ws_bytes(b, c, n, s, 1);
+  return seg_ws_bytes(b, c, n, s, 1);
 }
 
 extern "C" int pcfm_avg_voxelize_fwd(const float* feat, const int* coords, int b, int c, int n,
@@ -67,23 +49,13 @@ extern "C" int pcfm_avg_voxelize_fwd(const float* feat, const int* coords, int b
   PCFM_CHECK_ARG(ws_bytes >= need, "avg_voxelize_fwd: workspace %zu < %zu bytes", ws_bytes, need);
   if (b == 0) return PCFM_OK;
   hipStream_t st = (hipStream_t)stream;
-  hipError_t he = hipMemsetAsync(cnt, 0, (size_t)b * s * sizeof(int), st);
-  if (he != hipSuccess) {
-    set_error("avg_voxelize_fwd: hipMemsetAsync: %s", hipGetErrorString(he));
-    return (int)he;
-  }
-  float* inv = (float*)ws;
-  void* seg = (char*)ws + align256((size_t)b * n * sizeof(float));
-  if (n > 0) {
-    dim3 grid(ceil_div(n, 256), b);
-    hipLaunchKernelGGL(vox_count_kernel, grid, dim3(256), 0, st, coords, n, r, s, ind, cnt);
-    hipLaunchKernelGGL(vox_inv_kernel, grid, dim3(256), 0, st, ind, cnt, n, s, inv);
-    int e = check_launch("avg_voxelize_fwd(count)");
-    if (e) return e;
-  }
-  // out[c, v] = sum_{i in voxel v} feat[c, i] * inv[i]   (per-term product, vox.cu:68)
-  return seg_scatter<1>(feat, ind, n, inv, nullptr, r, b, c, n, s, cnt, out, seg, st,
-                        "avg_voxelize_fwd(segsum)");
+  if (n > 0)
+    hipLaunchKernelGGL(vox_ind_kernel, dim3(ceil_div(n, 256), b), dim3(256), 0, st, coords, n, r,
+                       ind);
+  // cnt = histogram of ind; out[c, v] = sum_{i in voxel v} feat[c, i] * (1/cnt[v])
+  // (per-term product, vox.cu:68)
+  return seg_scatter<1>(feat, ind, n, true, nullptr, r, b, c, n, s, cnt, out, ws, st,
+                        "avg_voxelize_fwd");
 }
 
 extern "C" int pcfm_avg_voxelize_bwd(const float* grad_y, const int* ind, const int* cnt, int b,
@@ -128,6 +100,6 @@ extern "C" int pcfm_trilinear_devoxelize_bwd(const float* grad_y, const int* ind
   // cell q lands on q + (dx r^2 + dy r + dz).  When a fraction is 0 the
   // reference folds that corner onto the low cell with weight exactly 0
   // (trilinear_devox.cu:64-75), so both placements add the same zeros.
-  return seg_scatter<8>(grad_y, inds, 8LL * n, nullptr, wgts, r, b, c, n, s, nullptr, grad_x, ws,
+  return seg_scatter<8>(grad_y, inds, 8LL * n, false, wgts, r, b, c, n, s, nullptr, grad_x, ws,
                         (hipStream_t)stream, "trilinear_devoxelize_bwd");
 }
