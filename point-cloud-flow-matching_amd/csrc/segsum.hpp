@@ -161,65 +161,115 @@ __global__ void __launch_bounds__(256)
 }
 
 // --------------------------------------------------------------------------
-// 5: range gather
+// 5: unit gather.
+//   The output is cut into tiles of kTV consecutive voxels.  Items feeding a
+//   tile form NR contiguous sorted ranges:
 //   TAPS == 8: column g = (dx, dy) in 0..3, off = dx r^2 + dy r.  A point of
 //     cell q adds w[dx,dy,0] * x to voxel q + off and w[dx,dy,1] * x to voxel
-//     q + off + 1; the column's source cells are [v0 - off - 1, v0 + TV - off).
+//     q + off + 1; the column's source cells are [v0 - off - 1, v0 + kTV - off).
 //     (When a fraction is 0 the reference folds that corner onto the low cell
 //     with weight exactly 0, trilinear_devox.cu:64-75, so both placements add
 //     the same zeros.)
-//   TAPS == 1: one range [v0, v0 + TV); a point of cell q adds x * vscale[q]
+//   TAPS == 1: one range [v0, v0 + kTV); a point of cell q adds x * vscale[q]
 //     (or x) to voxel q.
-// A tile's ranges are cut into chunks of kChunk sorted items.  Chunk t goes
-// to part t / kWaves mod P (one block per part) and to wave t mod kWaves in
-// it, so a crowded tile (the centre cells of a Gaussian cloud hold thousands
-// of points at r = 8) is spread over up to P blocks.  Part 0 writes the tile
-// to `out` (zeros if empty); parts 1.. that received chunks write partial
-// tiles that seg_part_sum_kernel adds in part order.  No atomics.
-// grid = (ceil(V/TV) * P, ceil(C/64), B), kWaves waves; LDS = kWaves partial tiles.
+//   A tile with T items (its ranges concatenated) becomes P = ceil(T / kItems)
+//   work units of ~T/P items (at least one, so empty tiles are written as
+//   zeros).  ONE wave runs a unit: it walks its items 64 at a time (one load
+//   round fetches perm / key / tap weights for all 64), reads the 16 next
+//   feature rows back to back through readlane'd row ids, keeps a register
+//   accumulator per tap for the current run of equal target voxels and adds
+//   it into its private LDS tile when the run ends.  Unit 0 of a tile writes
+//   the tile to `out`; units 1.. of a crowded tile write partial tiles that
+//   seg_part_sum_kernel adds in unit order.  Waves never wait for each other
+//   and nothing is atomic.
 // --------------------------------------------------------------------------
-constexpr int kWaves = 4;
-constexpr int kChunk = 128;
-constexpr int kInFlight = 16;  // row loads issued back to back per wave
+constexpr int kTV = 32;          // voxels per tile
+constexpr int kItems = 256;      // target items per work unit
+constexpr int kInFlight = 16;    // feature-row loads issued back to back per wave
+constexpr int kUnitWaves = 4;    // waves (independent units) per block
 
 template <int TAPS>
-struct TileRanges {
-  static constexpr int NR = TAPS == 8 ? 4 : 1;
-  int rs[NR], re[NR], nch[NR];
-  int total;
-  // every lane of the wave ends with the same (wave-uniform) values
-  __device__ __forceinline__ TileRanges(const int* sb, int v0, int TV, int V, int r, int lane) {
-    int bnd = 0;
-    if (lane < 2 * NR) {
-      const int g = lane >> 1;
-      int lo = v0, hi = v0 + TV;
-      if constexpr (TAPS == 8) {
-        const int off = (g >> 1) * r * r + (g & 1) * r;
-        lo = v0 - off - 1;
-        hi = v0 + TV - off;
-      }
-      bnd = sb[min(max((lane & 1) ? hi : lo, 0), V)];
+constexpr int seg_ranges() { return TAPS == 8 ? 4 : 1; }
+
+// Range g of tile v0: lanes 2g / 2g+1 return the sorted positions [lo, hi).
+template <int TAPS>
+__device__ __forceinline__ int seg_range_bound(const int* sb, int v0, int V, int r, int lane) {
+  int bnd = 0;
+  if (lane < 2 * seg_ranges<TAPS>()) {
+    const int g = lane >> 1;
+    int lo = v0, hi = v0 + kTV;
+    if constexpr (TAPS == 8) {
+      const int off = (g >> 1) * r * r + (g & 1) * r;
+      lo = v0 - off - 1;
+      hi = v0 + kTV - off;
     }
-    total = 0;
+    bnd = sb[min(max((lane & 1) ? hi : lo, 0), V)];
+  }
+  return bnd;
+}
+
+// Work-unit list, one block (1024 threads) per batch element:
+//   units[b, u] = {tile, part, parts, items}, tinfo[b, tile] = {parts, first
+//   partial slot}, nunits[b].
+template <int TAPS>
+__global__ void __launch_bounds__(1024)
+    seg_units_kernel(const int* __restrict__ start, int V, int r, int tiles, int umax,
+                     int4* __restrict__ units, int2* __restrict__ tinfo, int* __restrict__ nunits) {
+  __shared__ int wsum[16];
+  constexpr int NR = seg_ranges<TAPS>();
+  const int b = blockIdx.x;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int* sb = start + (size_t)b * (V + 1);
+  int carry = 0;
+  for (int t0 = 0; t0 < tiles; t0 += 1024) {
+    const int tile = t0 + t;
+    int T = 0, P = 0;
+    if (tile < tiles) {
+      const int v0 = tile * kTV;
 #pragma unroll
-    for (int g = 0; g < NR; ++g) {
-      rs[g] = __builtin_amdgcn_readlane(bnd, 2 * g);
-      re[g] = __builtin_amdgcn_readlane(bnd, 2 * g + 1);
-      nch[g] = (re[g] - rs[g] + kChunk - 1) / kChunk;
-      total += nch[g];
+      for (int g = 0; g < NR; ++g) {
+        int lo = v0, hi = v0 + kTV;
+        if constexpr (TAPS == 8) {
+          const int off = (g >> 1) * r * r + (g & 1) * r;
+          lo = v0 - off - 1;
+          hi = v0 + kTV - off;
+        }
+        T += sb[min(max(hi, 0), V)] - sb[min(max(lo, 0), V)];
+      }
+      P = max(1, (T + kItems - 1) / kItems);
     }
+    int x = P;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(x, o, 64);
+      if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[w] = x;
+    __syncthreads();
+    int ofs = carry, total = 0;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      const int s = wsum[g];
+      ofs += g < w ? s : 0;
+      total += s;
+    }
+    const int U = ofs + x - P;
+    if (tile < tiles) {
+      tinfo[(size_t)b * tiles + tile] = make_int2(P, U - tile);
+      for (int p = 0; p < P && U + p < umax; ++p)
+        units[(size_t)b * umax + U + p] = make_int4(tile, p, P, T);
+    }
+    carry += total;
+    __syncthreads();
   }
-  __device__ __forceinline__ int parts_used(int P) const {
-    return min(P, (total + kWaves - 1) / kWaves);
-  }
-};
+  if (t == 0) nunits[b] = min(carry, umax);
+}
 
 template <int TAPS>
-__device__ __forceinline__ void seg_flush(float* part, int slot0, int TV, int lane, float a0,
-                                          float a1) {
-  if ((unsigned)slot0 < (unsigned)TV) part[slot0 * 65 + lane] += a0;
+__device__ __forceinline__ void seg_flush(float* tl, int slot, int lane, float a0, float a1) {
+  if ((unsigned)slot < (unsigned)kTV) tl[slot * 65 + lane] += a0;
   if constexpr (TAPS == 8) {
-    if ((unsigned)(slot0 + 1) < (unsigned)TV) part[(slot0 + 1) * 65 + lane] += a1;
+    if ((unsigned)(slot + 1) < (unsigned)kTV) tl[(slot + 1) * 65 + lane] += a1;
   }
 }
 
@@ -227,134 +277,147 @@ __device__ __forceinline__ float rl_f(float v, int l) {
   return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
 }
 
+// grid = (ceil(umax / kUnitWaves), ceil(C/64), B), kUnitWaves * 64 threads.
 template <int TAPS>
-__global__ void __launch_bounds__(kWaves * 64)
-    seg_range_gather_kernel(const float* __restrict__ xt, const int* __restrict__ perm,
-                            const int* __restrict__ skey, const float* __restrict__ tapw,
-                            const int* __restrict__ start, const float* __restrict__ vscale,
-                            int C, int n, int V, int r, int TV, int P, float* __restrict__ out,
-                            float* __restrict__ partial) {
-  extern __shared__ __attribute__((aligned(16))) float part[];  // [kWaves][TV][65]
-  constexpr int NR = TileRanges<TAPS>::NR;
-  const int b = blockIdx.z;
-  const int tile = blockIdx.x / P, pp = blockIdx.x - tile * P;
-  const int v0 = tile * TV, c0 = blockIdx.y * 64;
-  // readfirstlane: tells the compiler the wave index is uniform, so the whole
-  // chunk walk below stays scalar (no exec-mask branches, no vmcnt(0) stalls
-  // between the row loads)
+__global__ void __launch_bounds__(kUnitWaves * 64)
+    seg_unit_gather_kernel(const float* __restrict__ xt, const int* __restrict__ perm,
+                           const int* __restrict__ skey, const float* __restrict__ tapw,
+                           const int* __restrict__ start, const float* __restrict__ vscale,
+                           const int4* __restrict__ units, const int* __restrict__ nunits, int C,
+                           int n, int V, int r, int umax, int slots, float* __restrict__ out,
+                           float* __restrict__ partial) {
+  __shared__ float lds[kUnitWaves][kTV * 65];
+  constexpr int NR = seg_ranges<TAPS>();
+  const int b = blockIdx.z, c0 = blockIdx.y * 64;
+  // readfirstlane: the wave index is uniform, so the whole walk stays scalar
+  // (no exec-mask branches, no vmcnt(0) stalls between the row loads)
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
+  const int u = blockIdx.x * kUnitWaves + w;
+  if (u >= nunits[b]) return;  // wave-uniform; no block barrier below
+  const int4 un = units[(size_t)b * umax + u];
+  const int tile = un.x, part = un.y, parts = un.z, T = un.w;
+  const int v0 = tile * kTV;
   const int c = c0 + lane;
   const bool cok = c < C;
   const int* __restrict__ sb = start + (size_t)b * (V + 1);
-  const TileRanges<TAPS> tr(sb, v0, TV, V, r, lane);
-  if (pp > 0 && pp >= tr.parts_used(P)) return;  // block-uniform
   const int* __restrict__ pb = perm + (size_t)b * n;
   const int* __restrict__ kb = skey + (size_t)b * n;
   const float* __restrict__ xb = xt + (size_t)b * n * C + (cok ? c : 0);
   const float* __restrict__ wb = TAPS == 8 ? tapw + (size_t)b * 8 * n : nullptr;
-  const float* __restrict__ vb = vscale != nullptr ? vscale + (size_t)b * V : nullptr;
 
-  for (int e = threadIdx.x; e < kWaves * TV * 65; e += kWaves * 64) part[e] = 0.0f;
-  __syncthreads();
-  float* mypart = part + w * TV * 65;
-  for (int t = pp * kWaves + w; t < tr.total; t += P * kWaves) {
-    // chunk t -> (range g, chunk tt within it)
-    int g = 0, tt = t;
+  const int bnd = seg_range_bound<TAPS>(sb, v0, V, r, lane);
+  int rs[NR], pre[NR + 1], offg[NR];
+  pre[0] = 0;
 #pragma unroll
-    for (int q = 0; q < NR - 1; ++q) {
-      if (g == q && tt >= tr.nch[q]) {
-        tt -= tr.nch[q];
-        g = q + 1;
-      }
-    }
-    int s = 0, e = 0, off = 0;
+  for (int g = 0; g < NR; ++g) {
+    rs[g] = __builtin_amdgcn_readlane(bnd, 2 * g);
+    pre[g + 1] = pre[g] + __builtin_amdgcn_readlane(bnd, 2 * g + 1) - rs[g];
+    offg[g] = TAPS == 8 ? (g >> 1) * r * r + (g & 1) * r : 0;
+  }
+  const int i0 = (int)((long long)T * part / parts);
+  const int i1 = (int)((long long)T * (part + 1) / parts);
+  float vs = 0.0f;  // TAPS == 1 average pool: lane l holds 1/cnt of voxel v0 + l
+  if (TAPS == 1 && vscale != nullptr && lane < kTV && v0 + lane < V)
+    vs = vscale[(size_t)b * V + v0 + lane];
+
+  float* tl = lds[w];
+  for (int e = lane; e < kTV * 65; e += 64) tl[e] = 0.0f;
+
+  int cur = -1000;
+  float a0 = 0.0f, a1 = 0.0f, sc = 1.0f;
+  for (int base = i0; base < i1; base += 64) {
+    const int m = min(64, i1 - base);
+    const int it = base + lane;
+    int pv = 0, sl = -1000;
+    float w0v = 0.0f, w1v = 0.0f;
+    if (lane < m) {
+      int g = 0;
 #pragma unroll
-    for (int q = 0; q < NR; ++q) {
-      if (g == q) {
-        s = tr.rs[q] + tt * kChunk;
-        e = min(tr.re[q], s + kChunk);
-        if constexpr (TAPS == 8) off = (q >> 1) * r * r + (q & 1) * r;
-      }
-    }
-    const int slot_base = off - v0;
-    int cur = -1;
-    float a0 = 0.0f, a1 = 0.0f, sc = 1.0f;
-    for (int base = s; base < e; base += 64) {
-      const int m = min(64, e - base);
-      const bool act = lane < m;
-      const int pv = act ? pb[base + lane] : 0;
-      const int kv = act ? kb[base + lane] : -1;
-      float w0v = 0.0f, w1v = 0.0f;
-      if constexpr (TAPS == 8) {
-        if (act) {  // taps k = 4dx + 2dy + dz = 2g + dz of wgts [b, 8, n]
-          w0v = wb[(size_t)(2 * g) * n + pv];
-          w1v = wb[(size_t)(2 * g + 1) * n + pv];
+      for (int q = 1; q < NR; ++q) g += it >= pre[q] ? 1 : 0;
+      int pos = 0, off = 0, gs = 0;
+#pragma unroll
+      for (int q = 0; q < NR; ++q)
+        if (g == q) {
+          pos = rs[q] + it - pre[q];
+          off = offg[q];
+          gs = q;
         }
+      pv = pb[pos];
+      sl = kb[pos] + off - v0;
+      if constexpr (TAPS == 8) {  // taps k = 4dx + 2dy + dz = 2g + dz of wgts [b, 8, n]
+        w0v = wb[(size_t)(2 * gs) * n + pv];
+        w1v = wb[(size_t)(2 * gs + 1) * n + pv];
       }
-      for (int u0 = 0; u0 < m; u0 += kInFlight) {
-        const int cnt = min(kInFlight, m - u0);
-        float x[kInFlight];
-        // unconditional: lanes >= m hold pv = 0, a valid row
+    }
+    for (int u0 = 0; u0 < m; u0 += kInFlight) {
+      float x[kInFlight];
+      // unconditional: lanes >= m hold pv = 0, a valid row
 #pragma unroll
-        for (int q = 0; q < kInFlight; ++q)
-          x[q] = xb[(size_t)__builtin_amdgcn_readlane(pv, u0 + q) * C];
+      for (int q = 0; q < kInFlight; ++q)
+        x[q] = xb[(size_t)__builtin_amdgcn_readlane(pv, u0 + q) * C];
+      const int cnt = min(kInFlight, m - u0);
 #pragma unroll
-        for (int q = 0; q < kInFlight; ++q) {
-          if (q < cnt) {
-            const int key = __builtin_amdgcn_readlane(kv, u0 + q);
-            if (key != cur) {
-              if (cur >= 0) seg_flush<TAPS>(mypart, cur + slot_base, TV, lane, a0, a1);
-              cur = key;
-              a0 = 0.0f;
-              a1 = 0.0f;
-              if constexpr (TAPS == 1) sc = vb != nullptr ? vb[key] : 1.0f;
-            }
-            if constexpr (TAPS == 8) {
-              a0 = a0 + rl_f(w0v, u0 + q) * x[q];
-              a1 = a1 + rl_f(w1v, u0 + q) * x[q];
-            } else {
-              a0 = vb != nullptr ? a0 + x[q] * sc : a0 + x[q];
-            }
+      for (int q = 0; q < kInFlight; ++q) {
+        if (q < cnt) {
+          const int slot = __builtin_amdgcn_readlane(sl, u0 + q);
+          if (slot != cur) {
+            seg_flush<TAPS>(tl, cur, lane, a0, a1);
+            cur = slot;
+            a0 = 0.0f;
+            a1 = 0.0f;
+            if constexpr (TAPS == 1) sc = rl_f(vs, slot & 63);
+          }
+          if constexpr (TAPS == 8) {
+            a0 = a0 + rl_f(w0v, u0 + q) * x[q];
+            a1 = a1 + rl_f(w1v, u0 + q) * x[q];
+          } else {
+            a0 = vscale != nullptr ? a0 + x[q] * sc : a0 + x[q];
           }
         }
       }
     }
-    if (cur >= 0) seg_flush<TAPS>(mypart, cur + slot_base, TV, lane, a0, a1);
   }
-  __syncthreads();
-  float* dst = pp == 0 ? out : partial + (size_t)(pp - 1) * gridDim.z * C * V;
-  for (int e = threadIdx.x; e < 64 * TV; e += kWaves * 64) {
-    const int cc = e / TV, vi = e - cc * TV;
-    const int cg = c0 + cc, v = v0 + vi;
-    if (cg < C && v < V) {
-      float sum = part[vi * 65 + cc];
-#pragma unroll
-      for (int q = 1; q < kWaves; ++q) sum = sum + part[(q * TV + vi) * 65 + cc];
-      dst[((size_t)b * C + cg) * V + v] = sum;
-    }
+  seg_flush<TAPS>(tl, cur, lane, a0, a1);
+
+  // tile -> global, 2 channels x 32 voxels (2 x 128 B) per store instruction
+  float* dst;
+  size_t cstride, bofs;
+  if (part == 0) {
+    dst = out + v0;
+    cstride = (size_t)V;
+    bofs = (size_t)b * C * V;
+  } else {  // partial slot: units of tiles before this one beyond their first, + part - 1
+    dst = partial;
+    cstride = (size_t)kTV;
+    bofs = ((size_t)b * slots + (size_t)(u - tile - 1)) * C * kTV;
+  }
+  const int vi = lane & (kTV - 1), ch = lane / kTV;
+  const bool vok = part > 0 || v0 + vi < V;
+#pragma unroll 4
+  for (int k = 0; k < 64; k += 64 / kTV) {
+    const int cc = k + ch, cg = c0 + cc;
+    if (cg < C && vok) dst[bofs + (size_t)cg * cstride + vi] = tl[vi * 65 + cc];
   }
 }
 
-// out += partial[0 .. used-2] for the tiles that were split over several parts.
-// grid = (ceil(V/TV), ceil(C/64), B), 256 threads.
-template <int TAPS>
+// out += partial tiles 1 .. P-1 of every crowded tile, in unit order.
+// grid = (tiles, ceil(C/64), B), 256 threads.
 __global__ void __launch_bounds__(256)
-    seg_part_sum_kernel(const int* __restrict__ start, const float* __restrict__ partial, int C,
-                        int V, int r, int TV, int P, float* __restrict__ out) {
-  const int b = blockIdx.z;
-  const int v0 = blockIdx.x * TV, c0 = blockIdx.y * 64;
-  const TileRanges<TAPS> tr(start + (size_t)b * (V + 1), v0, TV, V, r, threadIdx.x & 63);
-  const int used = tr.parts_used(P);
-  if (used <= 1) return;
-  const size_t pstride = (size_t)gridDim.z * C * V;
-  for (int e = threadIdx.x; e < 64 * TV; e += 256) {
-    const int cc = e / TV, vi = e - cc * TV;
+    seg_part_sum_kernel(const int2* __restrict__ tinfo, const float* __restrict__ partial,
+                        int C, int V, int tiles, int slots, float* __restrict__ out) {
+  const int b = blockIdx.z, tile = blockIdx.x, c0 = blockIdx.y * 64;
+  const int2 ti = tinfo[(size_t)b * tiles + tile];
+  if (ti.x <= 1) return;
+  const int v0 = tile * kTV;
+  for (int e = threadIdx.x; e < 64 * kTV; e += 256) {
+    const int cc = e / kTV, vi = e - cc * kTV;
     const int cg = c0 + cc, v = v0 + vi;
     if (cg < C && v < V) {
       const size_t o = ((size_t)b * C + cg) * V + v;
       float sum = out[o];
-      for (int q = 0; q < used - 1; ++q) sum = sum + partial[q * pstride + o];
+      for (int p = 1; p < ti.x; ++p)
+        sum = sum + partial[(((size_t)b * slots + ti.y + p - 1) * C + cg) * kTV + vi];
       out[o] = sum;
     }
   }
@@ -367,29 +430,40 @@ __global__ void __launch_bounds__(256)
 // --------------------------------------------------------------------------
 inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
-inline int seg_tile_voxels(int V) { return V >= 4096 ? 32 : 16; }
-// parts per tile: small grids (coarse voxel grids hold the dense cells) split more
-inline int seg_parts(int V) { return V <= 4096 ? 16 : 4; }
+// Upper bound of work units per batch element: one per tile plus one per
+// kItems of range items (an item lies in at most 2 tiles per stencil column).
+inline int seg_tiles(int V) { return (V + kTV - 1) / kTV; }
+inline int seg_umax(int n, int V, int taps) {
+  return seg_tiles(V) + (int)(((long long)(taps == 8 ? 8 : 1) * n + kItems - 1) / kItems) + 1;
+}
 
 struct SegWs {
   int* start;      // B*(V+1)
   float* vinv;     // B*V (per-voxel 1/cnt)
   int* perm;       // B*n
   int* skey;       // B*n
+  int4* units;     // B*umax
+  int2* tinfo;     // B*tiles
+  int* nunits;     // B
   float* xt;       // B*n*C
-  float* partial;  // (P-1)*B*C*V
+  float* partial;  // B*slots*C*kTV
 };
 
 inline size_t seg_ws_bytes(int B, int C, int n, int V, int taps) {
+  const int umax = seg_umax(n, V, taps), tiles = seg_tiles(V);
   size_t s = align256((size_t)B * (V + 1) * 4);
   s += align256((size_t)B * V * 4);
   s += 2 * align256((size_t)B * n * 4);
+  s += align256((size_t)B * umax * 16);
+  s += align256((size_t)B * tiles * 8);
+  s += align256((size_t)B * 4);
   s += align256((size_t)B * n * std::max(C, 1) * 4);
-  s += align256((size_t)(seg_parts(V) - 1) * B * C * V * 4);
+  s += align256((size_t)B * (umax - tiles) * std::max(C, 1) * kTV * 4);
   return s;
 }
 
 inline SegWs seg_ws_carve(void* ws, int B, int C, int n, int V, int taps) {
+  const int umax = seg_umax(n, V, taps), tiles = seg_tiles(V);
   char* p = (char*)ws;
   auto take = [&p](size_t bytes) {
     char* q = p;
@@ -401,8 +475,11 @@ inline SegWs seg_ws_carve(void* ws, int B, int C, int n, int V, int taps) {
   w.vinv = (float*)take((size_t)B * V * 4);
   w.perm = (int*)take((size_t)B * n * 4);
   w.skey = (int*)take((size_t)B * n * 4);
+  w.units = (int4*)take((size_t)B * umax * 16);
+  w.tinfo = (int2*)take((size_t)B * tiles * 8);
+  w.nunits = (int*)take((size_t)B * 4);
   w.xt = (float*)take((size_t)B * n * std::max(C, 1) * 4);
-  w.partial = (float*)take((size_t)(seg_parts(V) - 1) * B * C * V * 4);
+  w.partial = (float*)take((size_t)B * (umax - tiles) * std::max(C, 1) * kTV * 4);
   return w;
 }
 
@@ -422,18 +499,18 @@ inline int seg_scatter(const float* in, const int* key, long long key_bstride, b
   hipLaunchKernelGGL(seg_sort_kernel, dim3(B), dim3(1024), sort_lds, st, key, key_bstride, n, V,
                      w.start, cnt_out, avg ? w.vinv : nullptr, w.perm, w.skey);
   if (C == 0) return check_launch(what);
+  const int tiles = seg_tiles(V), umax = seg_umax(n, V, TAPS), slots = umax - tiles;
+  hipLaunchKernelGGL(seg_units_kernel<TAPS>, dim3(B), dim3(1024), 0, st, w.start, V, r, tiles,
+                     umax, w.units, w.tinfo, w.nunits);
   if (n > 0)
     hipLaunchKernelGGL(seg_transpose_kernel, dim3(ceil_div(n, 64), ceil_div(C, 64), B),
                        dim3(256), 0, st, in, C, n, w.xt);
-  const int TV = seg_tile_voxels(V), P = seg_parts(V);
-  const int tiles = ceil_div(V, TV);
-  const size_t lds = (size_t)kWaves * TV * 65 * sizeof(float);
-  hipLaunchKernelGGL(seg_range_gather_kernel<TAPS>, dim3(tiles * P, ceil_div(C, 64), B),
-                     dim3(kWaves * 64), lds, st, w.xt, w.perm, w.skey, tapw, w.start,
-                     avg ? w.vinv : nullptr, C, n, V, r, TV, P, out, w.partial);
-  if (P > 1)
-    hipLaunchKernelGGL(seg_part_sum_kernel<TAPS>, dim3(tiles, ceil_div(C, 64), B), dim3(256), 0,
-                       st, w.start, w.partial, C, V, r, TV, P, out);
+  hipLaunchKernelGGL(seg_unit_gather_kernel<TAPS>,
+                     dim3(ceil_div(umax, kUnitWaves), ceil_div(C, 64), B), dim3(kUnitWaves * 64),
+                     0, st, w.xt, w.perm, w.skey, tapw, w.start, avg ? w.vinv : nullptr, w.units,
+                     w.nunits, C, n, V, r, umax, slots, out, w.partial);
+  hipLaunchKernelGGL(seg_part_sum_kernel, dim3(tiles, ceil_div(C, 64), B), dim3(256), 0, st,
+                     w.tinfo, w.partial, C, V, tiles, slots, out);
   return check_launch(what);
 }
 

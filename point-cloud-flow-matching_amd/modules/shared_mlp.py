@@ -20,8 +20,16 @@ class PointwiseConv1d(nn.Conv1d):
         if self.kernel_size != (1,) or self.groups != 1 or self.stride != (1,) \
                 or self.padding not in ((0,), "valid") or self.dilation != (1,):
             return super().forward(x)
-        y = torch.matmul(self.weight[:, :, 0], x)
-        return y if self.bias is None else y + self.bias[:, None]
+        if x.dim() != 3:
+            return super().forward(x)
+        # bmm against the batch-broadcast weight: the result is a contiguous
+        # (B, C_out, N) tensor (torch.matmul(2-D, 3-D) returns a transposed view,
+        # which turns every following BatchNorm/ReLU/add into a strided kernel),
+        # and the bias is folded into the GEMM's C operand.
+        w = self.weight[:, :, 0].unsqueeze(0).expand(x.shape[0], -1, -1)
+        if self.bias is None:
+            return torch.bmm(w, x)
+        return torch.baddbmm(self.bias[None, :, None], w, x)
 
 
 _KINDS = {1: (PointwiseConv1d, nn.BatchNorm1d), 2: (nn.Conv2d, nn.BatchNorm2d)}
