@@ -38,6 +38,19 @@ import torch.distributed as dist  # noqa: E402
 METRIC = "train-step points/sec (B=8, N=20000, xyz+rgb) at 1/2/4/8 MI355X; Chamfer ms"
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 H100_DERIVED_PTS = 1.88e6       # 25 s/epoch at <= 293 steps/epoch (derived)
+# HBM bytes per launch of the voxel ops from rocprofv3 PMC passes (tools/op_traffic.py)
+TRAFFIC_FILE = os.path.join(REPO, "profiles", "r01_traffic.json")
+
+
+def measured_traffic(op):
+    """Mean PMC traffic per launch of `op` over the bench's three stage shapes
+    (each runs twice per step), or None when no PMC summary is committed."""
+    try:
+        data = json.load(open(TRAFFIC_FILE))["ops"]
+    except (OSError, ValueError, KeyError):
+        return None
+    vals = [v["traffic_bytes"] for k, v in data.items() if k.split("@")[0] == op]
+    return sum(vals) / len(vals) if len(vals) == 3 else None
 
 
 def log(*a):
@@ -183,9 +196,11 @@ def main():
             dom = max(summary, key=lambda k: summary[k]["ms"])
             d = summary[dom]
             achieved = d["bytes"] / (d["ms"] * 1e-3) / 1e9
+            traffic = measured_traffic(dom)
             roofline = {"kernel": dom, "bound": "hbm", "achieved": achieved,
                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                        "traffic": None,
+                        "traffic": traffic, "traffic_unit": "bytes per launch (PMC, "
+                        "profiles/r01_traffic.json)" if traffic else None,
                         "algorithmic_bytes_per_launch": d["bytes"] / d["launches"],
                         "avg_launch_ms": d["ms"] / d["launches"]}
         log(f"{ms:.2f} ms/step, {value / 1e6:.3f} M points/s; losses {loss_p:.4f} {loss_z:.4f}")

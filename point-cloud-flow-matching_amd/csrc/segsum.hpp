@@ -415,9 +415,18 @@ __global__ void __launch_bounds__(256)
     const int cg = c0 + cc, v = v0 + vi;
     if (cg < C && v < V) {
       const size_t o = ((size_t)b * C + cg) * V + v;
+      const float* pp = partial + (((size_t)b * slots + ti.y) * C + cg) * kTV + vi;
+      const size_t ps = (size_t)C * kTV;  // one partial tile
       float sum = out[o];
-      for (int p = 1; p < ti.x; ++p)
-        sum = sum + partial[(((size_t)b * slots + ti.y + p - 1) * C + cg) * kTV + vi];
+      int p = 0;
+      for (; p + 8 <= ti.x - 1; p += 8) {  // 8 independent loads in flight, summed in order
+        float x[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) x[q] = pp[(size_t)(p + q) * ps];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) sum = sum + x[q];
+      }
+      for (; p < ti.x - 1; ++p) sum = sum + pp[(size_t)p * ps];
       out[o] = sum;
     }
   }
