@@ -1,32 +1,31 @@
 // Sorted, atomic-free scatter ("segment sum") for the PVConv path.
 //
-// Measured on MI355X (tools/voxel_probe.py): an LDS float atomic (ds_add_f32)
-// costs ~200 cycles per wave instruction whatever the address pattern, so an
-// LDS-privatised scatter with one atomic per (item, channel, tap) runs at
-// 0.15-0.9 TB/s.  The scatters are recast as gathers over items sorted by
-// their target cell:
+// The reference scatters with one float atomic per (item, channel, tap)
+// (vox.cu:48-72, trilinear_devox.cu:119-162, grouping.cu:58-77).  On MI355X a
+// device-scope float atomic executes at the memory side (~1.3 TB/s of added
+// bytes chip-wide) and an LDS float atomic costs ~200 cycles per wave
+// instruction (measured, tools/voxel_probe.py), so the scatters are recast as
+// gathers over items sorted by their target cell:
 //
-//   1-3. counting sort, one block per batch element, histogram in LDS:
-//      start[b, 0..V] (exclusive prefix of the counts) and perm / skey at
-//      start[key] + rank
-//   4. transpose  xt[b, i, c] = in[b, c, i]       channels-last rows, item order
-//   5. range gather, output-stationary per voxel tile, lanes = 64 channels.
-//      The items feeding a tile [v0, v0+TV) through stencil column (dx, dy)
-//      are ONE contiguous sorted range (cells v0-off-1 .. v0+TV-off-1 are
-//      consecutive keys), so a wave streams that range, keeps one register
-//      accumulator per dz tap for the current run of equal keys, and flushes
-//      it into its own LDS partial tile when the key changes.  Ranges are cut
-//      into chunks shared round robin by the block's waves and, for crowded
-//      tiles, by up to P blocks (a dense r=8 cell holds thousands of points);
-//      partial tiles are summed in a fixed order and leave as coalesced rows.
-//      No atomics in the data path.
+//   1. seg_sort     counting sort, one block per batch element, histogram in
+//                   LDS: start[b, 0..V] and rank[b, i] (sorted position of
+//                   item i; written coalesced, in item order)
+//   2. seg_units    tiles of kTV voxels -> balanced work units (device-built)
+//   3. seg_rows     xs[b, rank[i], :] = in[b, :, i]: channels-last rows in
+//                   SORTED order, plus the item's key and tap weights at the
+//                   same sorted position (the main loop then streams
+//                   contiguous memory and chases no index)
+//   4. seg_unit_gather  output-stationary, lanes = 64 channels: one wave per
+//                   unit, register run-accumulators per tap flushed into a
+//                   wave-private LDS tile, coalesced tile store
+//   5. seg_part_sum adds the partial tiles of tiles split over several units
 //
 // Used by avg_voxelize forward (key = voxel, term = feat * (1/cnt)),
 // trilinear devoxelize backward (key = base cell inds[b,0,:], term = wgt * g
 // for the 8 corners) and grouping backward (key = neighbour index, term = g).
-// The order of items inside one key comes from step 3's atomics, so float sums
-// are order-nondeterministic at the last bit -- exactly like the reference's
-// float atomics.
+// The order of items inside one key comes from the sort's LDS atomics, so
+// float sums are order-nondeterministic at the last bit -- exactly like the
+// reference's float atomics.
 #pragma once
 
 #include <algorithm>
@@ -37,15 +36,15 @@ namespace pcfm {
 namespace {  // kernels get internal linkage: this header is included by several .hip files
 
 // --------------------------------------------------------------------------
-// 1-3: counting sort by key, one block (1024 threads) per batch element.
+// 1: counting sort by key, one block (1024 threads) per batch element.
 // The key histogram lives in LDS (kSortKeys ints = 128 KiB; larger key spaces
 // take several passes over the keys), so counting and ranking use LDS atomics
-// only -- device-scope global atomics cost ~5 G/s on this part (measured:
-// 160K of them took ~30 us), an LDS atomic a few hundred cycles per wave.
+// only.
 //   start[b, 0..V]  exclusive prefix of the counts (start[b, V] = total)
 //   cnt_out[b, v]   the counts (optional: the voxelization's `cnt` output)
 //   vinv[b, v]      (float)(1.0 / (double)cnt) (optional, vox.cu:66)
-//   perm/skey[b, pos]  item and key at pos = start[key] + (arrival rank)
+//   rank[b, i]      start[key_i] + arrival rank within the key; -1 when the
+//                   key is outside [0, V) (the item contributes nothing)
 // --------------------------------------------------------------------------
 constexpr int kSortKeys = 32768;
 constexpr int kSortBatch = 8;  // keys per thread in flight
@@ -53,13 +52,14 @@ constexpr int kSortBatch = 8;  // keys per thread in flight
 __global__ void __launch_bounds__(1024)
     seg_sort_kernel(const int* __restrict__ key, long long key_bstride, int n, int V,
                     int* __restrict__ start, int* __restrict__ cnt_out, float* __restrict__ vinv,
-                    int* __restrict__ perm, int* __restrict__ skey) {
+                    int* __restrict__ rank) {
   extern __shared__ int hist[];  // [min(V, kSortKeys)]
   __shared__ int wsum[16];
   const int b = blockIdx.x;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int* __restrict__ kb = key + (size_t)b * key_bstride;
   int* __restrict__ sb = start + (size_t)b * (V + 1);
+  int* __restrict__ rb = rank + (size_t)b * n;
   int carry = 0;
   for (int k0 = 0; k0 < V; k0 += kSortKeys) {
     const int len = min(kSortKeys, V - k0);
@@ -75,7 +75,8 @@ __global__ void __launch_bounds__(1024)
 #pragma unroll
       for (int q = 0; q < kSortBatch; ++q)
         if ((unsigned)kk[q] < (unsigned)len) atomicAdd(hist + kk[q], 1);
-    }    __syncthreads();
+    }
+    __syncthreads();
     // exclusive scan: wave w owns the 64-aligned segment [lo, hi)
     const int seg = ((len + 15) / 16 + 63) & ~63;
     const int lo = min(len, w * seg), hi = min(len, lo + seg);
@@ -120,12 +121,9 @@ __global__ void __launch_bounds__(1024)
       }
 #pragma unroll
       for (int q = 0; q < kSortBatch; ++q) {
-        if ((unsigned)kk[q] < (unsigned)len) {
-          const int pos = atomicAdd(hist + kk[q], 1);
-          const size_t o = (size_t)b * n + pos;
-          perm[o] = i0 + q * 1024 + t;
-          skey[o] = kk[q] + k0;
-        }
+        const int i = i0 + q * 1024 + t;
+        if ((unsigned)kk[q] < (unsigned)len) rb[i] = atomicAdd(hist + kk[q], 1);
+        else if (k0 == 0 && i < n && (unsigned)(kk[q] + k0) >= (unsigned)V) rb[i] = -1;
       }
     }
     carry += total;
@@ -135,33 +133,81 @@ __global__ void __launch_bounds__(1024)
 }
 
 // --------------------------------------------------------------------------
-// 4: transpose the item features to channels-last rows, ORIGINAL item order:
-//    xt[b, i, c] = in[b, c, i]   (64x64 LDS tiles; 256-B reads and writes)
+// 3: rows in sorted order.  xs[b, rank[i], c] = in[b, c, i] (64 x 64 LDS
+// tile: 256-B coalesced reads along i, one 256-B row segment per store).
+// Blocks of channel group 0 also write skey[b, rank[i]] = key[i] and, for the
+// trilinear stencil, ws8[b, rank[i], k] = tapw[b, k, i].
 // grid = (ceil(n/64), ceil(C/64), B), 256 threads.
 // --------------------------------------------------------------------------
+#ifndef PCFM_ROWS_ITEMS
+#define PCFM_ROWS_ITEMS 64
+#endif
+constexpr int kRowsItems = PCFM_ROWS_ITEMS;  // items per block (64 or 128)
+
 __global__ void __launch_bounds__(256)
-    seg_transpose_kernel(const float* __restrict__ in, int C, int n, float* __restrict__ xt) {
-  __shared__ float tile[64][65];
+    seg_rows_kernel(const float* __restrict__ in, const int* __restrict__ rank,
+                    const int* __restrict__ key, long long key_bstride,
+                    const float* __restrict__ tapw, int C, int n, float* __restrict__ xs,
+                    int* __restrict__ skey, float* __restrict__ ws8) {
+  __shared__ float tile[64][kRowsItems + 1];
+  __shared__ int rk[kRowsItems];
   const int b = blockIdx.z;
-  const int j0 = blockIdx.x * 64, c0 = blockIdx.y * 64;
+  const int j0 = blockIdx.x * kRowsItems, c0 = blockIdx.y * 64;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int j = j0 + lane;
-  for (int cc = w; cc < 64; cc += 4) {
-    const int c = c0 + cc;
-    tile[cc][lane] = (c < C && j < n) ? in[((size_t)b * C + c) * n + j] : 0.0f;
+  for (int jj = threadIdx.x; jj < kRowsItems; jj += 256) {
+    const int j = j0 + jj;
+    const int r = j < n ? rank[(size_t)b * n + j] : -1;
+    rk[jj] = r;
+    if (blockIdx.y == 0 && r >= 0) {
+      const size_t o = (size_t)b * n + r;
+      skey[o] = key[(size_t)b * key_bstride + j];
+      if (tapw != nullptr) {
+        const float* tb = tapw + (size_t)b * 8 * n + j;
+        float4* d = reinterpret_cast<float4*>(ws8 + o * 8);
+        d[0] = make_float4(tb[0], tb[(size_t)n], tb[(size_t)2 * n], tb[(size_t)3 * n]);
+        d[1] = make_float4(tb[(size_t)4 * n], tb[(size_t)5 * n], tb[(size_t)6 * n],
+                           tb[(size_t)7 * n]);
+      }
+    }
+  }
+  if constexpr (kRowsItems == 128) {
+    // one wave reads 128 items of a channel row as float2 (512 B)
+    const int j = j0 + 2 * lane;
+    const bool vec = (n & 1) == 0 && j + 1 < n;
+    for (int cc = w; cc < 64; cc += 4) {
+      const int c = c0 + cc;
+      float2 v = make_float2(0.0f, 0.0f);
+      if (c < C) {
+        const float* src = in + ((size_t)b * C + c) * n + j;
+        if (vec) {
+          v = *reinterpret_cast<const float2*>(src);
+        } else {
+          if (j < n) v.x = src[0];
+          if (j + 1 < n) v.y = src[1];
+        }
+      }
+      tile[cc][2 * lane] = v.x;
+      tile[cc][2 * lane + 1] = v.y;
+    }
+  } else {
+    const int j = j0 + lane;
+    for (int cc = w; cc < 64; cc += 4) {
+      const int c = c0 + cc;
+      tile[cc][lane] = (c < C && j < n) ? in[((size_t)b * C + c) * n + j] : 0.0f;
+    }
   }
   __syncthreads();
   const int c = c0 + lane;
   if (c < C) {
-    for (int jr = w; jr < 64; jr += 4) {
-      const int jj = j0 + jr;
-      if (jj < n) xt[((size_t)b * n + jj) * C + c] = tile[lane][jr];
+    for (int jr = w; jr < kRowsItems; jr += 4) {
+      const int r = rk[jr];
+      if (r >= 0) xs[((size_t)b * n + r) * C + c] = tile[lane][jr];
     }
   }
 }
 
 // --------------------------------------------------------------------------
-// 5: unit gather.
+// 2 + 4 + 5: units, unit gather, partial sums.
 //   The output is cut into tiles of kTV consecutive voxels.  Items feeding a
 //   tile form NR contiguous sorted ranges:
 //   TAPS == 8: column g = (dx, dy) in 0..3, off = dx r^2 + dy r.  A point of
@@ -174,16 +220,18 @@ __global__ void __launch_bounds__(256)
 //     (or x) to voxel q.
 //   A tile with T items (its ranges concatenated) becomes P = ceil(T / kItems)
 //   work units of ~T/P items (at least one, so empty tiles are written as
-//   zeros).  ONE wave runs a unit: it walks its items 64 at a time (one load
-//   round fetches perm / key / tap weights for all 64), reads the 16 next
-//   feature rows back to back through readlane'd row ids, keeps a register
-//   accumulator per tap for the current run of equal target voxels and adds
-//   it into its private LDS tile when the run ends.  Unit 0 of a tile writes
-//   the tile to `out`; units 1.. of a crowded tile write partial tiles that
-//   seg_part_sum_kernel adds in unit order.  Waves never wait for each other
-//   and nothing is atomic.
+//   zeros).  ONE wave runs a unit: per 64 items one load round fetches the
+//   sorted keys and tap weights, the 16 next feature rows (consecutive rows
+//   of xs) are loaded back to back, a register accumulator per tap runs over
+//   equal target voxels and is added into the wave's private LDS tile when the
+//   voxel changes.  Unit 0 of a tile writes the tile to `out`; units 1.. of a
+//   crowded tile write partial tiles that seg_part_sum_kernel adds in unit
+//   order.  Waves never wait for each other and nothing is atomic.
 // --------------------------------------------------------------------------
-constexpr int kTV = 32;          // voxels per tile
+#ifndef PCFM_KTV
+#define PCFM_KTV 16
+#endif
+constexpr int kTV = PCFM_KTV;    // voxels per tile
 constexpr int kItems = 256;      // target items per work unit
 constexpr int kInFlight = 16;    // feature-row loads issued back to back per wave
 constexpr int kUnitWaves = 4;    // waves (independent units) per block
@@ -265,12 +313,24 @@ __global__ void __launch_bounds__(1024)
   if (t == 0) nunits[b] = min(carry, umax);
 }
 
+// Run bookkeeping: when a run of equal target voxels starts, the tile's
+// current partials for its slots are READ (p0, p1) without waiting; when it
+// ends, p + acc is written back.  The LDS read latency then hides behind the
+// run's row loads instead of stalling every flush (LDS ops of one wave stay in
+// order, so a read of slot s+1 after the previous run's write of s+1 sees it).
 template <int TAPS>
-__device__ __forceinline__ void seg_flush(float* tl, int slot, int lane, float a0, float a1) {
-  if ((unsigned)slot < (unsigned)kTV) tl[slot * 65 + lane] += a0;
+__device__ __forceinline__ void seg_run_end(float* tl, int slot, int lane, float p0, float p1,
+                                            float a0, float a1) {
+  if ((unsigned)slot < (unsigned)kTV) tl[slot * 65 + lane] = p0 + a0;
   if constexpr (TAPS == 8) {
-    if ((unsigned)(slot + 1) < (unsigned)kTV) tl[(slot + 1) * 65 + lane] += a1;
+    if ((unsigned)(slot + 1) < (unsigned)kTV) tl[(slot + 1) * 65 + lane] = p1 + a1;
   }
+}
+template <int TAPS>
+__device__ __forceinline__ void seg_run_begin(const float* tl, int slot, int lane, float& p0,
+                                              float& p1) {
+  p0 = (unsigned)slot < (unsigned)kTV ? tl[slot * 65 + lane] : 0.0f;
+  if constexpr (TAPS == 8) p1 = (unsigned)(slot + 1) < (unsigned)kTV ? tl[(slot + 1) * 65 + lane] : 0.0f;
 }
 
 __device__ __forceinline__ float rl_f(float v, int l) {
@@ -280,12 +340,11 @@ __device__ __forceinline__ float rl_f(float v, int l) {
 // grid = (ceil(umax / kUnitWaves), ceil(C/64), B), kUnitWaves * 64 threads.
 template <int TAPS>
 __global__ void __launch_bounds__(kUnitWaves * 64)
-    seg_unit_gather_kernel(const float* __restrict__ xt, const int* __restrict__ perm,
-                           const int* __restrict__ skey, const float* __restrict__ tapw,
-                           const int* __restrict__ start, const float* __restrict__ vscale,
-                           const int4* __restrict__ units, const int* __restrict__ nunits, int C,
-                           int n, int V, int r, int umax, int slots, float* __restrict__ out,
-                           float* __restrict__ partial) {
+    seg_unit_gather_kernel(const float* __restrict__ xs, const int* __restrict__ skey,
+                           const float* __restrict__ ws8, const int* __restrict__ start,
+                           const float* __restrict__ vscale, const int4* __restrict__ units,
+                           const int* __restrict__ nunits, int C, int n, int V, int r, int umax,
+                           int slots, float* __restrict__ out, float* __restrict__ partial) {
   __shared__ float lds[kUnitWaves][kTV * 65];
   constexpr int NR = seg_ranges<TAPS>();
   const int b = blockIdx.z, c0 = blockIdx.y * 64;
@@ -293,27 +352,30 @@ __global__ void __launch_bounds__(kUnitWaves * 64)
   // (no exec-mask branches, no vmcnt(0) stalls between the row loads)
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
+  // natural block order: the 4 units of a block are consecutive tiles and the
+  // tile 32 units back (stencil columns dx = 1) ran 8 blocks earlier on the
+  // same XCD, so column re-reads mostly hit L2 (an XCD-contiguous deal
+  // measured 1.5-1.9x slower)
+  const int nu = nunits[b];
   const int u = blockIdx.x * kUnitWaves + w;
-  if (u >= nunits[b]) return;  // wave-uniform; no block barrier below
+  if (u >= nu) return;  // wave-uniform; no block barrier below
   const int4 un = units[(size_t)b * umax + u];
   const int tile = un.x, part = un.y, parts = un.z, T = un.w;
   const int v0 = tile * kTV;
   const int c = c0 + lane;
   const bool cok = c < C;
   const int* __restrict__ sb = start + (size_t)b * (V + 1);
-  const int* __restrict__ pb = perm + (size_t)b * n;
   const int* __restrict__ kb = skey + (size_t)b * n;
-  const float* __restrict__ xb = xt + (size_t)b * n * C + (cok ? c : 0);
-  const float* __restrict__ wb = TAPS == 8 ? tapw + (size_t)b * 8 * n : nullptr;
+  const float* __restrict__ xb = xs + (size_t)b * n * C + (cok ? c : 0);
+  const float* __restrict__ wb = TAPS == 8 ? ws8 + (size_t)b * n * 8 : nullptr;
 
   const int bnd = seg_range_bound<TAPS>(sb, v0, V, r, lane);
-  int rs[NR], pre[NR + 1], offg[NR];
+  int rs[NR], pre[NR + 1];
   pre[0] = 0;
 #pragma unroll
   for (int g = 0; g < NR; ++g) {
     rs[g] = __builtin_amdgcn_readlane(bnd, 2 * g);
     pre[g + 1] = pre[g] + __builtin_amdgcn_readlane(bnd, 2 * g + 1) - rs[g];
-    offg[g] = TAPS == 8 ? (g >> 1) * r * r + (g & 1) * r : 0;
   }
   const int i0 = (int)((long long)T * part / parts);
   const int i1 = (int)((long long)T * (part + 1) / parts);
@@ -325,45 +387,46 @@ __global__ void __launch_bounds__(kUnitWaves * 64)
   for (int e = lane; e < kTV * 65; e += 64) tl[e] = 0.0f;
 
   int cur = -1000;
-  float a0 = 0.0f, a1 = 0.0f, sc = 1.0f;
+  float a0 = 0.0f, a1 = 0.0f, p0 = 0.0f, p1 = 0.0f, sc = 1.0f;
   for (int base = i0; base < i1; base += 64) {
     const int m = min(64, i1 - base);
     const int it = base + lane;
-    int pv = 0, sl = -1000;
+    int pos = 0, sl = -1000;
     float w0v = 0.0f, w1v = 0.0f;
     if (lane < m) {
       int g = 0;
 #pragma unroll
       for (int q = 1; q < NR; ++q) g += it >= pre[q] ? 1 : 0;
-      int pos = 0, off = 0, gs = 0;
+      int off = 0, gs = 0;
 #pragma unroll
       for (int q = 0; q < NR; ++q)
         if (g == q) {
           pos = rs[q] + it - pre[q];
-          off = offg[q];
+          off = TAPS == 8 ? (q >> 1) * r * r + (q & 1) * r : 0;
           gs = q;
         }
-      pv = pb[pos];
       sl = kb[pos] + off - v0;
-      if constexpr (TAPS == 8) {  // taps k = 4dx + 2dy + dz = 2g + dz of wgts [b, 8, n]
-        w0v = wb[(size_t)(2 * gs) * n + pv];
-        w1v = wb[(size_t)(2 * gs + 1) * n + pv];
+      if constexpr (TAPS == 8) {  // taps k = 4dx + 2dy + dz = 2g + dz
+        const float2 ww = *reinterpret_cast<const float2*>(wb + (size_t)pos * 8 + 2 * gs);
+        w0v = ww.x;
+        w1v = ww.y;
       }
     }
     for (int u0 = 0; u0 < m; u0 += kInFlight) {
       float x[kInFlight];
-      // unconditional: lanes >= m hold pv = 0, a valid row
+      // unconditional: lanes >= m hold pos = 0, a valid row
 #pragma unroll
       for (int q = 0; q < kInFlight; ++q)
-        x[q] = xb[(size_t)__builtin_amdgcn_readlane(pv, u0 + q) * C];
+        x[q] = xb[(size_t)__builtin_amdgcn_readlane(pos, u0 + q) * C];
       const int cnt = min(kInFlight, m - u0);
 #pragma unroll
       for (int q = 0; q < kInFlight; ++q) {
         if (q < cnt) {
           const int slot = __builtin_amdgcn_readlane(sl, u0 + q);
           if (slot != cur) {
-            seg_flush<TAPS>(tl, cur, lane, a0, a1);
+            seg_run_end<TAPS>(tl, cur, lane, p0, p1, a0, a1);
             cur = slot;
+            seg_run_begin<TAPS>(tl, cur, lane, p0, p1);
             a0 = 0.0f;
             a1 = 0.0f;
             if constexpr (TAPS == 1) sc = rl_f(vs, slot & 63);
@@ -378,7 +441,7 @@ __global__ void __launch_bounds__(kUnitWaves * 64)
       }
     }
   }
-  seg_flush<TAPS>(tl, cur, lane, a0, a1);
+  seg_run_end<TAPS>(tl, cur, lane, p0, p1, a0, a1);
 
   // tile -> global, 2 channels x 32 voxels (2 x 128 B) per store instruction
   float* dst;
@@ -449,12 +512,13 @@ inline int seg_umax(int n, int V, int taps) {
 struct SegWs {
   int* start;      // B*(V+1)
   float* vinv;     // B*V (per-voxel 1/cnt)
-  int* perm;       // B*n
+  int* rank;       // B*n
   int* skey;       // B*n
+  float* ws8;      // B*n*8 (TAPS == 8)
   int4* units;     // B*umax
   int2* tinfo;     // B*tiles
   int* nunits;     // B
-  float* xt;       // B*n*C
+  float* xs;       // B*n*C
   float* partial;  // B*slots*C*kTV
 };
 
@@ -463,6 +527,7 @@ inline size_t seg_ws_bytes(int B, int C, int n, int V, int taps) {
   size_t s = align256((size_t)B * (V + 1) * 4);
   s += align256((size_t)B * V * 4);
   s += 2 * align256((size_t)B * n * 4);
+  if (taps == 8) s += align256((size_t)B * n * 8 * 4);
   s += align256((size_t)B * umax * 16);
   s += align256((size_t)B * tiles * 8);
   s += align256((size_t)B * 4);
@@ -482,12 +547,13 @@ inline SegWs seg_ws_carve(void* ws, int B, int C, int n, int V, int taps) {
   SegWs w;
   w.start = (int*)take((size_t)B * (V + 1) * 4);
   w.vinv = (float*)take((size_t)B * V * 4);
-  w.perm = (int*)take((size_t)B * n * 4);
+  w.rank = (int*)take((size_t)B * n * 4);
   w.skey = (int*)take((size_t)B * n * 4);
+  w.ws8 = taps == 8 ? (float*)take((size_t)B * n * 8 * 4) : nullptr;
   w.units = (int4*)take((size_t)B * umax * 16);
   w.tinfo = (int2*)take((size_t)B * tiles * 8);
   w.nunits = (int*)take((size_t)B * 4);
-  w.xt = (float*)take((size_t)B * n * std::max(C, 1) * 4);
+  w.xs = (float*)take((size_t)B * n * std::max(C, 1) * 4);
   w.partial = (float*)take((size_t)B * (umax - tiles) * std::max(C, 1) * kTV * 4);
   return w;
 }
@@ -506,18 +572,21 @@ inline int seg_scatter(const float* in, const int* key, long long key_bstride, b
   int e = allow_big_lds((const void*)seg_sort_kernel);
   if (e) return e;
   hipLaunchKernelGGL(seg_sort_kernel, dim3(B), dim3(1024), sort_lds, st, key, key_bstride, n, V,
-                     w.start, cnt_out, avg ? w.vinv : nullptr, w.perm, w.skey);
+                     w.start, cnt_out, avg ? w.vinv : nullptr, w.rank);
   if (C == 0) return check_launch(what);
   const int tiles = seg_tiles(V), umax = seg_umax(n, V, TAPS), slots = umax - tiles;
   hipLaunchKernelGGL(seg_units_kernel<TAPS>, dim3(B), dim3(1024), 0, st, w.start, V, r, tiles,
                      umax, w.units, w.tinfo, w.nunits);
   if (n > 0)
-    hipLaunchKernelGGL(seg_transpose_kernel, dim3(ceil_div(n, 64), ceil_div(C, 64), B),
-                       dim3(256), 0, st, in, C, n, w.xt);
-  hipLaunchKernelGGL(seg_unit_gather_kernel<TAPS>,
-                     dim3(ceil_div(umax, kUnitWaves), ceil_div(C, 64), B), dim3(kUnitWaves * 64),
-                     0, st, w.xt, w.perm, w.skey, tapw, w.start, avg ? w.vinv : nullptr, w.units,
-                     w.nunits, C, n, V, r, umax, slots, out, w.partial);
+    hipLaunchKernelGGL(seg_rows_kernel, dim3(ceil_div(n, kRowsItems), ceil_div(C, 64), B),
+                       dim3(256), 0,
+                       st, in, w.rank, key, key_bstride, TAPS == 8 ? tapw : nullptr, C, n, w.xs,
+                       w.skey, w.ws8);
+  const int gx = ceil_div(umax, kUnitWaves);
+  hipLaunchKernelGGL(seg_unit_gather_kernel<TAPS>, dim3(gx, ceil_div(C, 64), B),
+                     dim3(kUnitWaves * 64), 0, st, w.xs, w.skey, w.ws8, w.start,
+                     avg ? w.vinv : nullptr, w.units, w.nunits, C, n, V, r, umax, slots, out,
+                     w.partial);
   hipLaunchKernelGGL(seg_part_sum_kernel, dim3(tiles, ceil_div(C, 64), B), dim3(256), 0, st,
                      w.tinfo, w.partial, C, V, tiles, slots, out);
   return check_launch(what);

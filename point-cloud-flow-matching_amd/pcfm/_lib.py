@@ -14,6 +14,8 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(os.path.dirname(_HERE), "csrc", "libpcfm_hip.so")
+# PCFM_LIB: load a measurement variant built by `make variant` (dev knob)
+LIB_PATH = os.environ.get("PCFM_LIB", LIB_PATH)
 
 _P = ctypes.c_void_p
 _I = ctypes.c_int

@@ -3,7 +3,8 @@
 
     python tools/conv3d_probe.py [variant ...]
 variants: default, cl3d (channels_last_3d), bench (cudnn.benchmark), nocudnn
-(PyTorch's native vol2col + GEMM path).
+(PyTorch's native vol2col + GEMM path); a "+bf16" suffix runs the same in bf16
+and "+cl3d" adds channels_last_3d to any variant.
 """
 import sys
 import time
@@ -14,18 +15,21 @@ SHAPES = [(8, 128, 32), (8, 256, 16), (8, 256, 8)]
 
 
 def run(variant, iters=5):
-    torch.backends.cudnn.enabled = variant != "nocudnn"
-    torch.backends.cudnn.benchmark = variant == "bench"
+    base = variant.split("+")[0]
+    dt = torch.bfloat16 if "+bf16" in variant else torch.float32
+    cl = base == "cl3d" or "+cl3d" in variant
+    torch.backends.cudnn.enabled = base != "nocudnn"
+    torch.backends.cudnn.benchmark = base == "bench"
     torch.backends.cudnn.allow_tf32 = False
     res = {}
     for b, c, r in SHAPES:
-        conv = torch.nn.Conv3d(c, c, 3, padding=1).cuda()
-        x = torch.randn(b, c, r, r, r, device="cuda", requires_grad=True)
-        if variant == "cl3d":
+        conv = torch.nn.Conv3d(c, c, 3, padding=1).cuda().to(dt)
+        x = torch.randn(b, c, r, r, r, device="cuda", dtype=dt, requires_grad=True)
+        if cl:
             conv = conv.to(memory_format=torch.channels_last_3d)
             x = x.detach().to(memory_format=torch.channels_last_3d).requires_grad_(True)
-        gy = torch.randn(b, c, r, r, r, device="cuda")
-        if variant == "cl3d":
+        gy = torch.randn(b, c, r, r, r, device="cuda", dtype=dt)
+        if cl:
             gy = gy.to(memory_format=torch.channels_last_3d)
         t = {}
         for phase in ("fwd", "fwd_bwd"):
