@@ -35,7 +35,7 @@ extern "C" {
 #define PCFM_OK 0
 #define PCFM_EINVAL -1
 
-/* ABI version: bumped on any signature change. */
+/* ABI version: bumped on any signature change (3: voxel convolution). */
 int pcfm_abi_version(void);
 /* Thread-local text of the last non-zero return code. */
 const char* pcfm_last_error(void);
@@ -166,6 +166,45 @@ int pcfm_emd_matchcost_bwd_f64(const double* grad_cost, const double* xyz1,
                                const double* xyz2, const double* match, int b, int n, int m,
                                double* grad1, double* grad2, void* ws, size_t ws_bytes,
                                void* stream);
+
+/* ------------------------------------------------------------------------
+ * Voxel convolution (PVConv's Conv3d, kernel 3, stride 1, padding 1;
+ * third_party/pvcnn/modules/pvconv.py:20-24 -> torch nn.Conv3d / cuDNN).
+ * Implicit GEMM on the bf16 matrix cores with a three-term split of every
+ * fp32 operand (hi + lo bf16; products hi*hi + hi*lo + lo*hi accumulated in
+ * fp32): ~2^-16 relative error per product, vs 2^-11 for the TF32 the
+ * reference's cuDNN path uses by default.  Tensors are NCDHW fp32.
+ * ---------------------------------------------------------------------- */
+
+/* Bytes of a split weight image for a (cout, cin, 3, 3, 3) kernel. */
+size_t pcfm_conv3d_weight_bytes(int cout, int cin);
+
+/* Split + rearrange w f32 [cout][cin][27] into `wsplit`.  transpose = 0: the
+ * forward image [27][cout][cin]; transpose = 1: the backward-data image
+ * [27][cin][cout] with the taps mirrored. */
+int pcfm_conv3d_prep_weight(const float* w, int cout, int cin, int transpose, void* wsplit,
+                            void* stream);
+
+/* 1 if pcfm_conv3d_igemm handles (b, cin, cout, r): cin % 32, cout % 128 and
+ * r^3 % 128 must all be 0. */
+int pcfm_conv3d_supported(int b, int cin, int cout, int r);
+
+/* y[b, cout, r^3] = conv3x3x3(x[b, cin, r^3], w) (+ bias[cout] if non-NULL),
+ * zero padding.  With the transpose=1 image of a (C_out, C_in) kernel and
+ * x = grad_y (cin = C_out, cout = C_in) this is the backward-data pass.
+ * Fully writes y. */
+int pcfm_conv3d_igemm(const float* x, const void* wsplit, const float* bias, int b, int cin,
+                      int cout, int r, float* y, void* stream);
+
+/* Scratch bytes for pcfm_conv3d_wgrad (0 = unsupported shape: cin % 128 is
+ * needed in addition to pcfm_conv3d_supported). */
+size_t pcfm_conv3d_wgrad_workspace_bytes(int b, int cin, int cout, int r);
+
+/* grad_w f32 [cout][cin][27] = sum_{b, v} grad_y[b, co, v] * x[b, ci, v + off(tap)]
+ * (the weight gradient of the padding-1 conv; bf16x3 products, fp32 sums).
+ * Fully writes grad_w (no accumulation). */
+int pcfm_conv3d_wgrad(const float* x, const float* grad_y, int b, int cin, int cout, int r,
+                      float* grad_w, void* ws, size_t ws_bytes, void* stream);
 
 #ifdef __cplusplus
 }

@@ -1,7 +1,8 @@
 """PVConv: point-voxel convolution block.
 
 Reference: third_party/pvcnn/modules/pvconv.py:11-39.  Voxelize (gfx950 scatter
-kernel) -> two Conv3d/BN3d/LeakyReLU(0.1) stages (+ SE) -> trilinear
+kernel) -> two Conv3d/BN3d/LeakyReLU(0.1) stages (+ SE; the 3x3x3 convs run on
+the bf16x3 matrix-core kernels of modules/voxel_conv.py) -> trilinear
 devoxelize (gfx950 gather kernel) -> + pointwise SharedMLP branch.  Modules are
 created in the reference's order, so a given torch seed yields the same
 initial weights, and the state_dict keys (voxel_layers.{0,1,3,4,6.fc.*},
@@ -12,6 +13,7 @@ import torch.nn as nn
 import modules.functional as F
 from modules.se import SE3d
 from modules.shared_mlp import SharedMLP
+from modules.voxel_conv import VoxelConv3d
 from modules.voxelization import Voxelization
 
 __all__ = ["PVConv"]
@@ -19,7 +21,7 @@ __all__ = ["PVConv"]
 
 def _conv_bn_lrelu(cin, cout, kernel_size):
     return [
-        nn.Conv3d(cin, cout, kernel_size, stride=1, padding=kernel_size // 2),
+        VoxelConv3d(cin, cout, kernel_size, stride=1, padding=kernel_size // 2),
         nn.BatchNorm3d(cout, eps=1e-4),
         nn.LeakyReLU(0.1, True),
     ]

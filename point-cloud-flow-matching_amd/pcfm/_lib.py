@@ -46,9 +46,15 @@ SIGNATURES = {
     "pcfm_emd_matchcost_f64": (_I, [_P, _P, _P, _I, _I, _I, _P, _P, _Z, _P]),
     "pcfm_emd_matchcost_bwd_f32": (_I, [_P, _P, _P, _P, _I, _I, _I, _P, _P, _P, _Z, _P]),
     "pcfm_emd_matchcost_bwd_f64": (_I, [_P, _P, _P, _P, _I, _I, _I, _P, _P, _P, _Z, _P]),
+    "pcfm_conv3d_weight_bytes": (_Z, [_I, _I]),
+    "pcfm_conv3d_prep_weight": (_I, [_P, _I, _I, _I, _P, _P]),
+    "pcfm_conv3d_supported": (_I, [_I, _I, _I, _I]),
+    "pcfm_conv3d_igemm": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P]),
+    "pcfm_conv3d_wgrad_workspace_bytes": (_Z, [_I, _I, _I, _I]),
+    "pcfm_conv3d_wgrad": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, _Z, _P]),
 }
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 _lock = threading.Lock()
 _lib = None

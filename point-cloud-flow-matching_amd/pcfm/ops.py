@@ -345,3 +345,77 @@ def matchcost_backward(grad_cost: torch.Tensor, xyz1: torch.Tensor, xyz2: torch.
 emd_cuda = types.SimpleNamespace(approxmatch_forward=approxmatch_forward,
                                  matchcost_forward=matchcost_forward,
                                  matchcost_backward=matchcost_backward)
+
+
+# --------------------------------------------------------------------------
+# Voxel convolution (PVConv's Conv3d k=3 s=1 p=1) on the bf16x3 matrix-core
+# path -- include/pcfm.h "Voxel convolution".
+# --------------------------------------------------------------------------
+def conv3d_wgrad_supported(x: torch.Tensor, weight: torch.Tensor) -> bool:
+    b, cin, r = x.shape[0], x.shape[1], x.shape[2]
+    return _lib.query("pcfm_conv3d_wgrad_workspace_bytes", b, cin, weight.shape[0], r) > 0
+
+
+def conv3d_supported(x: torch.Tensor, weight: torch.Tensor) -> bool:
+    """True if the bf16x3 implicit GEMM handles this (input, weight) pair."""
+    if x.dim() != 5 or weight.dim() != 5 or tuple(weight.shape[2:]) != (3, 3, 3):
+        return False
+    b, cin, d, hh, ww = x.shape
+    if not (d == hh == ww) or weight.shape[1] != cin:
+        return False
+    cout = weight.shape[0]
+    return bool(_lib.query("pcfm_conv3d_supported", b, cin, cout, d)) and \
+        bool(_lib.query("pcfm_conv3d_supported", b, cout, cin, d))
+
+
+def conv3d_prep_weight(weight: torch.Tensor, transpose: bool) -> torch.Tensor:
+    """Split + rearrange a (Cout, Cin, 3, 3, 3) fp32 kernel into the bf16 hi/lo image."""
+    _check(weight, "weight", "f")
+    cout, cin = weight.shape[0], weight.shape[1]
+    w = weight.contiguous()
+    img = torch.empty(_lib.query("pcfm_conv3d_weight_bytes", cout, cin), dtype=torch.uint8,
+                      device=weight.device)
+    _lib.call("pcfm_conv3d_prep_weight", _ptr(w), cout, cin, int(transpose), _ptr(img),
+              _stream(w))
+    return img
+
+
+def conv3d_forward(x: torch.Tensor, weight: torch.Tensor, bias) -> torch.Tensor:
+    """y = conv3d(x, weight, bias, stride 1, padding 1) (NCDHW fp32)."""
+    _check(x, "input", "f")
+    x = x.contiguous()
+    b, cin, r = x.shape[0], x.shape[1], x.shape[2]
+    cout = weight.shape[0]
+    img = conv3d_prep_weight(weight, False)
+    y = torch.empty((b, cout, r, r, r), dtype=torch.float32, device=x.device)
+    bias_p = _ptr(bias.contiguous()) if bias is not None else None
+    _lib.call("pcfm_conv3d_igemm", _ptr(x), _ptr(img), bias_p, b, cin, cout, r, _ptr(y),
+              _stream(x))
+    return y
+
+
+def conv3d_backward_data(grad_y: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
+    """dL/dx of conv3d(x, weight, padding 1) for dL/dy = grad_y."""
+    _check(grad_y, "grad_output", "f")
+    g = grad_y.contiguous()
+    b, cout, r = g.shape[0], g.shape[1], g.shape[2]
+    cin = weight.shape[1]
+    img = conv3d_prep_weight(weight, True)
+    dx = torch.empty((b, cin, r, r, r), dtype=torch.float32, device=g.device)
+    _lib.call("pcfm_conv3d_igemm", _ptr(g), _ptr(img), None, b, cout, cin, r, _ptr(dx),
+              _stream(g))
+    return dx
+
+
+def conv3d_backward_weight(x: torch.Tensor, grad_y: torch.Tensor) -> torch.Tensor:
+    """dL/dW (Cout, Cin, 3, 3, 3) of conv3d(x, W, padding 1) for dL/dy = grad_y."""
+    _check(x, "input", "f")
+    _check(grad_y, "grad_output", "f")
+    x, g = x.contiguous(), grad_y.contiguous()
+    b, cin, r = x.shape[0], x.shape[1], x.shape[2]
+    cout = g.shape[1]
+    ws = _workspace(_lib.query("pcfm_conv3d_wgrad_workspace_bytes", b, cin, cout, r), x)
+    dw = torch.empty((cout, cin, 3, 3, 3), dtype=torch.float32, device=x.device)
+    _lib.call("pcfm_conv3d_wgrad", _ptr(x), _ptr(g), b, cin, cout, r, _ptr(dw), _ptr(ws),
+              ws.numel(), _stream(x))
+    return dw
