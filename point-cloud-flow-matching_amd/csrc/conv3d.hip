@@ -122,18 +122,24 @@ __device__ __forceinline__ void tile_mfma(const uint16_t* buf, int wr, int wc, i
   }
 }
 
-// split N consecutive fp32 (same LDS row) into the hi and lo images
+// split N consecutive fp32 (same LDS row) into the hi and lo images.  The
+// (__bf16) casts round to nearest even and lower to gfx950's packed
+// v_cvt_pk_bf16_f32 (one instruction per pair), hi is widened back exactly.
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 template <int N>
 __device__ __forceinline__ void store_split(const float (&v)[N], uint16_t* dh, uint16_t* dl) {
   uint32_t* h32 = reinterpret_cast<uint32_t*>(dh);
   uint32_t* l32 = reinterpret_cast<uint32_t*>(dl);
 #pragma unroll
   for (int q = 0; q < N / 2; ++q) {
-    uint32_t h0, l0, h1, l1;
-    split_bf16(v[2 * q], h0, l0);
-    split_bf16(v[2 * q + 1], h1, l1);
-    h32[q] = h0 | (h1 << 16);
-    l32[q] = l0 | (l1 << 16);
+    bf16x2 hi;
+    hi.x = (__bf16)v[2 * q];
+    hi.y = (__bf16)v[2 * q + 1];
+    bf16x2 lo;
+    lo.x = (__bf16)(v[2 * q] - (float)hi.x);
+    lo.y = (__bf16)(v[2 * q + 1] - (float)hi.y);
+    h32[q] = __builtin_bit_cast(uint32_t, hi);
+    l32[q] = __builtin_bit_cast(uint32_t, lo);
   }
 }
 
@@ -337,10 +343,16 @@ __global__ void __launch_bounds__(256)
   __syncthreads();
   for (long long ks = k0; ks < k1; ++ks) {
     uint16_t* cur = lds + (kNBuf == 2 ? ((ks - k0) & 1) * T::BUF : 0);
+#ifndef PCFM_EXP_NOLOAD
     if (ks + 1 < k1) load(ks + 1);
+#endif
+#ifndef PCFM_EXP_NOMFMA
     tile_mfma<128, 128>(cur, wr, wc, r, h, acc);
+#endif
     if constexpr (kNBuf == 1) __syncthreads();
+#ifndef PCFM_EXP_NOLOAD
     if (ks + 1 < k1) store(lds + (kNBuf == 2 ? ((ks + 1 - k0) & 1) * T::BUF : 0));
+#endif
     __syncthreads();
   }
   // partial[s][tap][co][ci]: column ci = lane & 31 -> coalesced rows
