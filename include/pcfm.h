@@ -35,7 +35,7 @@ extern "C" {
 #define PCFM_OK 0
 #define PCFM_EINVAL -1
 
-/* ABI version: bumped on any signature change (3: voxel convolution). */
+/* ABI version: bumped on any signature change (4: voxel and pointwise convolution). */
 int pcfm_abi_version(void);
 /* Thread-local text of the last non-zero return code. */
 const char* pcfm_last_error(void);
@@ -205,6 +205,31 @@ size_t pcfm_conv3d_wgrad_workspace_bytes(int b, int cin, int cout, int r);
  * Fully writes grad_w (no accumulation). */
 int pcfm_conv3d_wgrad(const float* x, const float* grad_y, int b, int cin, int cout, int r,
                       float* grad_w, void* ws, size_t ws_bytes, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Pointwise convolution: SharedMLP's Conv1d(C_in, C_out, 1)
+ * (third_party/pvcnn/modules/shared_mlp.py:15-27; cuDNN/TF32 in the
+ * reference) as bf16x3 GEMMs.  Tensors (B, C, N) fp32; any sizes.
+ * ---------------------------------------------------------------------- */
+
+/* Bytes of a split weight image (either orientation) for w [cout][cin]. */
+size_t pcfm_pointwise_weight_bytes(int cout, int cin);
+
+/* transpose = 0: forward image of w f32 [cout][cin]; 1: backward-data image. */
+int pcfm_pointwise_prep_weight(const float* w, int cout, int cin, int transpose, void* wsplit,
+                               void* stream);
+
+/* y[b, cout, n] = W x[b, cin, n] (+ bias).  With the transpose = 1 image of a
+ * (C_out, C_in) weight, x = grad_y (cin = C_out) and cout = C_in this is the
+ * backward-data pass.  Fully writes y. */
+int pcfm_pointwise_gemm(const float* x, const void* wsplit, const float* bias, int b, int cin,
+                        int cout, int n, float* y, void* stream);
+
+size_t pcfm_pointwise_wgrad_workspace_bytes(int b, int cin, int cout, int n);
+
+/* grad_w f32 [cout][cin] = sum_{b, p} grad_y[b, co, p] * x[b, ci, p]; fully written. */
+int pcfm_pointwise_wgrad(const float* x, const float* grad_y, int b, int cin, int cout, int n,
+                         float* grad_w, void* ws, size_t ws_bytes, void* stream);
 
 #ifdef __cplusplus
 }

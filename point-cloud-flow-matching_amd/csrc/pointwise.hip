@@ -1,0 +1,327 @@
+// Pointwise (1x1) convolution -- SharedMLP's Conv1d(C_in, C_out, 1)
+// (third_party/pvcnn/modules/shared_mlp.py:15-27) and ContextNet's
+// head_pre/head_out -- as bf16x3 GEMMs on the matrix cores (mfma_x3.hpp):
+//   forward        y[b, m, p] = sum_k W[m, k] x[b, k, p] (+ bias[m])
+//   backward-data  dx[b, k, p] = sum_m W[m, k] dy[b, m, p]   (transposed image)
+//   backward-wt    dW[m, k] = sum_{b, p} dy[b, m, p] x[b, k, p]
+// Tensors are (B, C, N) fp32 as the reference's Conv1d sees them.  Any C_in,
+// C_out and N: the weight image is zero-padded to the tile grid and partial
+// point / channel tiles are masked.
+#include <algorithm>
+
+#include "mfma_x3.hpp"
+
+namespace pcfm {
+namespace {
+
+inline int pad_to(int x, int m) { return (x + m - 1) / m * m; }
+
+// W [cout][cin] -> image [Mpad][Kpad] bf16 hi, lo; transpose: [cin][cout]
+__global__ void __launch_bounds__(256)
+    pw_wsplit_kernel(const float* __restrict__ w, int cout, int cin, int transpose, int Mpad,
+                     int Kpad, uint16_t* __restrict__ wh, uint16_t* __restrict__ wl) {
+  const size_t total = (size_t)Mpad * Kpad;
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int m = (int)(i / Kpad), k = (int)(i - (size_t)m * Kpad);
+  const int M = transpose ? cin : cout, K = transpose ? cout : cin;
+  float v = 0.0f;
+  if (m < M && k < K) v = transpose ? w[(size_t)k * cin + m] : w[(size_t)m * cin + k];
+  uint32_t hi, lo;
+  split_bf16(v, hi, lo);
+  wh[i] = (uint16_t)hi;
+  wl[i] = (uint16_t)lo;
+}
+
+// grid = (ceil(N / TN), Mpad / TM, B), 256 threads.
+template <int TM, int TN>
+__global__ void __launch_bounds__(256)
+    pw_gemm_kernel(const float* __restrict__ x, const uint16_t* __restrict__ wh,
+                   const uint16_t* __restrict__ wl, const float* __restrict__ bias,
+                   float* __restrict__ y, int K, int M, int N, int Kpad) {
+  using T = Tile<TM, TN>;
+  __shared__ __attribute__((aligned(16))) uint16_t lds[T::BUF];
+  const int b = blockIdx.z, m0 = blockIdx.y * TM, p0 = blockIdx.x * TN;
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wr = w >> 1, wc = w & 1, r = lane & 31, h = lane >> 5;
+  const float* __restrict__ xb = x + (size_t)b * K * N;
+
+  constexpr int CPT = kKT * TN / 256;  // channels per thread per K-step
+  const int sp = t % TN, ch = (t / TN) * CPT;
+  const int pt = p0 + sp;
+  const bool pok = pt < N;
+  const int ptc = pok ? pt : N - 1;  // clamped: always a valid address
+  const bool astage = 2 * TM >= 256 || t < 2 * TM;
+  const int arow = t >> 1, ahalf = (t & 1) * 16;
+  const int nsteps = Kpad / kKT;
+
+  uint4 ra0 = {}, ra1 = {}, ra2 = {}, ra3 = {};
+  float rb[CPT];
+  uint32_t rmask = 0u;  // elements to zero (channel >= K or point >= N)
+  auto load = [&](int s) {
+    const int c0 = s * kKT;
+    if (astage) {
+      const size_t g = (size_t)(m0 + arow) * Kpad + c0 + ahalf;
+      ra0 = *reinterpret_cast<const uint4*>(wh + g);
+      ra1 = *reinterpret_cast<const uint4*>(wh + g + 8);
+      ra2 = *reinterpret_cast<const uint4*>(wl + g);
+      ra3 = *reinterpret_cast<const uint4*>(wl + g + 8);
+    }
+    rmask = 0u;
+#pragma unroll
+    for (int q = 0; q < CPT; ++q) {
+      const int c = c0 + ch + q;
+      const bool ok = pok && c < K;
+      rb[q] = xb[(size_t)(c < K ? c : K - 1) * N + ptc];
+      rmask |= ok ? 0u : (1u << q);
+    }
+  };
+  auto store = [&](uint16_t* buf) {
+    if (astage) {
+      uint16_t* dh = buf + arow * kLDR + ahalf;
+      uint16_t* dl = buf + T::A_ELEMS + arow * kLDR + ahalf;
+      *reinterpret_cast<uint4*>(dh) = ra0;
+      *reinterpret_cast<uint4*>(dh + 8) = ra1;
+      *reinterpret_cast<uint4*>(dl) = ra2;
+      *reinterpret_cast<uint4*>(dl + 8) = ra3;
+    }
+#pragma unroll
+    for (int q = 0; q < CPT; ++q) rb[q] = (rmask >> q) & 1u ? 0.0f : rb[q];
+    uint16_t* bh = buf + 2 * T::A_ELEMS + sp * kLDR + ch;
+    store_split<CPT>(rb, bh, bh + T::B_ELEMS);
+  };
+
+  f32x16 acc[T::SI][T::SJ];
+#pragma unroll
+  for (int i = 0; i < T::SI; ++i)
+#pragma unroll
+    for (int j = 0; j < T::SJ; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
+
+  load(0);
+  store(lds);
+  __syncthreads();
+  for (int s = 0; s < nsteps; ++s) {
+    if (s + 1 < nsteps) load(s + 1);
+    tile_mfma<TM, TN>(lds, wr, wc, r, h, acc);
+    __syncthreads();
+    if (s + 1 < nsteps) store(lds);
+    __syncthreads();
+  }
+  float* __restrict__ yb = y + (size_t)b * M * N;
+#pragma unroll
+  for (int i = 0; i < T::SI; ++i)
+#pragma unroll
+    for (int j = 0; j < T::SJ; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int m = m0 + wr * (TM / 2) + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+        const int p = p0 + wc * (TN / 2) + j * 32 + r;
+        if (m < M && p < N)
+          yb[(size_t)m * N + p] = acc[i][j][e] + (bias != nullptr ? bias[m] : 0.0f);
+      }
+}
+
+// dW partials: grid = (ceil(Cout/128) * ceil(Cin/128), S); K-steps of 32
+// points (a step never crosses a batch element).  part [S][Cout][Cin].
+__global__ void __launch_bounds__(256)
+    pw_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ dy, int B, int cin,
+                    int cout, int N, int S, float* __restrict__ part) {
+  using T = Tile<128, 128>;
+  __shared__ __attribute__((aligned(16))) uint16_t lds[T::BUF];
+  const int nco = (cout + 127) / 128;
+  const int co0 = (blockIdx.x % nco) * 128, ci0 = (blockIdx.x / nco) * 128;
+  const int sp = blockIdx.y;
+  const int steps_per_b = (N + kKT - 1) / kKT;
+  const long long nsteps = (long long)B * steps_per_b;
+  const long long k0 = nsteps * sp / S, k1 = nsteps * (sp + 1) / S;
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wr = w >> 1, wc = w & 1, r = lane & 31, h = lane >> 5;
+  const int srow = t >> 1, shalf = (t & 1) * 16;
+  const int co = co0 + srow, ci = ci0 + srow;
+  const bool cook = co < cout, ciok = ci < cin;
+  const int coc = cook ? co : cout - 1, cic = ciok ? ci : cin - 1;
+  const bool vec = (N & 3) == 0;  // rows 16-B aligned (the runs start at multiples of 16)
+
+  float ra[16], rb[16];
+  uint32_t amask = 0u, bmask = 0u;
+  auto load = [&](long long ks) {
+    const int b = (int)(ks / steps_per_b);
+    const int p0 = (int)(ks - (long long)b * steps_per_b) * kKT + shalf;
+    const float* as = dy + ((size_t)b * cout + coc) * N;
+    const float* bs = x + ((size_t)b * cin + cic) * N;
+    amask = cook ? 0u : 0xFFFFu;
+    bmask = ciok ? 0u : 0xFFFFu;
+    if (vec && p0 + 16 <= N) {  // whole 16-point run: four 16-B loads per operand
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 fa = *reinterpret_cast<const float4*>(as + p0 + 4 * q);
+        const float4 fb = *reinterpret_cast<const float4*>(bs + p0 + 4 * q);
+        ra[4 * q] = fa.x;
+        ra[4 * q + 1] = fa.y;
+        ra[4 * q + 2] = fa.z;
+        ra[4 * q + 3] = fa.w;
+        rb[4 * q] = fb.x;
+        rb[4 * q + 1] = fb.y;
+        rb[4 * q + 2] = fb.z;
+        rb[4 * q + 3] = fb.w;
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int p = p0 + q;
+        const int pc = p < N ? p : N - 1;
+        ra[q] = as[pc];
+        rb[q] = bs[pc];
+        const uint32_t bit = p < N ? 0u : (1u << q);
+        amask |= bit;
+        bmask |= bit;
+      }
+    }
+  };
+  auto store = [&](uint16_t* buf) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      ra[q] = (amask >> q) & 1u ? 0.0f : ra[q];
+      rb[q] = (bmask >> q) & 1u ? 0.0f : rb[q];
+    }
+    uint16_t* ah = buf + srow * kLDR + shalf;
+    store_split<16>(ra, ah, ah + T::A_ELEMS);
+    uint16_t* bh = buf + 2 * T::A_ELEMS + srow * kLDR + shalf;
+    store_split<16>(rb, bh, bh + T::B_ELEMS);
+  };
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
+
+  if (k0 < k1) {
+    load(k0);
+    store(lds);
+  }
+  __syncthreads();
+  for (long long ks = k0; ks < k1; ++ks) {
+    if (ks + 1 < k1) load(ks + 1);
+    tile_mfma<128, 128>(lds, wr, wc, r, h, acc);
+    __syncthreads();
+    if (ks + 1 < k1) store(lds);
+    __syncthreads();
+  }
+  float* pb = part + (size_t)sp * cout * cin;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int o = co0 + wr * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+        const int c = ci0 + wc * 64 + j * 32 + r;
+        if (o < cout && c < cin) pb[(size_t)o * cin + c] = acc[i][j][e];
+      }
+}
+
+__global__ void __launch_bounds__(256)
+    pw_wgrad_reduce_kernel(const float* __restrict__ part, size_t total, int S,
+                           float* __restrict__ dw) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  float sum = 0.0f;
+  for (int q = 0; q < S; ++q) sum = sum + part[(size_t)q * total + i];
+  dw[i] = sum;
+}
+
+int pw_wgrad_splits(int B, int cin, int cout, int N) {
+  const long long tiles = (long long)((cout + 127) / 128) * ((cin + 127) / 128);
+  const long long steps = (long long)B * ((N + kKT - 1) / kKT);
+  long long s = std::max(1LL, (2LL * kCUs + tiles - 1) / tiles);
+  s = std::min(s, std::max(1LL, steps / 16));
+  return (int)std::min(s, 128LL);
+}
+
+bool pw_ok(int b, int cin, int cout, int n) {
+  return b >= 0 && cin > 0 && cout > 0 && n >= 0 && (long long)cin * n < (1LL << 31) &&
+         (long long)cout * n < (1LL << 31);
+}
+
+}  // namespace
+}  // namespace pcfm
+
+using namespace pcfm;
+
+extern "C" size_t pcfm_pointwise_weight_bytes(int cout, int cin) {
+  if (cout <= 0 || cin <= 0) return 0;
+  const size_t a = (size_t)pad_to(cout, 128) * pad_to(cin, kKT);
+  const size_t b = (size_t)pad_to(cin, 128) * pad_to(cout, kKT);
+  return 2 * std::max(a, b) * sizeof(uint16_t);
+}
+
+extern "C" int pcfm_pointwise_prep_weight(const float* w, int cout, int cin, int transpose,
+                                          void* wsplit, void* stream) {
+  PCFM_CHECK_ARG(cout > 0 && cin > 0, "pointwise_prep_weight: bad size %d x %d", cout, cin);
+  const int M = transpose ? cin : cout, K = transpose ? cout : cin;
+  const int Mpad = pad_to(M, 128), Kpad = pad_to(K, kKT);
+  const size_t total = (size_t)Mpad * Kpad;
+  uint16_t* wh = (uint16_t*)wsplit;
+  hipLaunchKernelGGL(pw_wsplit_kernel, dim3(ceil_div((long long)total, 256)), dim3(256), 0,
+                     (hipStream_t)stream, w, cout, cin, transpose ? 1 : 0, Mpad, Kpad, wh,
+                     wh + total);
+  return check_launch("pointwise_prep_weight");
+}
+
+extern "C" int pcfm_pointwise_gemm(const float* x, const void* wsplit, const float* bias, int b,
+                                   int cin, int cout, int n, float* y, void* stream) {
+  PCFM_CHECK_ARG(pw_ok(b, cin, cout, n), "pointwise_gemm: bad shape b=%d cin=%d cout=%d n=%d", b,
+                 cin, cout, n);
+  if (b == 0 || n == 0) return PCFM_OK;
+  const int Mpad = pad_to(cout, 128), Kpad = pad_to(cin, kKT);
+  const size_t total = (size_t)Mpad * Kpad;
+  const uint16_t* wh = (const uint16_t*)wsplit;
+  hipStream_t st = (hipStream_t)stream;
+  const long long big = (long long)ceil_div(n, 128) * (Mpad / 128) * b;
+  if (big >= 2 * kCUs) {
+    hipLaunchKernelGGL((pw_gemm_kernel<128, 128>), dim3(ceil_div(n, 128), Mpad / 128, b),
+                       dim3(256), 0, st, x, wh, wh + total, bias, y, cin, cout, n, Kpad);
+  } else {
+    hipLaunchKernelGGL((pw_gemm_kernel<64, 64>), dim3(ceil_div(n, 64), Mpad / 64, b), dim3(256),
+                       0, st, x, wh, wh + total, bias, y, cin, cout, n, Kpad);
+  }
+  return check_launch("pointwise_gemm");
+}
+
+extern "C" size_t pcfm_pointwise_wgrad_workspace_bytes(int b, int cin, int cout, int n) {
+  if (!pw_ok(b, cin, cout, n) || b == 0 || n == 0) return 0;
+  return (size_t)pw_wgrad_splits(b, cin, cout, n) * cout * cin * sizeof(float);
+}
+
+extern "C" int pcfm_pointwise_wgrad(const float* x, const float* grad_y, int b, int cin, int cout,
+                                    int n, float* grad_w, void* ws, size_t ws_bytes,
+                                    void* stream) {
+  PCFM_CHECK_ARG(pw_ok(b, cin, cout, n), "pointwise_wgrad: bad shape b=%d cin=%d cout=%d n=%d",
+                 b, cin, cout, n);
+  hipStream_t st = (hipStream_t)stream;
+  const size_t total = (size_t)cout * cin;
+  if (b == 0 || n == 0) {
+    const hipError_t e = hipMemsetAsync(grad_w, 0, total * sizeof(float), st);
+    if (e != hipSuccess) {
+      set_error("pointwise_wgrad: hipMemsetAsync: %s", hipGetErrorString(e));
+      return (int)e;
+    }
+    return PCFM_OK;
+  }
+  const size_t need = pcfm_pointwise_wgrad_workspace_bytes(b, cin, cout, n);
+  PCFM_CHECK_ARG(ws_bytes >= need, "pointwise_wgrad: workspace %zu < %zu bytes", ws_bytes, need);
+  const int S = pw_wgrad_splits(b, cin, cout, n);
+  const int tiles = ((cout + 127) / 128) * ((cin + 127) / 128);
+  hipLaunchKernelGGL(pw_wgrad_kernel, dim3(tiles, S), dim3(256), 0, st, x, grad_y, b, cin, cout,
+                     n, S, (float*)ws);
+  hipLaunchKernelGGL(pw_wgrad_reduce_kernel, dim3(ceil_div((long long)total, 256)), dim3(256), 0,
+                     st, (const float*)ws, total, S, grad_w);
+  return check_launch("pointwise_wgrad");
+}

@@ -4,8 +4,11 @@ Reference: third_party/pvcnn/modules/shared_mlp.py:6-33.  Parameter names
 (layers.{3k}, layers.{3k+1}) match, so reference checkpoints load unchanged.
 
 The 1x1 Conv1d is evaluated as what it is, a GEMM over the channel axis
-(y[b] = W x[b] + bias, hipBLASLt fp32 MFMA kernels), instead of going through
-MIOpen's convolution solvers: same product, no per-shape solver search.
+(y[b] = W x[b] + bias).  On the GPU in fp32 (the reference runs these layers
+with autocast off, models.py:512-513) it goes through pcfm's bf16x3
+matrix-core GEMMs (csrc/pointwise.hip; ~2^-16 relative error per product,
+tighter than the TF32 cuDNN uses for the reference's Conv1d by default);
+under autocast it stays a batched GEMM so torch's autocast casting applies.
 """
 import torch
 import torch.nn as nn
@@ -13,8 +16,33 @@ import torch.nn as nn
 __all__ = ["SharedMLP", "PointwiseConv1d"]
 
 
+class _PointwiseX3(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        from pcfm import ops
+        ctx.save_for_backward(x, weight)
+        ctx.has_bias = bias is not None
+        return ops.pointwise_forward(x, weight, bias)
+
+    @staticmethod
+    def backward(ctx, gy):
+        from pcfm import ops
+        x, weight = ctx.saved_tensors
+        gy = gy.contiguous()
+        gx = gw = gb = None
+        if ctx.needs_input_grad[0]:
+            gx = ops.pointwise_backward_data(gy, weight)
+        if ctx.needs_input_grad[1]:
+            gw = ops.pointwise_backward_weight(x, gy).view_as(weight)
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            gb = gy.sum(dim=(0, 2))
+        return gx, gw, gb
+
+
 class PointwiseConv1d(nn.Conv1d):
     """nn.Conv1d(in, out, 1) whose forward is a channel GEMM (same parameters)."""
+
+    exact_fp32 = False
 
     def forward(self, x):
         if self.kernel_size != (1,) or self.groups != 1 or self.stride != (1,) \
@@ -22,6 +50,9 @@ class PointwiseConv1d(nn.Conv1d):
             return super().forward(x)
         if x.dim() != 3:
             return super().forward(x)
+        if (x.is_cuda and x.dtype == torch.float32 and self.weight.dtype == torch.float32
+                and not self.exact_fp32 and not torch.is_autocast_enabled("cuda")):
+            return _PointwiseX3.apply(x, self.weight, self.bias)
         # bmm against the batch-broadcast weight: the result is a contiguous
         # (B, C_out, N) tensor (torch.matmul(2-D, 3-D) returns a transposed view,
         # which turns every following BatchNorm/ReLU/add into a strided kernel),

@@ -52,9 +52,14 @@ SIGNATURES = {
     "pcfm_conv3d_igemm": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P]),
     "pcfm_conv3d_wgrad_workspace_bytes": (_Z, [_I, _I, _I, _I]),
     "pcfm_conv3d_wgrad": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, _Z, _P]),
+    "pcfm_pointwise_weight_bytes": (_Z, [_I, _I]),
+    "pcfm_pointwise_prep_weight": (_I, [_P, _I, _I, _I, _P, _P]),
+    "pcfm_pointwise_gemm": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P]),
+    "pcfm_pointwise_wgrad_workspace_bytes": (_Z, [_I, _I, _I, _I]),
+    "pcfm_pointwise_wgrad": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, _Z, _P]),
 }
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 _lock = threading.Lock()
 _lib = None

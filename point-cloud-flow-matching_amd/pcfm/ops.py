@@ -419,3 +419,58 @@ def conv3d_backward_weight(x: torch.Tensor, grad_y: torch.Tensor) -> torch.Tenso
     _lib.call("pcfm_conv3d_wgrad", _ptr(x), _ptr(g), b, cin, cout, r, _ptr(dw), _ptr(ws),
               ws.numel(), _stream(x))
     return dw
+
+
+# --------------------------------------------------------------------------
+# Pointwise (1x1) convolution on the bf16x3 matrix-core path
+# (include/pcfm.h "Pointwise convolution").  x, y are (B, C, N) fp32.
+# --------------------------------------------------------------------------
+def pointwise_prep_weight(weight: torch.Tensor, transpose: bool) -> torch.Tensor:
+    _check(weight, "weight", "f")
+    w = weight.reshape(weight.shape[0], -1).contiguous()
+    cout, cin = w.shape
+    img = torch.empty(_lib.query("pcfm_pointwise_weight_bytes", cout, cin), dtype=torch.uint8,
+                      device=w.device)
+    _lib.call("pcfm_pointwise_prep_weight", _ptr(w), cout, cin, int(transpose), _ptr(img),
+              _stream(w))
+    return img
+
+
+def pointwise_forward(x: torch.Tensor, weight: torch.Tensor, bias) -> torch.Tensor:
+    """y = Conv1d(x; weight (Cout, Cin[, 1]), bias) for x (B, Cin, N)."""
+    _check(x, "input", "f")
+    x = x.contiguous()
+    b, cin, n = x.shape
+    cout = weight.shape[0]
+    img = pointwise_prep_weight(weight, False)
+    y = torch.empty((b, cout, n), dtype=torch.float32, device=x.device)
+    bias_p = _ptr(bias.contiguous()) if bias is not None else None
+    _lib.call("pcfm_pointwise_gemm", _ptr(x), _ptr(img), bias_p, b, cin, cout, n, _ptr(y),
+              _stream(x))
+    return y
+
+
+def pointwise_backward_data(grad_y: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
+    _check(grad_y, "grad_output", "f")
+    g = grad_y.contiguous()
+    b, cout, n = g.shape
+    cin = weight.shape[1]
+    img = pointwise_prep_weight(weight, True)
+    dx = torch.empty((b, cin, n), dtype=torch.float32, device=g.device)
+    _lib.call("pcfm_pointwise_gemm", _ptr(g), _ptr(img), None, b, cout, cin, n, _ptr(dx),
+              _stream(g))
+    return dx
+
+
+def pointwise_backward_weight(x: torch.Tensor, grad_y: torch.Tensor) -> torch.Tensor:
+    """dL/dW (Cout, Cin) of y = W x."""
+    _check(x, "input", "f")
+    _check(grad_y, "grad_output", "f")
+    x, g = x.contiguous(), grad_y.contiguous()
+    b, cin, n = x.shape
+    cout = g.shape[1]
+    ws = _workspace(_lib.query("pcfm_pointwise_wgrad_workspace_bytes", b, cin, cout, n), x)
+    dw = torch.empty((cout, cin), dtype=torch.float32, device=x.device)
+    _lib.call("pcfm_pointwise_wgrad", _ptr(x), _ptr(g), b, cin, cout, n, _ptr(dw), _ptr(ws),
+              ws.numel(), _stream(x))
+    return dw
