@@ -220,7 +220,10 @@ def main():
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "vs_h100_derived_upper_bound": value / H100_DERIVED_PTS,
-            "dtype": "fp32 voxel path + bf16 autocast MLP head (reference AMP config)",
+            "dtype": "fp32 ContextNet (scatter/gather ops fp32; Conv3d + 1x1 convs as bf16x3 "
+                     "split-operand matrix-core products, fp32 accumulate, ~2^-16 per product vs "
+                     "the reference's default cuDNN TF32 2^-11) + bf16 autocast MLP head "
+                     "(reference AMP config)",
             "data": "synthetic (randn xyz, U[0,1] rgb, U[0,1] cond; no dataset on the box)",
             "config": {"workload": "hybrid flow-matching train step, B=8/GPU, N=20000 xyz+rgb, "
                                    "latent 128, 1 joint, stages (128,256,256)@(32,16,8)",
