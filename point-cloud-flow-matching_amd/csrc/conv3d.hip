@@ -298,10 +298,14 @@ __global__ void __launch_bounds__(256)
   dw[i] = sum;
 }
 
+#ifndef PCFM_WGRAD_OCC
+#define PCFM_WGRAD_OCC 4
+#endif
 int conv3_wgrad_splits(int B, int cin, int cout, int R) {
   const long long tiles = 27LL * (cout / kMT) * (cin / kMT);
   const long long steps = (long long)B * R * R * R / kWK;
-  long long s = std::max(1LL, (2LL * kCUs + tiles - 1) / tiles);
+  // blocks per CU the split aims for (one block's staging overlaps another's MFMAs)
+  long long s = std::max(1LL, ((long long)PCFM_WGRAD_OCC * kCUs + tiles - 1) / tiles);
   s = std::min(s, std::max(1LL, steps / 16));  // keep >= 16 K-steps per block
   return (int)std::min(s, 64LL);
 }
