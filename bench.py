@@ -37,6 +37,8 @@ import torch.distributed as dist  # noqa: E402
 
 METRIC = "train-step points/sec (B=8, N=20000, xyz+rgb) at 1/2/4/8 MI355X; Chamfer ms"
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+BF16_DENSE_TF = 2500.0          # MI355X dense bf16 MFMA peak (no sparsity)
+BF16X3_PEAK_TF = BF16_DENSE_TF / 3  # fp32-equivalent peak of the 3-product split
 H100_DERIVED_PTS = 1.88e6       # 25 s/epoch at <= 293 steps/epoch (derived)
 # HBM bytes per launch of the voxel ops from rocprofv3 PMC passes (tools/op_traffic.py)
 TRAFFIC_FILE = os.path.join(REPO, "profiles", "r01_traffic.json")
@@ -189,20 +191,35 @@ def main():
         summary = ops.timer.summary()
         kernels = {k: {"launches_per_step": v["launches"] / args.steps,
                        "ms_per_step": v["ms"] / args.steps,
-                       "GBps": v["bytes"] / (v["ms"] * 1e-3) / 1e9 if v["ms"] > 0 else None}
+                       ("GBps" if v["kind"] == "hbm" else "TFLOPs_fp32_equiv"):
+                       (v["amount"] / (v["ms"] * 1e-3) / (1e9 if v["kind"] == "hbm" else 1e12))
+                       if v["ms"] > 0 else None}
                    for k, v in summary.items()}
-        roofline = None
-        if summary:
-            dom = max(summary, key=lambda k: summary[k]["ms"])
-            d = summary[dom]
-            achieved = d["bytes"] / (d["ms"] * 1e-3) / 1e9
-            traffic = measured_traffic(dom)
-            roofline = {"kernel": dom, "bound": "hbm", "achieved": achieved,
-                        "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
-                        "traffic": traffic, "traffic_unit": "bytes per launch (PMC, "
-                        "profiles/r01_traffic.json)" if traffic else None,
-                        "algorithmic_bytes_per_launch": d["bytes"] / d["launches"],
+
+        def roof(op):
+            d = summary[op]
+            sec = d["ms"] * 1e-3
+            if d["kind"] == "hbm":
+                achieved = d["amount"] / sec / 1e9
+                traffic = measured_traffic(op)
+                return {"kernel": op, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                        "traffic_unit": "bytes per launch (PMC, profiles/r01_traffic.json)"
+                        if traffic else None,
+                        "algorithmic_bytes_per_launch": d["amount"] / d["launches"],
                         "avg_launch_ms": d["ms"] / d["launches"]}
+            achieved = d["amount"] / sec / 1e12
+            return {"kernel": op, "bound": "mfma", "achieved": achieved, "peak": BF16X3_PEAK_TF,
+                    "unit": "TFLOP/s", "frac": achieved / BF16X3_PEAK_TF, "traffic": None,
+                    "note": "achieved = algorithmic fp32 conv FLOPs / time; each is 3 bf16 "
+                            "MFMA products, so peak = dense bf16 2500 TF / 3; raw bf16 MFMA "
+                            f"utilisation = {3 * achieved / BF16_DENSE_TF:.3f}",
+                    "algorithmic_flops_per_launch": d["amount"] / d["launches"],
+                    "avg_launch_ms": d["ms"] / d["launches"]}
+
+        roofline = roof(max(summary, key=lambda k: summary[k]["ms"])) if summary else None
+        hbm_ops = [k for k in summary if summary[k]["kind"] == "hbm"]
+        roofline_scatter = roof(max(hbm_ops, key=lambda k: summary[k]["ms"])) if hbm_ops else None
         log(f"{ms:.2f} ms/step, {value / 1e6:.3f} M points/s; losses {loss_p:.4f} {loss_z:.4f}")
         cham = None
         if not args.no_chamfer:
@@ -229,7 +246,8 @@ def main():
                                    "latent 128, 1 joint, stages (128,256,256)@(32,16,8)",
                        "global_batch": world * cfg.batch_size, "points_per_cloud": cfg.num_points,
                        "backbone": cfg.pf_backbone, "parallelism": f"dp{world}"},
-            "roofline": roofline, "kernels": kernels, "cpu_baseline": cpu, "chamfer": cham,
+            "roofline": roofline, "roofline_voxel_scatter_gather": roofline_scatter,
+            "kernels": kernels, "cpu_baseline": cpu, "chamfer": cham,
             "loss_point": loss_p, "loss_latent": loss_z,
         }
         print(json.dumps(line), flush=True)

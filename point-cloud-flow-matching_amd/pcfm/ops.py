@@ -68,19 +68,21 @@ def _workspace(nbytes: int, like: torch.Tensor) -> torch.Tensor:
 class _OpTimer:
     def __init__(self):
         self.enabled = False
-        self.records = []  # (op, start_event, end_event, algorithmic_bytes)
+        self.records = []  # (op, start_event, end_event, amount, kind)
 
     def reset(self):
         self.records = []
 
     def summary(self):
-        """{op: {"launches", "ms", "bytes"}} -- synchronize() first."""
+        """{op: {"launches", "ms", "amount", "kind"}} -- synchronize() first.
+        kind "hbm": amount = algorithmic bytes; kind "mfma":
+        amount = algorithmic fp32 FLOPs of the convolution."""
         out = {}
-        for op, e0, e1, nbytes in self.records:
-            d = out.setdefault(op, {"launches": 0, "ms": 0.0, "bytes": 0})
+        for op, e0, e1, amount, kind in self.records:
+            d = out.setdefault(op, {"launches": 0, "ms": 0.0, "amount": 0, "kind": kind})
             d["launches"] += 1
             d["ms"] += e0.elapsed_time(e1)
-            d["bytes"] += nbytes
+            d["amount"] += amount
         return out
 
 
@@ -88,10 +90,10 @@ timer = _OpTimer()
 
 
 class _timed:
-    __slots__ = ("op", "nbytes", "dev", "e0")
+    __slots__ = ("op", "amount", "kind", "dev", "e0")
 
-    def __init__(self, op, nbytes, like):
-        self.op, self.nbytes, self.dev = op, int(nbytes), like.device
+    def __init__(self, op, amount, like, kind="hbm"):
+        self.op, self.amount, self.kind, self.dev = op, int(amount), kind, like.device
 
     def __enter__(self):
         if timer.enabled:
@@ -102,7 +104,7 @@ class _timed:
         if timer.enabled and exc[0] is None:
             e1 = torch.cuda.Event(enable_timing=True)
             e1.record(torch.cuda.current_stream(self.dev))
-            timer.records.append((self.op, self.e0, e1, self.nbytes))
+            timer.records.append((self.op, self.e0, e1, self.amount, self.kind))
         return False
 
 
@@ -389,8 +391,9 @@ def conv3d_forward(x: torch.Tensor, weight: torch.Tensor, bias) -> torch.Tensor:
     img = conv3d_prep_weight(weight, False)
     y = torch.empty((b, cout, r, r, r), dtype=torch.float32, device=x.device)
     bias_p = _ptr(bias.contiguous()) if bias is not None else None
-    _lib.call("pcfm_conv3d_igemm", _ptr(x), _ptr(img), bias_p, b, cin, cout, r, _ptr(y),
-              _stream(x))
+    with _timed("conv3d_fwd", 54 * b * r ** 3 * cin * cout, x, "mfma"):
+        _lib.call("pcfm_conv3d_igemm", _ptr(x), _ptr(img), bias_p, b, cin, cout, r, _ptr(y),
+                  _stream(x))
     return y
 
 
@@ -402,8 +405,9 @@ def conv3d_backward_data(grad_y: torch.Tensor, weight: torch.Tensor) -> torch.Te
     cin = weight.shape[1]
     img = conv3d_prep_weight(weight, True)
     dx = torch.empty((b, cin, r, r, r), dtype=torch.float32, device=g.device)
-    _lib.call("pcfm_conv3d_igemm", _ptr(g), _ptr(img), None, b, cout, cin, r, _ptr(dx),
-              _stream(g))
+    with _timed("conv3d_bwd_data", 54 * b * r ** 3 * cin * cout, g, "mfma"):
+        _lib.call("pcfm_conv3d_igemm", _ptr(g), _ptr(img), None, b, cout, cin, r, _ptr(dx),
+                  _stream(g))
     return dx
 
 
@@ -416,8 +420,9 @@ def conv3d_backward_weight(x: torch.Tensor, grad_y: torch.Tensor) -> torch.Tenso
     cout = g.shape[1]
     ws = _workspace(_lib.query("pcfm_conv3d_wgrad_workspace_bytes", b, cin, cout, r), x)
     dw = torch.empty((cout, cin, 3, 3, 3), dtype=torch.float32, device=x.device)
-    _lib.call("pcfm_conv3d_wgrad", _ptr(x), _ptr(g), b, cin, cout, r, _ptr(dw), _ptr(ws),
-              ws.numel(), _stream(x))
+    with _timed("conv3d_wgrad", 54 * b * r ** 3 * cin * cout, x, "mfma"):
+        _lib.call("pcfm_conv3d_wgrad", _ptr(x), _ptr(g), b, cin, cout, r, _ptr(dw), _ptr(ws),
+                  ws.numel(), _stream(x))
     return dw
 
 
@@ -445,8 +450,9 @@ def pointwise_forward(x: torch.Tensor, weight: torch.Tensor, bias) -> torch.Tens
     img = pointwise_prep_weight(weight, False)
     y = torch.empty((b, cout, n), dtype=torch.float32, device=x.device)
     bias_p = _ptr(bias.contiguous()) if bias is not None else None
-    _lib.call("pcfm_pointwise_gemm", _ptr(x), _ptr(img), bias_p, b, cin, cout, n, _ptr(y),
-              _stream(x))
+    with _timed("pointwise_fwd", 2 * b * n * cin * cout, x, "mfma"):
+        _lib.call("pcfm_pointwise_gemm", _ptr(x), _ptr(img), bias_p, b, cin, cout, n, _ptr(y),
+                  _stream(x))
     return y
 
 
@@ -457,8 +463,9 @@ def pointwise_backward_data(grad_y: torch.Tensor, weight: torch.Tensor) -> torch
     cin = weight.shape[1]
     img = pointwise_prep_weight(weight, True)
     dx = torch.empty((b, cin, n), dtype=torch.float32, device=g.device)
-    _lib.call("pcfm_pointwise_gemm", _ptr(g), _ptr(img), None, b, cout, cin, n, _ptr(dx),
-              _stream(g))
+    with _timed("pointwise_bwd_data", 2 * b * n * cin * cout, g, "mfma"):
+        _lib.call("pcfm_pointwise_gemm", _ptr(g), _ptr(img), None, b, cout, cin, n, _ptr(dx),
+                  _stream(g))
     return dx
 
 
@@ -471,6 +478,7 @@ def pointwise_backward_weight(x: torch.Tensor, grad_y: torch.Tensor) -> torch.Te
     cout = g.shape[1]
     ws = _workspace(_lib.query("pcfm_pointwise_wgrad_workspace_bytes", b, cin, cout, n), x)
     dw = torch.empty((cout, cin), dtype=torch.float32, device=x.device)
-    _lib.call("pcfm_pointwise_wgrad", _ptr(x), _ptr(g), b, cin, cout, n, _ptr(dw), _ptr(ws),
-              ws.numel(), _stream(x))
+    with _timed("pointwise_wgrad", 2 * b * n * cin * cout, x, "mfma"):
+        _lib.call("pcfm_pointwise_wgrad", _ptr(x), _ptr(g), b, cin, cout, n, _ptr(dw), _ptr(ws),
+                  ws.numel(), _stream(x))
     return dw
