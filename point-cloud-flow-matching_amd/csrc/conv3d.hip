@@ -152,7 +152,7 @@ __global__ void __launch_bounds__(256)
 // One GEMM per tap with K = B*V voxels: A = dY tile [co][voxel], B = shifted X
 // tile [ci][voxel] -- both are voxel-contiguous rows of the NCDHW tensors, so
 // the A/B fragments (8 consecutive k per lane) come straight from LDS rows.
-// grid.x = 27 * (Cout/128) * (Cin/128) tiles, grid.y = S voxel splits; each
+// 27 * (Cout/128) * (Cin/128) tiles x S voxel splits (1-D grid); each
 // block writes an fp32 partial [s][tap][co][ci]; conv3_wgrad_reduce_kernel
 // sums the S partials in split order into dW [co][ci][27].
 // ---------------------------------------------------------------------------
@@ -165,12 +165,23 @@ __global__ void __launch_bounds__(256)
   __shared__ __attribute__((aligned(16))) uint16_t lds[kNBuf * T::BUF];
   const int V = R * R * R, R2 = R * R;
   const int nco = cout / kMT;
-  int id = blockIdx.x;
+  // 1-D grid of items ((ci tile * nco + co tile) * S + split) * 27 + tap, dealt
+  // to XCDs in contiguous runs (bijective remap, cdna_hip_programming.md T1):
+  // the 27 taps of one (tile, voxel range) share the dY rows and overlapping X
+  // rows, so they should meet in one XCD's L2 instead of all re-reading HBM.
+  int id = (int)blockIdx.x;
+#ifndef PCFM_WGRAD_NOSWZ
+  {
+    const int nwg = (int)gridDim.x, q = nwg / 8, rr = nwg % 8, xcd = id % 8;
+    id = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + id / 8;
+  }
+#endif
   const int tap = id % 27;
   id /= 27;
+  const int sp = id % S;
+  id /= S;
   const int co0 = (id % nco) * kMT;
   const int ci0 = (id / nco) * kMT;
-  const int sp = blockIdx.y;
   const int steps_per_b = V / kWK;
   const long long nsteps = (long long)B * steps_per_b;
   const long long k0 = nsteps * sp / S, k1 = nsteps * (sp + 1) / S;
@@ -376,7 +387,7 @@ extern "C" int pcfm_conv3d_wgrad(const float* x, const float* grad_y, int b, int
   const int S = conv3_wgrad_splits(b, cin, cout, r);
   hipStream_t st = (hipStream_t)stream;
   const int tiles = 27 * (cout / kMT) * (cin / kMT);
-  hipLaunchKernelGGL(conv3_wgrad_kernel, dim3(tiles, S), dim3(256), 0, st, x, grad_y, b, cin,
+  hipLaunchKernelGGL(conv3_wgrad_kernel, dim3(tiles * S), dim3(256), 0, st, x, grad_y, b, cin,
                      cout, r, S, (float*)ws);
   const size_t total = (size_t)27 * cout * cin;
   hipLaunchKernelGGL(conv3_wgrad_reduce_kernel, dim3(ceil_div((long long)total, 256)), dim3(256),
