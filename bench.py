@@ -189,9 +189,10 @@ def main():
         value = points / elapsed
         ms = elapsed * 1e3 / args.steps
         summary = ops.timer.summary()
+        rate_key = {"hbm": "GBps", "mfma": "TFLOPs_fp32_equiv", "mfma_bf16": "TFLOPs_bf16"}
         kernels = {k: {"launches_per_step": v["launches"] / args.steps,
                        "ms_per_step": v["ms"] / args.steps,
-                       ("GBps" if v["kind"] == "hbm" else "TFLOPs_fp32_equiv"):
+                       rate_key[v["kind"]]:
                        (v["amount"] / (v["ms"] * 1e-3) / (1e9 if v["kind"] == "hbm" else 1e12))
                        if v["ms"] > 0 else None}
                    for k, v in summary.items()}
@@ -209,6 +210,12 @@ def main():
                         "algorithmic_bytes_per_launch": d["amount"] / d["launches"],
                         "avg_launch_ms": d["ms"] / d["launches"]}
             achieved = d["amount"] / sec / 1e12
+            if d["kind"] == "mfma_bf16":
+                return {"kernel": op, "bound": "mfma", "achieved": achieved,
+                        "peak": BF16_DENSE_TF, "unit": "TFLOP/s",
+                        "frac": achieved / BF16_DENSE_TF, "traffic": None,
+                        "algorithmic_flops_per_launch": d["amount"] / d["launches"],
+                        "avg_launch_ms": d["ms"] / d["launches"]}
             return {"kernel": op, "bound": "mfma", "achieved": achieved, "peak": BF16X3_PEAK_TF,
                     "unit": "TFLOP/s", "frac": achieved / BF16X3_PEAK_TF, "traffic": None,
                     "note": "achieved = algorithmic fp32 conv FLOPs / time; each is 3 bf16 "

@@ -35,7 +35,8 @@ extern "C" {
 #define PCFM_OK 0
 #define PCFM_EINVAL -1
 
-/* ABI version: bumped on any signature change (4: voxel and pointwise convolution). */
+/* ABI version: bumped on any signature change (4: voxel and pointwise convolution;
+ * 5: per-point head kernels). */
 int pcfm_abi_version(void);
 /* Thread-local text of the last non-zero return code. */
 const char* pcfm_last_error(void);
@@ -230,6 +231,64 @@ size_t pcfm_pointwise_wgrad_workspace_bytes(int b, int cin, int cout, int n);
 /* grad_w f32 [cout][cin] = sum_{b, p} grad_y[b, co, p] * x[b, ci, p]; fully written. */
 int pcfm_pointwise_wgrad(const float* x, const float* grad_y, int b, int cin, int cout, int n,
                          float* grad_w, void* ws, size_t ws_bytes, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Per-point head (models.py:62-153, 546-601: the Linear layers of
+ * VelocityNetWithContext / ShapeEncoder run under bf16 autocast on
+ * rows = B*N points; torch's autocast mm -> cuBLAS in the reference).
+ * ---------------------------------------------------------------------- */
+
+size_t pcfm_rows_wgrad_workspace_bytes(long long rows, int m, int n);
+
+/* Weight gradient of a bf16 Linear over `rows` rows (the backward of
+ * F.linear's weight under autocast, i.e. mm(grad_y^T, x) in bf16):
+ *   a   bf16 [rows][lda]  (grad_y; columns 0..m)
+ *   b   bf16 [rows][ldb]  (x; columns 0..n)
+ *   out bf16 [m][n] = bf16( sum_r a[r][i] * b[r][j] )  (fp32 accumulation,
+ *   split over rows, partials added in a fixed order: deterministic).
+ * Fully writes out. */
+int pcfm_rows_wgrad_bf16(const void* a, int lda, const void* b, int ldb, long long rows, int m,
+                         int n, void* out, void* ws, size_t ws_bytes, void* stream);
+
+/* Trunk rows of VelocityNetWithContext / VelocityNet (models.py:62-79 FiLMBlock,
+ * :107-116 residual loop), W = 256 or 512 channels, rows = b*n (batch-major).
+ * bf16 tensors are passed as void* (raw 16-bit bf16 bits).
+ * h of a block = h16 (bf16 [b*n][w], the input Linear's output) if non-NULL,
+ * else uprev + gprev (fp32 + bf16: the previous block's residual sum).
+ * Forward of one FiLM block:
+ *   y = LayerNorm(h; gamma, beta, eps)   u = y * sp1[b] + shift[b]
+ *   (sp1 = bf16(1 + scale), shift: bf16 [b][w], per batch element)
+ *   writes u f32 [b*n][w], a = bf16(SiLU(u)) [b*n][w], mean/rstd f32 [b*n]. */
+int pcfm_head_film_fwd(const void* h16, const float* uprev, const void* gprev,
+                       const float* gamma, const float* beta, const void* sp1,
+                       const void* shift, int b, int n, int w, float eps, float* u, void* a,
+                       float* mean, float* rstd, void* stream);
+
+/* Output layer's input: a = bf16(SiLU(uprev + gprev)). */
+int pcfm_head_silu_fwd(const float* uprev, const void* gprev, int b, int n, int w, void* a,
+                       void* stream);
+
+size_t pcfm_head_bwd_workspace_bytes(int b, int n, int w);
+
+/* Backward of one FiLM block given dh_next = dL/dh_{i+1} (f32) and
+ * da16 = dL/da (bf16, = dL/dg @ W of the block's Linear):
+ *   du = dh_next + da * SiLU'(u);  d sp1[b] = sum_rows du*y;  d shift[b] = sum du;
+ *   dy = du * sp1;  d gamma = sum dy*xhat;  d beta = sum dy;
+ *   dh = LayerNorm backward (f32, written if dh != NULL) and bf16(dh) -> dh16;
+ *   dbias = sum_rows bf16(dh) (the bias gradient of the Linear that produced h).
+ * dsp1/dshift f32 [b][w], dgamma/dbeta/dbias f32 [w]; any may be NULL. */
+int pcfm_head_film_bwd(const float* dh_next, const void* da16, const float* u, const void* h16,
+                       const float* uprev, const void* gprev, const float* mean,
+                       const float* rstd, const float* gamma, const float* beta,
+                       const void* sp1, int b, int n, int w, float* dh, void* dh16,
+                       float* dsp1, float* dshift, float* dgamma, float* dbeta, float* dbias,
+                       void* ws, size_t ws_bytes, void* stream);
+
+/* Backward of a = bf16(SiLU(uprev + gprev)): dh = da * SiLU'(h) -> dh (f32),
+ * dh16 (bf16), dbias = sum_rows bf16(dh). */
+int pcfm_head_silu_bwd(const void* da16, const float* uprev, const void* gprev, int b, int n,
+                       int w, float* dh, void* dh16, float* dbias, void* ws, size_t ws_bytes,
+                       void* stream);
 
 #ifdef __cplusplus
 }

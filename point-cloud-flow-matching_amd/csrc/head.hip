@@ -1,0 +1,259 @@
+// Per-point head of the flow model (models.py:62-153, 546-601 in the
+// reference): the Linear layers of VelocityNetWithContext / ShapeEncoder run
+// under bf16 autocast on rows = B*N points (160000 at the bench config).
+//
+// Weight gradient of such a Linear:  dW[m][n] = sum_r dY[r][m] * X[r][n]
+// with R = 160000 and M, N <= 512 -- a GEMM whose reduction axis is the long
+// one.  The library GEMM runs it as a handful of output tiles with the whole
+// K = R each (16 x 128x128 tiles on 256 CUs, ~160 TFLOP/s measured); here the
+// row axis is split over the grid (split-K, every CU busy), each block
+// accumulates a 128 x 128 fp32 tile with v_mfma_f32_32x32x16_bf16, and an
+// ordered reduce adds the partials (deterministic) and rounds to bf16 -- the
+// dtype autocast's mm returns for the reference's layer.
+//
+// Operand staging: both operands are row-major [r][col] with the reduction
+// index r on the slow axis, so the LDS image is the global tile as it is
+// ([64 rows][128 cols] bf16, 16-B chunks XOR-swizzled within a 256-B row) and
+// the MFMA operands (8 consecutive r per lane) come out of gfx950's
+// transposing LDS read ds_read_b64_tr_b16 (cdna_hip_programming.md T10).
+#include <algorithm>
+
+#include "pcfm_common.hpp"
+
+namespace pcfm {
+namespace {
+
+typedef short v4s __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8h __attribute__((ext_vector_type(8)));
+typedef float f32x16h __attribute__((ext_vector_type(16)));
+
+constexpr int kRT = 64;    // rows (reduction) per K-step
+constexpr int kTile = 128; // output tile edge
+
+// byte offset of 16-B chunk `ch` (0..15) of LDS row `row` (256-B rows),
+// the T10 (b) swizzle: conflict-free ds_write_b128 rows and tr_b16 reads
+__device__ __forceinline__ int swz(int row, int ch) {
+  return 256 * row + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
+}
+
+__device__ __forceinline__ v4s tr_read(const uint8_t* base, int off) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) v4s*)(base + off));
+}
+
+// One 64-row x 128-col bf16 tile of a row-major matrix into 4 uint4 per thread
+// (rows >= R and columns >= ncols are zero).  MODE 2: ld % 8 == 0, 16-B
+// aligned base and the tile's 128 columns all in range (one 16-B load per
+// chunk); MODE 1: ld even, 4-B aligned base (32-bit loads); MODE 0: 16-bit loads.
+template <int MODE>
+__device__ __forceinline__ void load_tile(const uint16_t* __restrict__ src, int ld, int ncols,
+                                          long long r0, long long R, int c0, int t,
+                                          uint4 (&v)[4]) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int c = t + 256 * q;
+    const int row = c >> 4, ch = c & 15;
+    const long long gr = r0 + row;
+    const bool rok = gr < R;
+    const long long grc = rok ? gr : R - 1;
+    if (MODE == 2) {
+      uint4 x = *reinterpret_cast<const uint4*>(src + (size_t)grc * ld + c0 + ch * 8);
+      if (!rok) x = uint4{0u, 0u, 0u, 0u};
+      v[q] = x;
+    } else {
+      const uint16_t* rp = src + (size_t)grc * ld;
+      uint32_t w[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int col = c0 + ch * 8 + 2 * e;
+        uint32_t x = 0u;
+        if (MODE == 1) {
+          if (col < ncols) x = *reinterpret_cast<const uint32_t*>(rp + col);
+          if (col + 1 >= ncols) x &= 0xFFFFu;
+        } else {
+          if (col < ncols) x = rp[col];
+          if (col + 1 < ncols) x |= (uint32_t)rp[col + 1] << 16;
+        }
+        w[e] = rok ? x : 0u;
+      }
+      v[q] = uint4{w[0], w[1], w[2], w[3]};
+    }
+  }
+}
+
+__device__ __forceinline__ void store_tile(uint8_t* img, int t, const uint4 (&v)[4]) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int c = t + 256 * q;
+    *reinterpret_cast<uint4*>(img + swz(c >> 4, c & 15)) = v[q];
+  }
+}
+
+// grid = (tiles_m * tiles_n, S), 256 threads (2 x 2 waves of 64 x 64).
+// part[s][M][N] fp32 = sum over split s's rows of A[r][m] * B[r][n].
+template <int MA, int MB>
+__global__ void __launch_bounds__(256)
+    rows_wgrad_kernel(const uint16_t* __restrict__ A, int lda, const uint16_t* __restrict__ B,
+                      int ldb, long long R, int M, int N, int S, float* __restrict__ part) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[2 * kRT * 256];
+  uint8_t* imgA = lds;
+  uint8_t* imgB = lds + kRT * 256;
+  const int tm = (M + kTile - 1) / kTile;
+  const int m0 = (blockIdx.x % tm) * kTile, n0 = (blockIdx.x / tm) * kTile;
+  const int sp = blockIdx.y;
+  const long long nsteps = (R + kRT - 1) / kRT;
+  const long long k0 = nsteps * sp / S, k1 = nsteps * (sp + 1) / S;
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wr = w >> 1, wc = w & 1;
+  const int g = lane >> 4, i16 = lane & 15, q4 = i16 >> 2, p4 = i16 & 3;
+
+  f32x16h acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
+
+  uint4 ra[4], rb[4];
+  if (k0 < k1) {
+    load_tile<MA>(A, lda, M, k0 * kRT, R, m0, t, ra);
+    load_tile<MB>(B, ldb, N, k0 * kRT, R, n0, t, rb);
+    store_tile(imgA, t, ra);
+    store_tile(imgB, t, rb);
+  }
+  __syncthreads();
+  for (long long ks = k0; ks < k1; ++ks) {
+    if (ks + 1 < k1) {
+      load_tile<MA>(A, lda, M, (ks + 1) * kRT, R, m0, t, ra);
+      load_tile<MB>(B, ldb, N, (ks + 1) * kRT, R, n0, t, rb);
+    }
+#pragma unroll
+    for (int kk = 0; kk < kRT / 16; ++kk) {
+      bf16x8h a[2], b[2];
+      const int row = kk * 16 + 8 * (g >> 1) + q4;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int col = wr * 64 + i * 32 + (g & 1) * 16 + 4 * p4;
+        const int off0 = swz(row, col >> 3) + 8 * (p4 & 1);
+        const int off1 = swz(row + 4, col >> 3) + 8 * (p4 & 1);
+        const v4s x0 = tr_read(imgA, off0), x1 = tr_read(imgA, off1);
+        a[i] = __builtin_bit_cast(bf16x8h, __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int col = wc * 64 + j * 32 + (g & 1) * 16 + 4 * p4;
+        const int off0 = swz(row, col >> 3) + 8 * (p4 & 1);
+        const int off1 = swz(row + 4, col >> 3) + 8 * (p4 & 1);
+        const v4s y0 = tr_read(imgB, off0), y1 = tr_read(imgB, off1);
+        b[j] = __builtin_bit_cast(bf16x8h, __builtin_shufflevector(y0, y1, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    __syncthreads();
+    if (ks + 1 < k1) {
+      store_tile(imgA, t, ra);
+      store_tile(imgB, t, rb);
+    }
+    __syncthreads();
+  }
+  float* pb = part + (size_t)sp * M * N;
+  const int h = lane >> 5, r = lane & 31;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int m = m0 + wr * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+        const int n = n0 + wc * 64 + j * 32 + r;
+        if (m < M && n < N) pb[(size_t)m * N + n] = acc[i][j][e];
+      }
+}
+
+// out[i] = bf16(sum_{s < S} part[s][i]) in split order (deterministic).
+__global__ void __launch_bounds__(256)
+    rows_wgrad_reduce_kernel(const float* __restrict__ part, size_t total, int S,
+                             uint16_t* __restrict__ out) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  float sum = 0.0f;
+  for (int q = 0; q < S; ++q) sum = sum + part[(size_t)q * total + i];
+  out[i] = __builtin_bit_cast(uint16_t, (__bf16)sum);
+}
+
+int rows_wgrad_splits(long long R, int M, int N) {
+  const long long tiles = (long long)((M + kTile - 1) / kTile) * ((N + kTile - 1) / kTile);
+  const long long steps = (R + kRT - 1) / kRT;
+  long long s = std::max(1LL, (2LL * kCUs + tiles - 1) / tiles);
+  s = std::min(s, std::max(1LL, steps / 8));  // >= 8 K-steps per block
+  return (int)std::min(s, 256LL);
+}
+
+bool rows_ok(long long R, int M, int N, int lda, int ldb) {
+  return R >= 0 && M > 0 && N > 0 && lda >= M && ldb >= N;
+}
+
+}  // namespace
+}  // namespace pcfm
+
+using namespace pcfm;
+
+extern "C" size_t pcfm_rows_wgrad_workspace_bytes(long long rows, int m, int n) {
+  if (!rows_ok(rows, m, n, m, n) || rows == 0) return 0;
+  return (size_t)rows_wgrad_splits(rows, m, n) * m * n * sizeof(float);
+}
+
+extern "C" int pcfm_rows_wgrad_bf16(const void* a, int lda, const void* b, int ldb,
+                                    long long rows, int m, int n, void* out, void* ws,
+                                    size_t ws_bytes, void* stream) {
+  PCFM_CHECK_ARG(rows_ok(rows, m, n, lda, ldb),
+                 "rows_wgrad_bf16: bad shape rows=%lld m=%d n=%d lda=%d ldb=%d", rows, m, n,
+                 lda, ldb);
+  hipStream_t st = (hipStream_t)stream;
+  const size_t total = (size_t)m * n;
+  if (rows == 0) {
+    const hipError_t e = hipMemsetAsync(out, 0, total * sizeof(uint16_t), st);
+    if (e != hipSuccess) {
+      set_error("rows_wgrad_bf16: hipMemsetAsync: %s", hipGetErrorString(e));
+      return (int)e;
+    }
+    return PCFM_OK;
+  }
+  const size_t need = pcfm_rows_wgrad_workspace_bytes(rows, m, n);
+  PCFM_CHECK_ARG(ws_bytes >= need, "rows_wgrad_bf16: workspace %zu < %zu bytes", ws_bytes, need);
+  const int S = rows_wgrad_splits(rows, m, n);
+  const int tiles = ((m + kTile - 1) / kTile) * ((n + kTile - 1) / kTile);
+  const uint16_t* A = (const uint16_t*)a;
+  const uint16_t* B = (const uint16_t*)b;
+  const auto mode = [](const void* p, int ld, int cols) {
+    const uintptr_t u = (uintptr_t)p;
+    if (ld % 8 == 0 && cols % kTile == 0 && (u & 15) == 0) return 2;
+    return (ld % 2 == 0 && (u & 3) == 0) ? 1 : 0;
+  };
+  const int ma = mode(a, lda, m), mb = mode(b, ldb, n);
+  const dim3 grid(tiles, S), blk(256);
+  float* part = (float*)ws;
+#define PCFM_ROWS_LAUNCH(X, Y)                                                              \
+  if (ma == X && mb == Y)                                                                   \
+    hipLaunchKernelGGL((rows_wgrad_kernel<X, Y>), grid, blk, 0, st, A, lda, B, ldb, rows, m, \
+                       n, S, part);
+  PCFM_ROWS_LAUNCH(2, 2)
+  PCFM_ROWS_LAUNCH(2, 1)
+  PCFM_ROWS_LAUNCH(2, 0)
+  PCFM_ROWS_LAUNCH(1, 2)
+  PCFM_ROWS_LAUNCH(1, 1)
+  PCFM_ROWS_LAUNCH(1, 0)
+  PCFM_ROWS_LAUNCH(0, 2)
+  PCFM_ROWS_LAUNCH(0, 1)
+  PCFM_ROWS_LAUNCH(0, 0)
+#undef PCFM_ROWS_LAUNCH
+  hipLaunchKernelGGL(rows_wgrad_reduce_kernel, dim3(ceil_div((long long)total, 256)), dim3(256),
+                     0, st, (const float*)ws, total, S, (uint16_t*)out);
+  return check_launch("rows_wgrad_bf16");
+}

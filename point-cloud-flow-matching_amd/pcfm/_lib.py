@@ -21,6 +21,7 @@ _P = ctypes.c_void_p
 _I = ctypes.c_int
 _F = ctypes.c_float
 _Z = ctypes.c_size_t
+_L = ctypes.c_longlong
 
 # name -> (restype, argtypes); must list every symbol of include/pcfm.h.
 SIGNATURES = {
@@ -57,9 +58,18 @@ SIGNATURES = {
     "pcfm_pointwise_gemm": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P]),
     "pcfm_pointwise_wgrad_workspace_bytes": (_Z, [_I, _I, _I, _I]),
     "pcfm_pointwise_wgrad": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, _Z, _P]),
+    "pcfm_rows_wgrad_workspace_bytes": (_Z, [_L, _I, _I]),
+    "pcfm_rows_wgrad_bf16": (_I, [_P, _I, _P, _I, _L, _I, _I, _P, _P, _Z, _P]),
+    "pcfm_head_film_fwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _F, _P, _P, _P, _P,
+                                _P]),
+    "pcfm_head_silu_fwd": (_I, [_P, _P, _I, _I, _I, _P, _P]),
+    "pcfm_head_bwd_workspace_bytes": (_Z, [_I, _I, _I]),
+    "pcfm_head_film_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P, _P,
+                                _P, _P, _P, _P, _P, _P, _Z, _P]),
+    "pcfm_head_silu_bwd": (_I, [_P, _P, _P, _I, _I, _I, _P, _P, _P, _P, _Z, _P]),
 }
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 _lock = threading.Lock()
 _lib = None

@@ -23,6 +23,7 @@ import torch.nn.functional as F
 
 from modules.pvconv import PVConv
 from modules.shared_mlp import PointwiseConv1d, SharedMLP
+from pcfm.layers import RowsLinear, fused_trunk, fused_trunk_supported
 
 __all__ = [
     "timestep_embedding", "FiLMBlock", "VelocityNet", "ShapeEncoder",
@@ -86,11 +87,11 @@ class _PointTrunk(_TimeCondEmbed):
     """input Linear -> (FiLM, residual SiLU+Linear) x (depth-1) -> SiLU+Linear."""
 
     def _build_trunk(self, in_dim: int, width: int, depth: int, emb_dim: int, out_dim: int):
-        self.input = nn.Linear(in_dim, width)
-        self.blocks = nn.ModuleList([nn.Sequential(nn.SiLU(), nn.Linear(width, width))
+        self.input = RowsLinear(in_dim, width)
+        self.blocks = nn.ModuleList([nn.Sequential(nn.SiLU(), RowsLinear(width, width))
                                      for _ in range(depth - 1)])
         self.films = nn.ModuleList([FiLMBlock(width, emb_dim) for _ in range(depth - 1)])
-        self.out = nn.Sequential(nn.SiLU(), nn.Linear(width, out_dim))
+        self.out = nn.Sequential(nn.SiLU(), RowsLinear(width, out_dim))
         _kaiming_relu_(self.input)
         for seq in self.blocks:
             _kaiming_relu_(seq[1])
@@ -104,7 +105,12 @@ class _PointTrunk(_TimeCondEmbed):
             c_in = ref.new_zeros((ref.shape[0], self.cond_dim if self.cond_dim > 0 else 1))
         return F.silu(self.c_proj(c_in))
 
+    # the gfx950 fused trunk (pcfm/layers.py) under bf16 autocast; False = torch ops
+    fused = True
+
     def _run_trunk(self, h: torch.Tensor, emb: torch.Tensor, n: int) -> torch.Tensor:
+        if self.fused and fused_trunk_supported(self, h, emb, n):
+            return fused_trunk(self, h, emb, n)
         if self.film_per_point:
             film_emb = emb[:, None, :].expand(emb.shape[0], n, -1).reshape(-1, emb.shape[-1])
         else:
@@ -159,8 +165,8 @@ class ShapeEncoder(nn.Module):
         self.latent_dim = int(latent_dim)
         self.in_channels = int(in_channels)
         w = width
-        self.mlp = nn.Sequential(nn.Linear(self.in_channels, w), nn.SiLU(), nn.Linear(w, w),
-                                 nn.SiLU(), nn.Linear(w, w), nn.SiLU())
+        self.mlp = nn.Sequential(RowsLinear(self.in_channels, w), nn.SiLU(), RowsLinear(w, w),
+                                 nn.SiLU(), RowsLinear(w, w), nn.SiLU())
         head: List[nn.Module] = []
         for _ in range(max(1, depth - 3)):
             head += [nn.Linear(w, w), nn.SiLU()]

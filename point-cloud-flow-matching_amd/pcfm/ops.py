@@ -482,3 +482,92 @@ def pointwise_backward_weight(x: torch.Tensor, grad_y: torch.Tensor) -> torch.Te
         _lib.call("pcfm_pointwise_wgrad", _ptr(x), _ptr(g), b, cin, cout, n, _ptr(dw), _ptr(ws),
                   ws.numel(), _stream(x))
     return dw
+
+
+# --------------------------------------------------------------------------
+# Per-point head: bf16 Linear weight gradient over B*N rows
+# (include/pcfm.h "Per-point head").
+# --------------------------------------------------------------------------
+def rows_wgrad_bf16(grad_y: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
+    """dW (M, N) bf16 = grad_y^T @ x for grad_y (R, M), x (R, N) bf16 row-major
+    (unit column stride; row strides may exceed the width)."""
+    for t, name in ((grad_y, "grad_y"), (x, "x")):
+        _check_cuda(t, name)
+        if t.dtype != torch.bfloat16 or t.dim() != 2 or t.stride(1) != 1:
+            raise RuntimeError(f"rows_wgrad_bf16: {name} must be a 2-D bf16 row-major tensor")
+    rows, m = grad_y.shape
+    n = x.shape[1]
+    if x.shape[0] != rows:
+        raise RuntimeError(f"rows_wgrad_bf16: row mismatch {rows} vs {x.shape[0]}")
+    out = torch.empty((m, n), dtype=torch.bfloat16, device=x.device)
+    ws = _workspace(_lib.query("pcfm_rows_wgrad_workspace_bytes", rows, m, n), x)
+    with _timed("rows_wgrad_bf16", 2 * rows * m * n, x, "mfma_bf16"):
+        _lib.call("pcfm_rows_wgrad_bf16", _ptr(grad_y), grad_y.stride(0), _ptr(x), x.stride(0),
+                  rows, m, n, _ptr(out), _ptr(ws), ws.numel(), _stream(x))
+    return out
+
+
+def _p(t):
+    return t.data_ptr() if t is not None else None
+
+
+def head_film_fwd(h16, uprev, gprev, gamma, beta, sp1, shift, n: int, eps: float):
+    """One FiLM block row pass (include/pcfm.h pcfm_head_film_fwd).
+    Returns u f32 (R, W), a bf16 (R, W), mean f32 (R,), rstd f32 (R,)."""
+    ref = h16 if h16 is not None else uprev
+    rows, w = ref.shape
+    b = rows // n
+    dev = ref.device
+    u = torch.empty((rows, w), dtype=torch.float32, device=dev)
+    a = torch.empty((rows, w), dtype=torch.bfloat16, device=dev)
+    mean = torch.empty((rows,), dtype=torch.float32, device=dev)
+    rstd = torch.empty((rows,), dtype=torch.float32, device=dev)
+    with _timed("head_film_fwd", rows * w * (2 if h16 is not None else 6) + rows * w * 6, ref):
+        _lib.call("pcfm_head_film_fwd", _p(h16), _p(uprev), _p(gprev), _p(gamma), _p(beta),
+                  _p(sp1), _p(shift), b, n, w, float(eps), _p(u), _p(a), _p(mean), _p(rstd),
+                  _stream(ref))
+    return u, a, mean, rstd
+
+
+def head_silu_fwd(uprev, gprev, n: int):
+    rows, w = uprev.shape
+    a = torch.empty((rows, w), dtype=torch.bfloat16, device=uprev.device)
+    _lib.call("pcfm_head_silu_fwd", _p(uprev), _p(gprev), rows // n, n, w, _p(a),
+              _stream(uprev))
+    return a
+
+
+def head_film_bwd(dh_next, da16, u, h16, uprev, gprev, mean, rstd, gamma, beta, sp1, n: int,
+                  want_dh: bool):
+    """Returns dh f32 (or None), dh16 bf16, dsp1 f32 (B, W), dshift f32 (B, W),
+    dgamma f32 (W,), dbeta f32 (W,), dbias f32 (W,)."""
+    rows, w = da16.shape
+    b = rows // n
+    dev = da16.device
+    dh = torch.empty((rows, w), dtype=torch.float32, device=dev) if want_dh else None
+    dh16 = torch.empty((rows, w), dtype=torch.bfloat16, device=dev)
+    small = torch.empty((2 * b + 3, w), dtype=torch.float32, device=dev)
+    dsp1, dshift = small[:b], small[b:2 * b]
+    dgamma, dbeta, dbias = small[2 * b], small[2 * b + 1], small[2 * b + 2]
+    ws = _workspace(_lib.query("pcfm_head_bwd_workspace_bytes", b, n, w), da16)
+    with _timed("head_film_bwd", rows * w * (4 + 2 + 4 + (2 if h16 is not None else 6)
+                                             + (4 if want_dh else 0) + 2), da16):
+        _lib.call("pcfm_head_film_bwd", _p(dh_next), _p(da16), _p(u), _p(h16), _p(uprev),
+                  _p(gprev), _p(mean), _p(rstd), _p(gamma), _p(beta), _p(sp1), b, n, w, _p(dh),
+                  _p(dh16), _p(dsp1), _p(dshift), _p(dgamma), _p(dbeta), _p(dbias), _p(ws),
+                  ws.numel(), _stream(da16))
+    return dh, dh16, dsp1, dshift, dgamma, dbeta, dbias
+
+
+def head_silu_bwd(da16, uprev, gprev, n: int):
+    """Returns dh f32, dh16 bf16, dbias f32 (W,)."""
+    rows, w = da16.shape
+    b = rows // n
+    dev = da16.device
+    dh = torch.empty((rows, w), dtype=torch.float32, device=dev)
+    dh16 = torch.empty((rows, w), dtype=torch.bfloat16, device=dev)
+    dbias = torch.empty((w,), dtype=torch.float32, device=dev)
+    ws = _workspace(_lib.query("pcfm_head_bwd_workspace_bytes", b, n, w), da16)
+    _lib.call("pcfm_head_silu_bwd", _p(da16), _p(uprev), _p(gprev), b, n, w, _p(dh), _p(dh16),
+              _p(dbias), _p(ws), ws.numel(), _stream(da16))
+    return dh, dh16, dbias
