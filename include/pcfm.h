@@ -36,7 +36,8 @@ extern "C" {
 #define PCFM_EINVAL -1
 
 /* ABI version: bumped on any signature change (4: voxel and pointwise convolution;
- * 5: per-point head kernels). */
+ * 5: per-point head kernels; 6: conv3d_igemm workspace,
+ * split-operand convolution entry points). */
 int pcfm_abi_version(void);
 /* Thread-local text of the last non-zero return code. */
 const char* pcfm_last_error(void);
@@ -186,7 +187,7 @@ size_t pcfm_conv3d_weight_bytes(int cout, int cin);
 int pcfm_conv3d_prep_weight(const float* w, int cout, int cin, int transpose, void* wsplit,
                             void* stream);
 
-/* 1 if pcfm_conv3d_igemm handles (b, cin, cout, r): cin % 32, cout % 128 and
+/* 1 if pcfm_conv3d_igemm handles (b, cin, cout, r): cin % 64, cout % 128 and
  * r^3 % 128 must all be 0. */
 int pcfm_conv3d_supported(int b, int cin, int cout, int r);
 
@@ -195,7 +196,29 @@ int pcfm_conv3d_supported(int b, int cin, int cout, int r);
  * x = grad_y (cin = C_out, cout = C_in) this is the backward-data pass.
  * Fully writes y. */
 int pcfm_conv3d_igemm(const float* x, const void* wsplit, const float* bias, int b, int cin,
-                      int cout, int r, float* y, void* stream);
+                      int cout, int r, float* y, void* ws, size_t ws_bytes, void* stream);
+
+/* Scratch bytes for pcfm_conv3d_igemm (the channels-last bf16 hi/lo copy of x);
+ * 0 = unsupported shape (cin % 64 is needed). */
+size_t pcfm_conv3d_igemm_workspace_bytes(int b, int cin, int cout, int r);
+
+/* Channels-last split operand of the convolution GEMMs: xs = [hi | lo], each
+ * bf16 [b][r^3][c] with hi = bf16(x), lo = bf16(x - hi), from x f32
+ * [b][c][r^3] (NCDHW).  pcfm_conv3d_split_bytes = its size (0: unsupported,
+ * c % 64 and r^3 % 64 are needed).  A split operand is reusable: the forward
+ * keeps split(x) for the weight gradient, the backward-data pass's split(dY)
+ * feeds it too. */
+size_t pcfm_conv3d_split_bytes(int b, int c, int r);
+int pcfm_conv3d_split(const float* x, int b, int c, int r, void* xs, void* stream);
+
+/* pcfm_conv3d_igemm on an already split input xs (= split(x)). */
+int pcfm_conv3d_igemm_cl(const void* xs, const void* wsplit, const float* bias, int b, int cin,
+                         int cout, int r, float* y, void* stream);
+
+/* pcfm_conv3d_wgrad on split operands xs = split(x), gys = split(grad_y);
+ * same workspace query (pcfm_conv3d_wgrad_workspace_bytes). */
+int pcfm_conv3d_wgrad_cl(const void* xs, const void* gys, int b, int cin, int cout, int r,
+                         float* grad_w, void* ws, size_t ws_bytes, void* stream);
 
 /* Scratch bytes for pcfm_conv3d_wgrad (0 = unsupported shape: cin % 128 is
  * needed in addition to pcfm_conv3d_supported). */

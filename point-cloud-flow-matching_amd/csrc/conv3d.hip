@@ -148,6 +148,198 @@ __global__ void __launch_bounds__(256)
 }
 
 // ---------------------------------------------------------------------------
+// Channels-last split of the GEMM's B operand, done once per convolution
+// instead of once per tap: X fp32 [B][C][V] -> hi, lo bf16 [B][V][C].
+// grid = (V / 64, C / 64, B), 256 threads; a 64 x 64 LDS transpose tile.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256)
+    conv3_split_cl_kernel(const float* __restrict__ x, int C, int V, uint16_t* __restrict__ xh,
+                          uint16_t* __restrict__ xl) {
+  __shared__ float tile[64][65];
+  const int v0 = blockIdx.x * 64, c0 = blockIdx.y * 64, b = blockIdx.z;
+  const int t = threadIdx.x;
+  const float* __restrict__ src = x + ((size_t)b * C + c0) * V + v0;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int c = i * 4 + (t >> 6), v = t & 63;
+    tile[c][v] = src[(size_t)c * V + v];
+  }
+  __syncthreads();
+  const int v = t >> 2, cg = (t & 3) * 16;
+  float f[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) f[q] = tile[cg + q][v];
+  const size_t o = ((size_t)b * V + v0 + v) * C + c0 + cg;
+  store_split<16>(f, xh + o, xl + o);
+}
+
+// ---------------------------------------------------------------------------
+// Forward / backward-data implicit GEMM over the channels-last split input.
+// grid = (V / TN, M / TM, B); K-steps s = tap * (K / KT) + channel chunk.
+// A = pre-split weights W'[tap][m][k], B = pre-split input rows xs[b][v][k]:
+// every staging access is a 16-B copy (no per-tap split arithmetic).  KT = 64
+// channels per step: 48 MFMAs per wave between barriers (TM = TN = 128).
+// LDS rows are KT + 8 bf16 (144 B): conflict-free ds_read_b128 fragments.
+// ---------------------------------------------------------------------------
+template <int TM, int TN, int KT>
+struct TileK {
+  static constexpr int LDR = KT + 8;
+  static constexpr int SI = TM / 64, SJ = TN / 64;
+  static constexpr int A_ELEMS = TM * LDR, B_ELEMS = TN * LDR;
+  static constexpr int BUF = 2 * A_ELEMS + 2 * B_ELEMS;
+  static constexpr int CPR = KT / 8;               // 16-B chunks per row
+  static constexpr int QA = TM * CPR / 256;        // A chunks per thread (per image)
+  static constexpr int QB = TN * CPR / 256;        // B chunks per thread (per image)
+};
+
+template <int TM, int TN, int KT>
+__device__ __forceinline__ void tile_mfma_k(const uint16_t* buf, int wr, int wc, int r, int h,
+                                            f32x16 (&acc)[TM / 64][TN / 64]) {
+  using T = TileK<TM, TN, KT>;
+  const uint16_t* sAh = buf;
+  const uint16_t* sAl = buf + T::A_ELEMS;
+  const uint16_t* sBh = buf + 2 * T::A_ELEMS;
+  const uint16_t* sBl = sBh + T::B_ELEMS;
+#pragma unroll
+  for (int kk = 0; kk < KT / 16; ++kk) {
+    bf16x8 ah[T::SI], al[T::SI], bh[T::SJ], bl[T::SJ];
+#pragma unroll
+    for (int i = 0; i < T::SI; ++i) {
+      const int o = (wr * (TM / 2) + i * 32 + r) * T::LDR + kk * 16 + 8 * h;
+      ah[i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(sAh + o));
+      al[i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(sAl + o));
+    }
+#pragma unroll
+    for (int j = 0; j < T::SJ; ++j) {
+      const int o = (wc * (TN / 2) + j * 32 + r) * T::LDR + kk * 16 + 8 * h;
+      bh[j] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(sBh + o));
+      bl[j] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(sBl + o));
+    }
+#pragma unroll
+    for (int i = 0; i < T::SI; ++i)
+#pragma unroll
+      for (int j = 0; j < T::SJ; ++j) {
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
+      }
+  }
+}
+
+// Staging registers as one vector value per operand image (an array of uint4
+// captured by the load/store lambdas is placed in scratch by hipcc).
+template <int Q>
+using StageVec = unsigned int __attribute__((ext_vector_type(4 * Q)));
+template <int Q>
+__device__ __forceinline__ void sv_put(StageVec<Q>& v, int q, uint4 x) {
+  v[4 * q] = x.x;
+  v[4 * q + 1] = x.y;
+  v[4 * q + 2] = x.z;
+  v[4 * q + 3] = x.w;
+}
+template <int Q>
+__device__ __forceinline__ uint4 sv_get(const StageVec<Q>& v, int q) {
+  return uint4{v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
+}
+
+template <int TM, int TN, int KT>
+__global__ void __launch_bounds__(256)
+    conv3_igemm_cl_kernel(const uint16_t* __restrict__ xh, const uint16_t* __restrict__ xl,
+                          const uint16_t* __restrict__ wh, const uint16_t* __restrict__ wl,
+                          const float* __restrict__ bias, float* __restrict__ y, int K, int M,
+                          int R) {
+  using T = TileK<TM, TN, KT>;
+  __shared__ __attribute__((aligned(16))) uint16_t lds[T::BUF];
+  const int V = R * R * R, R2 = R * R;
+  const int b = blockIdx.z, m0 = blockIdx.y * TM, v0 = blockIdx.x * TN;
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wr = w >> 1, wc = w & 1, r = lane & 31, h = lane >> 5;
+  const uint16_t* __restrict__ xbh = xh + (size_t)b * V * K;
+  const uint16_t* __restrict__ xbl = xl + (size_t)b * V * K;
+  const int nck = K / KT, nsteps = 27 * nck;
+  // chunk q of this thread: row (t + 256 q) / CPR, 8-channel column (t % CPR) * 8
+  const int col = (t % T::CPR) * 8;
+  int bv[T::QB], bx[T::QB], by[T::QB], bz[T::QB];
+#pragma unroll
+  for (int q = 0; q < T::QB; ++q) {
+    bv[q] = v0 + (t + 256 * q) / T::CPR;
+    bx[q] = bv[q] / R2;
+    by[q] = (bv[q] / R) % R;
+    bz[q] = bv[q] % R;
+  }
+
+  StageVec<T::QA> rah, ral;
+  StageVec<T::QB> rbh, rbl;
+  auto load = [&](int s) {
+    const int tap = s / nck, c0 = (s - tap * nck) * KT;
+#pragma unroll
+    for (int q = 0; q < T::QA; ++q) {
+      const int row = (t + 256 * q) / T::CPR;
+      const size_t g = ((size_t)tap * M + m0 + row) * K + c0 + col;
+      sv_put<T::QA>(rah, q, *reinterpret_cast<const uint4*>(wh + g));
+      sv_put<T::QA>(ral, q, *reinterpret_cast<const uint4*>(wl + g));
+    }
+    const int dx = tap / 9 - 1, dy = (tap / 3) % 3 - 1, dz = tap % 3 - 1;
+    const int doff = dx * R2 + dy * R + dz;
+#pragma unroll
+    for (int q = 0; q < T::QB; ++q) {
+      const bool inb = (unsigned)(bx[q] + dx) < (unsigned)R &&
+                       (unsigned)(by[q] + dy) < (unsigned)R && (unsigned)(bz[q] + dz) < (unsigned)R;
+      const size_t o = (size_t)(inb ? bv[q] + doff : bv[q]) * K + c0 + col;
+      const uint4 hv = *reinterpret_cast<const uint4*>(xbh + o);
+      const uint4 lv = *reinterpret_cast<const uint4*>(xbl + o);
+      sv_put<T::QB>(rbh, q, inb ? hv : uint4{0u, 0u, 0u, 0u});
+      sv_put<T::QB>(rbl, q, inb ? lv : uint4{0u, 0u, 0u, 0u});
+    }
+  };
+  auto store = [&](uint16_t* buf) {
+#pragma unroll
+    for (int q = 0; q < T::QA; ++q) {
+      uint16_t* d = buf + ((t + 256 * q) / T::CPR) * T::LDR + col;
+      *reinterpret_cast<uint4*>(d) = sv_get<T::QA>(rah, q);
+      *reinterpret_cast<uint4*>(d + T::A_ELEMS) = sv_get<T::QA>(ral, q);
+    }
+#pragma unroll
+    for (int q = 0; q < T::QB; ++q) {
+      uint16_t* d = buf + 2 * T::A_ELEMS + ((t + 256 * q) / T::CPR) * T::LDR + col;
+      *reinterpret_cast<uint4*>(d) = sv_get<T::QB>(rbh, q);
+      *reinterpret_cast<uint4*>(d + T::B_ELEMS) = sv_get<T::QB>(rbl, q);
+    }
+  };
+
+  f32x16 acc[T::SI][T::SJ];
+#pragma unroll
+  for (int i = 0; i < T::SI; ++i)
+#pragma unroll
+    for (int j = 0; j < T::SJ; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
+
+  load(0);
+  store(lds);
+  __syncthreads();
+  for (int s = 0; s < nsteps; ++s) {
+    if (s + 1 < nsteps) load(s + 1);
+    tile_mfma_k<TM, TN, KT>(lds, wr, wc, r, h, acc);
+    __syncthreads();
+    if (s + 1 < nsteps) store(lds);
+    __syncthreads();
+  }
+  float* __restrict__ yb = y + (size_t)b * M * V;
+#pragma unroll
+  for (int i = 0; i < T::SI; ++i)
+#pragma unroll
+    for (int j = 0; j < T::SJ; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int m = m0 + wr * (TM / 2) + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+        const int v = v0 + wc * (TN / 2) + j * 32 + r;
+        yb[(size_t)m * V + v] = acc[i][j][e] + (bias != nullptr ? bias[m] : 0.0f);
+      }
+}
+
+// ---------------------------------------------------------------------------
 // Weight gradient: dW[co, ci, tap] = sum_{b, v} dY[b, co, v] * X[b, ci, v + off(tap)]
 // One GEMM per tap with K = B*V voxels: A = dY tile [co][voxel], B = shifted X
 // tile [ci][voxel] -- both are voxel-contiguous rows of the NCDHW tensors, so
@@ -284,6 +476,138 @@ __global__ void __launch_bounds__(256)
       }
 }
 
+// ---------------------------------------------------------------------------
+// Weight gradient over the channels-last split operands (the forward's split
+// input xs and the backward-data pass's split dY): per tap a GEMM reducing over
+// voxels, dW[co][ci] = sum_v dY[v][co] * X[v + off][ci], both operands
+// row-major [voxel][channel], so the LDS images are the global rows as they lie
+// ([64 voxels][128 channels], T10 swizzle) and the MFMA operands (8 consecutive
+// voxels per lane) come from ds_read_b64_tr_b16.  Rows whose neighbour is out of
+// the grid are zero (padding).  Same 1-D item order, XCD deal and partial
+// layout as conv3_wgrad_kernel; 48 MFMAs per wave per 64-voxel step.
+// ---------------------------------------------------------------------------
+constexpr int kWV = 64;  // voxels per K-step
+
+__global__ void __launch_bounds__(256)
+    conv3_wgrad_cl_kernel(const uint16_t* __restrict__ xh, const uint16_t* __restrict__ xl,
+                          const uint16_t* __restrict__ gh, const uint16_t* __restrict__ gl,
+                          int B, int cin, int cout, int R, int S, float* __restrict__ part) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[4 * kWV * 256];
+  uint8_t* iAh = lds;
+  uint8_t* iAl = lds + kWV * 256;
+  uint8_t* iBh = lds + 2 * kWV * 256;
+  uint8_t* iBl = lds + 3 * kWV * 256;
+  const int V = R * R * R, R2 = R * R;
+  const int nco = cout / kMT;
+  int id = (int)blockIdx.x;
+  {
+    const int nwg = (int)gridDim.x, q = nwg / 8, rr = nwg % 8, xcd = id % 8;
+    id = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + id / 8;
+  }
+  const int tap = id % 27;
+  id /= 27;
+  const int sp = id % S;
+  id /= S;
+  const int co0 = (id % nco) * kMT;
+  const int ci0 = (id / nco) * kMT;
+  const long long nsteps = (long long)B * V / kWV;
+  const long long k0 = nsteps * sp / S, k1 = nsteps * (sp + 1) / S;
+  const int dx = tap / 9 - 1, dy_ = (tap / 3) % 3 - 1, dz = tap % 3 - 1;
+  const int off = dx * R2 + dy_ * R + dz;
+
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wr = w >> 1, wc = w & 1;
+  const int ch = t & 15;  // 16-B chunk of the 128-channel row
+
+  StageVec<4> rah, ral, rbh, rbl;
+  auto load = [&](long long ks) {
+    const long long gv0 = ks * kWV;
+    const int b = (int)(gv0 / V), v0 = (int)(gv0 - (long long)b * V);
+    const size_t rowA = (size_t)b * V;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int row = (t >> 4) + 16 * q;
+      const int v = v0 + row;
+      const size_t ga = (rowA + v) * cout + co0 + ch * 8;
+      sv_put<4>(rah, q, *reinterpret_cast<const uint4*>(gh + ga));
+      sv_put<4>(ral, q, *reinterpret_cast<const uint4*>(gl + ga));
+      const int xq = v / R2, yq = (v / R) % R, zq = v % R;
+      const bool inb = (unsigned)(xq + dx) < (unsigned)R && (unsigned)(yq + dy_) < (unsigned)R &&
+                       (unsigned)(zq + dz) < (unsigned)R;
+      const size_t gb = (rowA + (inb ? v + off : v)) * cin + ci0 + ch * 8;
+      const uint4 hv = *reinterpret_cast<const uint4*>(xh + gb);
+      const uint4 lv = *reinterpret_cast<const uint4*>(xl + gb);
+      sv_put<4>(rbh, q, inb ? hv : uint4{0u, 0u, 0u, 0u});
+      sv_put<4>(rbl, q, inb ? lv : uint4{0u, 0u, 0u, 0u});
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int o = swz256((t >> 4) + 16 * q, ch);
+      *reinterpret_cast<uint4*>(iAh + o) = sv_get<4>(rah, q);
+      *reinterpret_cast<uint4*>(iAl + o) = sv_get<4>(ral, q);
+      *reinterpret_cast<uint4*>(iBh + o) = sv_get<4>(rbh, q);
+      *reinterpret_cast<uint4*>(iBl + o) = sv_get<4>(rbl, q);
+    }
+  };
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
+
+  if (k0 < k1) {
+    load(k0);
+    store();
+  }
+  __syncthreads();
+  for (long long ks = k0; ks < k1; ++ks) {
+    if (ks + 1 < k1) load(ks + 1);
+#pragma unroll
+    for (int kk = 0; kk < kWV / 16; ++kk) {
+      bf16x8 ah[2], al[2], bh[2], bl[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        ah[i] = tr_operand(iAh, kk, wr * 64 + i * 32, lane);
+        al[i] = tr_operand(iAl, kk, wr * 64 + i * 32, lane);
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        bh[j] = tr_operand(iBh, kk, wc * 64 + j * 32, lane);
+        bl[j] = tr_operand(iBl, kk, wc * 64 + j * 32, lane);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
+        }
+    }
+    __syncthreads();
+    if (ks + 1 < k1) store();
+    __syncthreads();
+  }
+  float* pb = part + ((size_t)sp * 27 + tap) * cout * cin;
+  const int h = lane >> 5, r = lane & 31;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int co = co0 + wr * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+        const int ci = ci0 + wc * 64 + j * 32 + r;
+        pb[(size_t)co * cin + ci] = acc[i][j][e];
+      }
+}
+
 // dw[co][ci][tap] = sum_s part[s][tap][co][ci], in split order
 __global__ void __launch_bounds__(256)
     conv3_wgrad_reduce_kernel(const float* __restrict__ part, int cout, int cin, int S,
@@ -324,7 +648,7 @@ int conv3_wgrad_splits(int B, int cin, int cout, int R) {
 bool conv3_shape_ok(int b, int cin, int cout, int r) {
   if (b < 0 || cin <= 0 || cout <= 0 || r <= 0 || r > 1024) return false;
   const long long v = (long long)r * r * r;
-  return cin % kKT == 0 && cout % kMT == 0 && v % kNT == 0 && v < (1LL << 31);
+  return cin % 64 == 0 && cout % kMT == 0 && v % kNT == 0 && v < (1LL << 31);
 }
 
 }  // namespace
@@ -351,24 +675,40 @@ extern "C" int pcfm_conv3d_supported(int b, int cin, int cout, int r) {
   return conv3_shape_ok(b, cin, cout, r) ? 1 : 0;
 }
 
+#ifndef PCFM_CONV_KT
+#define PCFM_CONV_KT 64
+#endif
+
+extern "C" size_t pcfm_conv3d_igemm_workspace_bytes(int b, int cin, int cout, int r) {
+  if (!conv3_shape_ok(b, cin, cout, r) || cin % 64 != 0) return 0;
+  return (size_t)2 * b * r * r * r * cin * sizeof(uint16_t);
+}
+
 extern "C" int pcfm_conv3d_igemm(const float* x, const void* wsplit, const float* bias, int b,
-                                 int cin, int cout, int r, float* y, void* stream) {
-  PCFM_CHECK_ARG(conv3_shape_ok(b, cin, cout, r),
-                 "conv3d_igemm: unsupported shape b=%d cin=%d cout=%d r=%d (need cin %% %d, "
+                                 int cin, int cout, int r, float* y, void* ws, size_t ws_bytes,
+                                 void* stream) {
+  PCFM_CHECK_ARG(conv3_shape_ok(b, cin, cout, r) && cin % 64 == 0,
+                 "conv3d_igemm: unsupported shape b=%d cin=%d cout=%d r=%d (need cin %% 64, "
                  "cout %% %d, r^3 %% %d == 0)",
-                 b, cin, cout, r, kKT, kMT, kNT);
+                 b, cin, cout, r, kMT, kNT);
   if (b == 0) return PCFM_OK;
+  const size_t need = pcfm_conv3d_igemm_workspace_bytes(b, cin, cout, r);
+  PCFM_CHECK_ARG(ws_bytes >= need, "conv3d_igemm: workspace %zu < %zu bytes", ws_bytes, need);
   const int V = r * r * r;
   const size_t total = (size_t)27 * cout * cin;
   const uint16_t* wh = (const uint16_t*)wsplit;
   hipStream_t st = (hipStream_t)stream;
+  uint16_t* xh = (uint16_t*)ws;
+  uint16_t* xl = xh + (size_t)b * V * cin;
+  hipLaunchKernelGGL(conv3_split_cl_kernel, dim3(V / 64, cin / 64, b), dim3(256), 0, st, x, cin,
+                     V, xh, xl);
   const long long big_blocks = (long long)(V / 128) * (cout / 128) * b;
   if (big_blocks >= 2 * kCUs) {
-    hipLaunchKernelGGL((conv3_igemm_kernel<128, 128>), dim3(V / 128, cout / 128, b), dim3(256), 0,
-                       st, x, wh, wh + total, bias, y, cin, cout, r);
+    hipLaunchKernelGGL((conv3_igemm_cl_kernel<128, 128, PCFM_CONV_KT>), dim3(V / 128, cout / 128, b),
+                       dim3(256), 0, st, xh, xl, wh, wh + total, bias, y, cin, cout, r);
   } else {
-    hipLaunchKernelGGL((conv3_igemm_kernel<64, 64>), dim3(V / 64, cout / 64, b), dim3(256), 0, st,
-                       x, wh, wh + total, bias, y, cin, cout, r);
+    hipLaunchKernelGGL((conv3_igemm_cl_kernel<64, 64, PCFM_CONV_KT>), dim3(V / 64, cout / 64, b), dim3(256), 0,
+                       st, xh, xl, wh, wh + total, bias, y, cin, cout, r);
   }
   return check_launch("conv3d_igemm");
 }
@@ -393,4 +733,63 @@ extern "C" int pcfm_conv3d_wgrad(const float* x, const float* grad_y, int b, int
   hipLaunchKernelGGL(conv3_wgrad_reduce_kernel, dim3(ceil_div((long long)total, 256)), dim3(256),
                      0, st, (const float*)ws, cout, cin, S, grad_w);
   return check_launch("conv3d_wgrad");
+}
+
+extern "C" size_t pcfm_conv3d_split_bytes(int b, int c, int r) {
+  if (b <= 0 || c <= 0 || c % 64 != 0 || r <= 0 || ((long long)r * r * r) % 64 != 0) return 0;
+  return (size_t)2 * b * r * r * r * c * sizeof(uint16_t);
+}
+
+extern "C" int pcfm_conv3d_split(const float* x, int b, int c, int r, void* xs, void* stream) {
+  PCFM_CHECK_ARG(pcfm_conv3d_split_bytes(b, c, r) > 0, "conv3d_split: bad shape b=%d c=%d r=%d",
+                 b, c, r);
+  const int V = r * r * r;
+  uint16_t* xh = (uint16_t*)xs;
+  hipLaunchKernelGGL(conv3_split_cl_kernel, dim3(V / 64, c / 64, b), dim3(256), 0,
+                     (hipStream_t)stream, x, c, V, xh, xh + (size_t)b * V * c);
+  return check_launch("conv3d_split");
+}
+
+extern "C" int pcfm_conv3d_igemm_cl(const void* xs, const void* wsplit, const float* bias, int b,
+                                    int cin, int cout, int r, float* y, void* stream) {
+  PCFM_CHECK_ARG(conv3_shape_ok(b, cin, cout, r),
+                 "conv3d_igemm_cl: unsupported shape b=%d cin=%d cout=%d r=%d", b, cin, cout, r);
+  if (b == 0) return PCFM_OK;
+  const int V = r * r * r;
+  const size_t total = (size_t)27 * cout * cin;
+  const uint16_t* wh = (const uint16_t*)wsplit;
+  const uint16_t* xh = (const uint16_t*)xs;
+  const uint16_t* xl = xh + (size_t)b * V * cin;
+  hipStream_t st = (hipStream_t)stream;
+  const long long big_blocks = (long long)(V / 128) * (cout / 128) * b;
+  if (big_blocks >= 2 * kCUs) {
+    hipLaunchKernelGGL((conv3_igemm_cl_kernel<128, 128, PCFM_CONV_KT>), dim3(V / 128, cout / 128, b),
+                       dim3(256), 0, st, xh, xl, wh, wh + total, bias, y, cin, cout, r);
+  } else {
+    hipLaunchKernelGGL((conv3_igemm_cl_kernel<64, 64, PCFM_CONV_KT>), dim3(V / 64, cout / 64, b),
+                       dim3(256), 0, st, xh, xl, wh, wh + total, bias, y, cin, cout, r);
+  }
+  return check_launch("conv3d_igemm_cl");
+}
+
+extern "C" int pcfm_conv3d_wgrad_cl(const void* xs, const void* gys, int b, int cin, int cout,
+                                    int r, float* grad_w, void* ws, size_t ws_bytes,
+                                    void* stream) {
+  PCFM_CHECK_ARG(b > 0 && conv3_shape_ok(b, cin, cout, r) && cin % kMT == 0,
+                 "conv3d_wgrad_cl: unsupported shape b=%d cin=%d cout=%d r=%d", b, cin, cout, r);
+  const size_t need = pcfm_conv3d_wgrad_workspace_bytes(b, cin, cout, r);
+  PCFM_CHECK_ARG(ws_bytes >= need, "conv3d_wgrad_cl: workspace %zu < %zu bytes", ws_bytes, need);
+  const int S = conv3_wgrad_splits(b, cin, cout, r);
+  const int V = r * r * r;
+  hipStream_t st = (hipStream_t)stream;
+  const int tiles = 27 * (cout / kMT) * (cin / kMT);
+  const uint16_t* xh = (const uint16_t*)xs;
+  const uint16_t* gh = (const uint16_t*)gys;
+  hipLaunchKernelGGL(conv3_wgrad_cl_kernel, dim3(tiles * S), dim3(256), 0, st, xh,
+                     xh + (size_t)b * V * cin, gh, gh + (size_t)b * V * cout, b, cin, cout, r, S,
+                     (float*)ws);
+  const size_t total = (size_t)27 * cout * cin;
+  hipLaunchKernelGGL(conv3_wgrad_reduce_kernel, dim3(ceil_div((long long)total, 256)), dim3(256),
+                     0, st, (const float*)ws, cout, cin, S, grad_w);
+  return check_launch("conv3d_wgrad_cl");
 }

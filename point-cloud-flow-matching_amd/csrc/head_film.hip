@@ -275,27 +275,42 @@ __global__ void __launch_bounds__(256)
   }
 }
 
-// Per-batch sums (k = 0, 1 -> dsp1 / dshift [B][W]) and global sums (k = 2, 3,
-// 4 -> dgamma / dbeta / dbias [W]) of the block partials, in block order; a null
-// output is skipped.  grid = (ceil(W / 64), 5), 64 threads.
-__global__ void __launch_bounds__(64)
+// Stage 1: per-batch sums of the block partials, chunk order fixed (4 thread
+// groups take every 4th chunk, combined in group order).  k = 0, 1 go straight
+// to dsp1 / dshift [B][W]; k = 2..4 go to perb[k - 2][B][W] for stage 2.
+// grid = (ceil(W / 64), 5, B), 256 threads.
+__global__ void __launch_bounds__(256)
     film_bwd_reduce_kernel(const float* __restrict__ part, int B, int chunks, int W,
                            float* __restrict__ dsp1, float* __restrict__ dshift,
-                           float* __restrict__ dgamma, float* __restrict__ dbeta,
-                           float* __restrict__ dbias) {
-  const int c = blockIdx.x * 64 + threadIdx.x, k = blockIdx.y;
-  float* const outs[kSums] = {dsp1, dshift, dgamma, dbeta, dbias};
-  float* out = outs[k];
-  if (c >= W || out == nullptr) return;
-  float tot = 0.0f;
-  for (int b = 0; b < B; ++b) {
-    float s = 0.0f;
+                           float* __restrict__ perb) {
+  __shared__ float red[4][64];
+  const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl, k = blockIdx.y, b = blockIdx.z;
+  float s = 0.0f;
+  if (c < W) {
     const float* p = part + ((size_t)b * chunks * kSums + k) * W + c;
-    for (int q = 0; q < chunks; ++q) s += p[(size_t)q * kSums * W];
-    if (k < 2) out[(size_t)b * W + c] = s;
-    tot += s;
+    for (int q = grp; q < chunks; q += 4) s += p[(size_t)q * kSums * W];
   }
-  if (k >= 2) out[c] = tot;
+  red[grp][cl] = s;
+  __syncthreads();
+  if (grp != 0 || c >= W) return;
+  s = ((red[0][cl] + red[1][cl]) + red[2][cl]) + red[3][cl];
+  float* out = k == 0 ? dsp1 : k == 1 ? dshift : perb + (size_t)(k - 2) * B * W;
+  if (out != nullptr) out[(size_t)b * W + c] = s;
+}
+
+// Stage 2: global sums over the batch (k = 2..4 -> dgamma / dbeta / dbias [W]);
+// a null output is skipped.  grid = (ceil(W / 64), 3), 64 threads.
+__global__ void __launch_bounds__(64)
+    film_bwd_reduce2_kernel(const float* __restrict__ perb, int B, int W,
+                            float* __restrict__ dgamma, float* __restrict__ dbeta,
+                            float* __restrict__ dbias) {
+  const int c = blockIdx.x * 64 + threadIdx.x, k = blockIdx.y;
+  float* out = k == 0 ? dgamma : k == 1 ? dbeta : dbias;
+  if (c >= W || out == nullptr) return;
+  float s = 0.0f;
+  for (int b = 0; b < B; ++b) s += perb[((size_t)k * B + b) * W + c];
+  out[c] = s;
 }
 
 bool film_ok(int b, int n, int w) {
@@ -348,8 +363,11 @@ int launch_bwd(const float* dhn, const void* da16, const float* u, const void* h
       hipLaunchKernelGGL((film_bwd_kernel<2, FILM>), grid, blk, 0, st, dhn, DA, u, H, uprev, G,
                          mean, rstd, gamma, beta, S1, n, dh, D16, part);
   }
-  hipLaunchKernelGGL(film_bwd_reduce_kernel, dim3(ceil_div(w, 64), kSums), dim3(64), 0, st,
-                     (const float*)part, b, chunks, w, dsp1, dshift, dgamma, dbeta, dbias);
+  float* perb = part + (size_t)b * chunks * kSums * w;
+  hipLaunchKernelGGL(film_bwd_reduce_kernel, dim3(ceil_div(w, 64), kSums, b), dim3(256), 0, st,
+                     (const float*)part, b, chunks, w, dsp1, dshift, perb);
+  hipLaunchKernelGGL(film_bwd_reduce2_kernel, dim3(ceil_div(w, 64), 3), dim3(64), 0, st,
+                     (const float*)perb, b, w, dgamma, dbeta, dbias);
   return check_launch(FILM ? "head_film_bwd" : "head_silu_bwd");
 }
 
@@ -378,7 +396,7 @@ extern "C" int pcfm_head_silu_fwd(const float* uprev, const void* gprev, int b, 
 
 extern "C" size_t pcfm_head_bwd_workspace_bytes(int b, int n, int w) {
   if (!film_ok(b, n, w)) return 0;
-  return (size_t)b * ceil_div(n, kRowsPerBlock) * kSums * w * sizeof(float);
+  return ((size_t)b * ceil_div(n, kRowsPerBlock) * kSums + 3 * (size_t)b) * w * sizeof(float);
 }
 
 extern "C" int pcfm_head_film_bwd(const float* dh_next, const void* da16, const float* u,

@@ -110,5 +110,34 @@ __device__ __forceinline__ void store_split(const float (&v)[N], uint16_t* dh, u
 }
 
 
+// ---------------------------------------------------------------------------
+// Transposed-read images (cdna_hip_programming.md T10): a [rows][128] bf16
+// tile stored as it lies in memory (256-B rows, 16-B chunks XOR-swizzled) and
+// read with ds_read_b64_tr_b16, which delivers 4 consecutive ROWS of one
+// column per lane -- the MFMA operand for a reduction over the row index.
+// ---------------------------------------------------------------------------
+typedef short v4s_tr __attribute__((ext_vector_type(4)));
+
+// byte offset of 16-B chunk `ch` (0..15) of row `row` (the T10 (b) swizzle)
+__device__ __forceinline__ int swz256(int row, int ch) {
+  return 256 * row + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
+}
+
+__device__ __forceinline__ v4s_tr tr_read16(const uint8_t* base, int off) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) v4s_tr*)(base + off));
+}
+
+// 32x32x16 operand (8 consecutive rows kk*16 + 8*(lane/32) .. +8 of column
+// col0 + lane%32) from a swizzled [rows][128] image
+__device__ __forceinline__ bf16x8 tr_operand(const uint8_t* img, int kk, int col0, int lane) {
+  const int g = lane >> 4, i16 = lane & 15, q4 = i16 >> 2, p4 = i16 & 3;
+  const int row = kk * 16 + 8 * (g >> 1) + q4;
+  const int col = col0 + (g & 1) * 16 + 4 * p4;
+  const v4s_tr x0 = tr_read16(img, swz256(row, col >> 3) + 8 * (p4 & 1));
+  const v4s_tr x1 = tr_read16(img, swz256(row + 4, col >> 3) + 8 * (p4 & 1));
+  return __builtin_bit_cast(bf16x8, __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+
 }  // namespace
 }  // namespace pcfm

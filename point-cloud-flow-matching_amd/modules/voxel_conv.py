@@ -18,26 +18,36 @@ __all__ = ["VoxelConv3d"]
 
 
 class _Conv3dX3(torch.autograd.Function):
+    """Forward keeps split(x) (channels-last bf16 hi/lo, the GEMM's B operand)
+    instead of x; the backward splits dY once and uses it for both the
+    backward-data GEMM and the weight gradient."""
+
     @staticmethod
     def forward(ctx, x, weight, bias):
         from pcfm import ops
-        ctx.save_for_backward(x, weight)
+        x = x.contiguous()
+        b, cin, r = x.shape[0], x.shape[1], x.shape[2]
+        cout = weight.shape[0]
+        xs = ops.conv3d_split(x)
+        y = ops.conv3d_igemm_split(xs, ops.conv3d_prep_weight(weight, False), bias, b, cin, cout,
+                                   r, "conv3d_fwd")
+        ctx.save_for_backward(xs, weight)
         ctx.has_bias = bias is not None
-        return ops.conv3d_forward(x, weight, bias)
+        ctx.dims = (b, cin, cout, r)
+        return y
 
     @staticmethod
     def backward(ctx, gy):
         from pcfm import ops
-        x, weight = ctx.saved_tensors
-        gy = gy.contiguous()
+        xs, weight = ctx.saved_tensors
+        b, cin, cout, r = ctx.dims
+        gys = ops.conv3d_split(gy.contiguous())
         gx = gw = gb = None
         if ctx.needs_input_grad[0]:
-            gx = ops.conv3d_backward_data(gy, weight)
+            gx = ops.conv3d_igemm_split(gys, ops.conv3d_prep_weight(weight, True), None, b, cout,
+                                        cin, r, "conv3d_bwd_data")
         if ctx.needs_input_grad[1]:
-            if ops.conv3d_wgrad_supported(x, weight):
-                gw = ops.conv3d_backward_weight(x, gy)
-            else:
-                gw = torch.nn.grad.conv3d_weight(x, weight.shape, gy, stride=1, padding=1)
+            gw = ops.conv3d_wgrad_split(xs, gys, b, cin, cout, r)
         if ctx.has_bias and ctx.needs_input_grad[2]:
             gb = gy.sum(dim=(0, 2, 3, 4))
         return gx, gw, gb
@@ -53,6 +63,6 @@ class VoxelConv3d(nn.Conv3d):
                 or self.padding_mode != "zeros"):
             return super().forward(x)
         from pcfm import ops
-        if not ops.conv3d_supported(x, self.weight):
+        if not (ops.conv3d_supported(x, self.weight) and ops.conv3d_wgrad_supported(x, self.weight)):
             return super().forward(x)
         return _Conv3dX3.apply(x, self.weight, self.bias)

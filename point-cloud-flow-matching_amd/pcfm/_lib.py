@@ -50,7 +50,12 @@ SIGNATURES = {
     "pcfm_conv3d_weight_bytes": (_Z, [_I, _I]),
     "pcfm_conv3d_prep_weight": (_I, [_P, _I, _I, _I, _P, _P]),
     "pcfm_conv3d_supported": (_I, [_I, _I, _I, _I]),
-    "pcfm_conv3d_igemm": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P]),
+    "pcfm_conv3d_igemm": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P, _Z, _P]),
+    "pcfm_conv3d_igemm_workspace_bytes": (_Z, [_I, _I, _I, _I]),
+    "pcfm_conv3d_split_bytes": (_Z, [_I, _I, _I]),
+    "pcfm_conv3d_split": (_I, [_P, _I, _I, _I, _P, _P]),
+    "pcfm_conv3d_igemm_cl": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P]),
+    "pcfm_conv3d_wgrad_cl": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, _Z, _P]),
     "pcfm_conv3d_wgrad_workspace_bytes": (_Z, [_I, _I, _I, _I]),
     "pcfm_conv3d_wgrad": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, _Z, _P]),
     "pcfm_pointwise_weight_bytes": (_Z, [_I, _I]),
@@ -69,7 +74,7 @@ SIGNATURES = {
     "pcfm_head_silu_bwd": (_I, [_P, _P, _P, _I, _I, _I, _P, _P, _P, _P, _Z, _P]),
 }
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 _lock = threading.Lock()
 _lib = None

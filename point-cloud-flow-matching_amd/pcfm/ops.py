@@ -391,9 +391,10 @@ def conv3d_forward(x: torch.Tensor, weight: torch.Tensor, bias) -> torch.Tensor:
     img = conv3d_prep_weight(weight, False)
     y = torch.empty((b, cout, r, r, r), dtype=torch.float32, device=x.device)
     bias_p = _ptr(bias.contiguous()) if bias is not None else None
+    ws = _workspace(_lib.query("pcfm_conv3d_igemm_workspace_bytes", b, cin, cout, r), x)
     with _timed("conv3d_fwd", 54 * b * r ** 3 * cin * cout, x, "mfma"):
         _lib.call("pcfm_conv3d_igemm", _ptr(x), _ptr(img), bias_p, b, cin, cout, r, _ptr(y),
-                  _stream(x))
+                  _ptr(ws), ws.numel(), _stream(x))
     return y
 
 
@@ -405,9 +406,10 @@ def conv3d_backward_data(grad_y: torch.Tensor, weight: torch.Tensor) -> torch.Te
     cin = weight.shape[1]
     img = conv3d_prep_weight(weight, True)
     dx = torch.empty((b, cin, r, r, r), dtype=torch.float32, device=g.device)
+    ws = _workspace(_lib.query("pcfm_conv3d_igemm_workspace_bytes", b, cout, cin, r), g)
     with _timed("conv3d_bwd_data", 54 * b * r ** 3 * cin * cout, g, "mfma"):
         _lib.call("pcfm_conv3d_igemm", _ptr(g), _ptr(img), None, b, cout, cin, r, _ptr(dx),
-                  _stream(g))
+                  _ptr(ws), ws.numel(), _stream(g))
     return dx
 
 
@@ -423,6 +425,46 @@ def conv3d_backward_weight(x: torch.Tensor, grad_y: torch.Tensor) -> torch.Tenso
     with _timed("conv3d_wgrad", 54 * b * r ** 3 * cin * cout, x, "mfma"):
         _lib.call("pcfm_conv3d_wgrad", _ptr(x), _ptr(g), b, cin, cout, r, _ptr(dw), _ptr(ws),
                   ws.numel(), _stream(x))
+    return dw
+
+
+def conv3d_split(x: torch.Tensor) -> torch.Tensor:
+    """Channels-last bf16 hi/lo split of a (B, C, R, R, R) fp32 tensor
+    (pcfm_conv3d_split); opaque uint8 storage for the split-operand entry points."""
+    _check(x, "input", "f")
+    b, c, r = x.shape[0], x.shape[1], x.shape[2]
+    n = _lib.query("pcfm_conv3d_split_bytes", b, c, r)
+    if n == 0:
+        raise RuntimeError(f"conv3d_split: unsupported shape {tuple(x.shape)}")
+    xs = torch.empty(n, dtype=torch.uint8, device=x.device)
+    _lib.call("pcfm_conv3d_split", _ptr(x), b, c, r, _ptr(xs), _stream(x))
+    return xs
+
+
+def conv3d_split_supported(x: torch.Tensor) -> bool:
+    return _lib.query("pcfm_conv3d_split_bytes", x.shape[0], x.shape[1], x.shape[2]) > 0
+
+
+def conv3d_igemm_split(xs: torch.Tensor, img: torch.Tensor, bias, b: int, cin: int, cout: int,
+                       r: int, op: str) -> torch.Tensor:
+    """y (b, cout, r, r, r) from a split input (forward, or backward-data with the
+    transposed weight image)."""
+    y = torch.empty((b, cout, r, r, r), dtype=torch.float32, device=xs.device)
+    bias_p = _ptr(bias.contiguous()) if bias is not None else None
+    with _timed(op, 54 * b * r ** 3 * cin * cout, xs, "mfma"):
+        _lib.call("pcfm_conv3d_igemm_cl", _ptr(xs), _ptr(img), bias_p, b, cin, cout, r, _ptr(y),
+                  _stream(xs))
+    return y
+
+
+def conv3d_wgrad_split(xs: torch.Tensor, gys: torch.Tensor, b: int, cin: int, cout: int,
+                       r: int) -> torch.Tensor:
+    """dW (cout, cin, 3, 3, 3) from split(x) and split(grad_y)."""
+    ws = _workspace(_lib.query("pcfm_conv3d_wgrad_workspace_bytes", b, cin, cout, r), xs)
+    dw = torch.empty((cout, cin, 3, 3, 3), dtype=torch.float32, device=xs.device)
+    with _timed("conv3d_wgrad", 54 * b * r ** 3 * cin * cout, xs, "mfma"):
+        _lib.call("pcfm_conv3d_wgrad_cl", _ptr(xs), _ptr(gys), b, cin, cout, r, _ptr(dw),
+                  _ptr(ws), ws.numel(), _stream(xs))
     return dw
 
 

@@ -26,7 +26,7 @@ def ops():
 
 
 @pytest.mark.parametrize("b,cin,cout,r", [(2, 128, 128, 8), (1, 128, 256, 8), (1, 256, 128, 8),
-                                          (2, 128, 128, 16)])
+                                          (2, 128, 128, 16), (1, 256, 256, 8), (1, 128, 128, 32)])
 def test_conv3d_fwd_bwd_vs_fp64(ops, b, cin, cout, r):
     g = torch.Generator(device="cuda").manual_seed(b * 1000 + cin + r)
     x = torch.randn(b, cin, r, r, r, device="cuda", generator=g)
@@ -41,6 +41,12 @@ def test_conv3d_fwd_bwd_vs_fp64(ops, b, cin, cout, r):
     if cin % 128 == 0:
         dw64 = torch.nn.grad.conv3d_weight(x64, w64.shape, g64, padding=1)
         assert _rel(ops.conv3d_backward_weight(x, gy), dw64) < TOL
+        if cout % 128 == 0:  # split-operand path (what VoxelConv3d's autograd runs)
+            xs, gys = ops.conv3d_split(x), ops.conv3d_split(gy)
+            assert _rel(ops.conv3d_wgrad_split(xs, gys, b, cin, cout, r), dw64) < TOL
+            img = ops.conv3d_prep_weight(w, False)
+            y = ops.conv3d_igemm_split(xs, img, bias, b, cin, cout, r, "t")
+            assert _rel(y, y64) < TOL
 
 
 def test_conv3d_padding_is_zero(ops):

@@ -53,7 +53,12 @@ for b, c, r in [(8, 128, 32), (8, 256, 16), (8, 256, 8)]:
     t_x3 = timeit(lambda: ops.conv3d_forward(x, w, bias))
     t_bd = timeit(lambda: ops.conv3d_backward_data(gy, w))
     t_32 = timeit(lambda: torch.nn.functional.conv3d(x, w, bias, padding=1))
-    t_wg = timeit(lambda: ops.conv3d_backward_weight(x, gy))
+    t_wg_old = timeit(lambda: ops.conv3d_backward_weight(x, gy))
+    xs_, gys_ = ops.conv3d_split(x), ops.conv3d_split(gy)
+    t_wg = timeit(lambda: ops.conv3d_wgrad_split(xs_, gys_, b, c, c, r))
+    t_split = timeit(lambda: ops.conv3d_split(gy))
+    print(f"   split {t_split:.3f} ms; wgrad (split operands) {t_wg:.3f} ms vs on-the-fly "
+          f"{t_wg_old:.3f} ms")
     t_wg32 = timeit(lambda: torch.nn.grad.conv3d_weight(x, w.shape, gy, padding=1))
     t_bd32 = timeit(lambda: torch.nn.grad.conv3d_input(x.shape, w, gy, padding=1))
     print(f"C{c}R{r}: fwd x3 {t_x3:.3f} ms ({flop / t_x3 / 1e9:.0f} TF)  bwd-data x3 {t_bd:.3f} ms"
