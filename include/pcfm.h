@@ -37,7 +37,7 @@ extern "C" {
 
 /* ABI version: bumped on any signature change (4: voxel and pointwise convolution;
  * 5: per-point head kernels; 6: conv3d_igemm workspace,
- * split-operand convolution entry points). */
+ * split-operand convolution entry points; fused BatchNorm + activation). */
 int pcfm_abi_version(void);
 /* Thread-local text of the last non-zero return code. */
 const char* pcfm_last_error(void);
@@ -312,6 +312,32 @@ int pcfm_head_film_bwd(const float* dh_next, const void* da16, const float* u, c
 int pcfm_head_silu_bwd(const void* da16, const float* uprev, const void* gprev, int b, int n,
                        int w, float* dh, void* dh16, float* dbias, void* ws, size_t ws_bytes,
                        void* stream);
+
+/* ------------------------------------------------------------------------
+ * BatchNorm (batch statistics, training mode) fused with the activation
+ * after it: SharedMLP's BN1d + ReLU (shared_mlp.py:15-27, slope = 0) and
+ * PVConv's BN3d + LeakyReLU(0.1) (pvconv.py:20-30, slope = 0.1), over
+ * x f32 [b][c][s] (s % 4 == 0).  torch.nn.functional.batch_norm semantics.
+ * ---------------------------------------------------------------------- */
+
+size_t pcfm_bn_workspace_bytes(int b, int c, int s);
+
+/* y = act((x - mean) * invstd * gamma + beta), act(v) = v > 0 ? v : slope * v,
+ * mean / invstd = batch statistics over (b, s) per channel (biased variance,
+ * invstd = 1/sqrt(var + eps)), written to mean / invstd [c].  If running_mean
+ * and running_var are non-NULL they are updated in place:
+ * r = (1 - momentum) * r + momentum * stat (unbiased variance for running_var). */
+int pcfm_bn_act_fwd(const float* x, const float* gamma, const float* beta, int b, int c, int s,
+                    float eps, float slope, float momentum, float* running_mean,
+                    float* running_var, float* y, float* mean, float* invstd, void* ws,
+                    size_t ws_bytes, void* stream);
+
+/* Backward of pcfm_bn_act_fwd given dz = dL/dy: dx [b][c][s] and
+ * dgamma / dbeta [c] (all fully written). */
+int pcfm_bn_act_bwd(const float* dz, const float* x, const float* gamma, const float* beta,
+                    const float* mean, const float* invstd, int b, int c, int s, float slope,
+                    float* dx, float* dgamma, float* dbeta, void* ws, size_t ws_bytes,
+                    void* stream);
 
 #ifdef __cplusplus
 }

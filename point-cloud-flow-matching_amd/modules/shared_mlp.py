@@ -13,6 +13,8 @@ under autocast it stays a batched GEMM so torch's autocast casting applies.
 import torch
 import torch.nn as nn
 
+from modules.norm_act import bn_act
+
 __all__ = ["SharedMLP", "PointwiseConv1d"]
 
 
@@ -80,8 +82,15 @@ class SharedMLP(nn.Module):
             prev = w
         self.layers = nn.Sequential(*stack)
 
+    def _run(self, x):
+        # (conv, BN, ReLU) triples; BN + ReLU fused on the GPU (modules/norm_act.py)
+        layers = self.layers
+        for i in range(0, len(layers), 3):
+            x = bn_act(layers[i](x), layers[i + 1], 0.0)
+        return x
+
     def forward(self, inputs):
         # (features, coords, ...) tuples pass the trailing items through untouched
         if isinstance(inputs, (list, tuple)):
-            return (self.layers(inputs[0]), *inputs[1:])
-        return self.layers(inputs)
+            return (self._run(inputs[0]), *inputs[1:])
+        return self._run(inputs)

@@ -72,6 +72,10 @@ SIGNATURES = {
     "pcfm_head_film_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P, _P,
                                 _P, _P, _P, _P, _P, _P, _Z, _P]),
     "pcfm_head_silu_bwd": (_I, [_P, _P, _P, _I, _I, _I, _P, _P, _P, _P, _Z, _P]),
+    "pcfm_bn_workspace_bytes": (_Z, [_I, _I, _I]),
+    "pcfm_bn_act_fwd": (_I, [_P, _P, _P, _I, _I, _I, _F, _F, _F, _P, _P, _P, _P, _P, _P, _Z,
+                             _P]),
+    "pcfm_bn_act_bwd": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _F, _P, _P, _P, _P, _Z, _P]),
 }
 
 ABI_VERSION = 6

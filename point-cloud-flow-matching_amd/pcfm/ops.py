@@ -613,3 +613,37 @@ def head_silu_bwd(da16, uprev, gprev, n: int):
     _lib.call("pcfm_head_silu_bwd", _p(da16), _p(uprev), _p(gprev), b, n, w, _p(dh), _p(dh16),
               _p(dbias), _p(ws), ws.numel(), _stream(da16))
     return dh, dh16, dbias
+
+
+# --------------------------------------------------------------------------
+# BatchNorm (batch statistics) + ReLU / LeakyReLU (include/pcfm.h)
+# --------------------------------------------------------------------------
+def bn_act_forward(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, eps: float,
+                   slope: float, momentum: float, running_mean, running_var):
+    """x (B, C, ...) fp32 contiguous -> (y, mean, invstd); running stats updated in place."""
+    _check(x, "input", "f")
+    b, c = x.shape[0], x.shape[1]
+    s = x.numel() // max(1, b * c)
+    y = torch.empty_like(x)
+    stats = torch.empty((2, c), dtype=torch.float32, device=x.device)
+    ws = _workspace(_lib.query("pcfm_bn_workspace_bytes", b, c, s), x)
+    with _timed("bn_act_fwd", 4 * 3 * x.numel(), x):
+        _lib.call("pcfm_bn_act_fwd", _ptr(x), _ptr(weight), _ptr(bias), b, c, s, float(eps),
+                  float(slope), float(momentum), _p(running_mean), _p(running_var), _ptr(y),
+                  _ptr(stats[0]), _ptr(stats[1]), _ptr(ws), ws.numel(), _stream(x))
+    return y, stats[0], stats[1]
+
+
+def bn_act_backward(dz: torch.Tensor, x: torch.Tensor, weight, bias, mean, invstd, slope: float):
+    """-> (dx, dgamma, dbeta)"""
+    dz = dz.contiguous()
+    b, c = x.shape[0], x.shape[1]
+    s = x.numel() // max(1, b * c)
+    dx = torch.empty_like(x)
+    dgb = torch.empty((2, c), dtype=torch.float32, device=x.device)
+    ws = _workspace(_lib.query("pcfm_bn_workspace_bytes", b, c, s), x)
+    with _timed("bn_act_bwd", 4 * 5 * x.numel(), x):
+        _lib.call("pcfm_bn_act_bwd", _ptr(dz), _ptr(x), _ptr(weight), _ptr(bias), _ptr(mean),
+                  _ptr(invstd), b, c, s, float(slope), _ptr(dx), _ptr(dgb[0]), _ptr(dgb[1]),
+                  _ptr(ws), ws.numel(), _stream(x))
+    return dx, dgb[0], dgb[1]

@@ -1,0 +1,66 @@
+"""Fused BatchNorm + ReLU / LeakyReLU (csrc/norm.hip) against torch's
+nn.BatchNorm + activation in training mode: output, input / gamma / beta
+gradients and the running-stat update.  fp32 with a different summation
+order than MIOpen: rtol 1e-4 (outputs and grads are O(1))."""
+import copy
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ops():
+    from pcfm import _lib, ops
+    _lib.load()
+    return ops
+
+
+@pytest.mark.parametrize("shape,slope,eps", [((8, 256, 20000), 0.0, 1e-5),
+                                             ((2, 128, 16, 16, 16), 0.1, 1e-4),
+                                             ((3, 64, 100), 0.0, 1e-5),
+                                             ((1, 32, 8, 8, 8), 0.1, 1e-4)])
+def test_bn_act_matches_torch(ops, shape, slope, eps):
+    from modules.norm_act import bn_act, _fusable
+    torch.manual_seed(0)
+    c = shape[1]
+    kind = torch.nn.BatchNorm1d if len(shape) == 3 else torch.nn.BatchNorm3d
+    ref = kind(c, eps=eps).cuda().train()
+    with torch.no_grad():
+        ref.weight.uniform_(0.5, 1.5)
+        ref.bias.uniform_(-0.5, 0.5)
+        ref.running_mean.uniform_(-1, 1)
+    mod = copy.deepcopy(ref)
+    x = (torch.randn(*shape, device="cuda") * 2.0 + 3.0)  # offset mean: cancellation check
+    assert _fusable(x, mod)
+    xa, xb = x.clone().requires_grad_(True), x.clone().requires_grad_(True)
+    act = torch.nn.ReLU() if slope == 0 else torch.nn.LeakyReLU(slope)
+    ya = act(ref(xa))
+    yb = bn_act(xb, mod, slope)
+    torch.testing.assert_close(yb, ya, rtol=1e-4, atol=1e-4)
+    gy = torch.randn_like(ya)
+    ya.backward(gy)
+    yb.backward(gy)
+    # elements whose BN output lies within rounding of the activation's kink can
+    # take the other branch (either side is a valid subgradient): only those may
+    # differ, and each moves the gamma / beta sums by at most |dy| * O(1)
+    bad = ~torch.isclose(xb.grad, xa.grad, rtol=1e-4, atol=1e-4)
+    pre = torch.nn.functional.batch_norm(x, None, None, ref.weight.detach(), ref.bias.detach(),
+                                         training=True, eps=eps)
+    assert int(bad.sum()) <= max(2, x.numel() // 1000000)
+    assert bool((pre[bad].abs() < 1e-4).all())
+    kink = 1e-3 + 4.0 * float(bad.sum()) * float(gy.abs().max())
+    torch.testing.assert_close(mod.weight.grad, ref.weight.grad, rtol=1e-4, atol=kink)
+    torch.testing.assert_close(mod.bias.grad, ref.bias.grad, rtol=1e-4, atol=kink)
+    torch.testing.assert_close(mod.running_mean, ref.running_mean, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(mod.running_var, ref.running_var, rtol=1e-5, atol=1e-5)
+    assert int(mod.num_batches_tracked) == int(ref.num_batches_tracked) == 1
+
+
+def test_bn_act_falls_back_in_eval(ops):
+    from modules.norm_act import bn_act, _fusable
+    bn = torch.nn.BatchNorm1d(16).cuda().eval()
+    x = torch.randn(2, 16, 40, device="cuda")
+    assert not _fusable(x, bn)
+    torch.testing.assert_close(bn_act(x, bn, 0.0), torch.relu(bn(x)))
