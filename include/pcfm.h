@@ -273,6 +273,14 @@ size_t pcfm_rows_wgrad_workspace_bytes(long long rows, int m, int n);
 int pcfm_rows_wgrad_bf16(const void* a, int lda, const void* b, int ldb, long long rows, int m,
                          int n, void* out, void* ws, size_t ws_bytes, void* stream);
 
+size_t pcfm_rows_max_workspace_bytes(int b, int n, int c);
+
+/* ShapeEncoder's global pooling h.max(dim=1) (models.py:156-187) over
+ * h bf16 [b][n][c] (c even): values bf16 [b][c] and indices i32 [b][c]
+ * (argmax over n, lowest index on ties; NaN propagates). */
+int pcfm_rows_max_bf16(const void* h, int b, int n, int c, void* values, int* indices, void* ws,
+                       size_t ws_bytes, void* stream);
+
 /* Trunk rows of VelocityNetWithContext / VelocityNet (models.py:62-79 FiLMBlock,
  * :107-116 residual loop), W = 256 or 512 channels, rows = b*n (batch-major).
  * bf16 tensors are passed as void* (raw 16-bit bf16 bits).
@@ -338,6 +346,22 @@ int pcfm_bn_act_bwd(const float* dz, const float* x, const float* gamma, const f
                     const float* mean, const float* invstd, int b, int c, int s, float slope,
                     float* dx, float* dgamma, float* dbeta, void* ws, size_t ws_bytes,
                     void* stream);
+
+/* GroupNorm + FiLM + residual of the hybrid backbone's PV blocks
+ * (models.py:322-346 _FiLM1d(norm="group"), :349-368 _PVBlock):
+ *   out = x + (GroupNorm(x; groups, w, bias, eps) * (1 + gamma[b]) + beta[b])
+ * x f32 [b][c][n] (n % 4 == 0, c <= 1024), gamma / beta f32 [b][c];
+ * mean / rstd f32 [b][groups] saved for the backward. */
+size_t pcfm_gn_film_workspace_bytes(int b, int c, int n, int groups);
+int pcfm_gn_film_res_fwd(const float* x, const float* w, const float* bias, const float* gamma,
+                         const float* beta, int b, int c, int n, int groups, float eps,
+                         float* out, float* mean, float* rstd, void* ws, size_t ws_bytes,
+                         void* stream);
+/* dx [b][c][n], dw / dbias [c], dgamma / dbeta [b][c] from dout = dL/dout. */
+int pcfm_gn_film_res_bwd(const float* dout, const float* x, const float* w, const float* bias,
+                         const float* gamma, const float* mean, const float* rstd, int b, int c,
+                         int n, int groups, float* dx, float* dw, float* dbias, float* dgamma,
+                         float* dbeta, void* ws, size_t ws_bytes, void* stream);
 
 #ifdef __cplusplus
 }

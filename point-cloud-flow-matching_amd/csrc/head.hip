@@ -257,3 +257,100 @@ extern "C" int pcfm_rows_wgrad_bf16(const void* a, int lda, const void* b, int l
                      0, st, (const float*)ws, total, S, (uint16_t*)out);
   return check_launch("rows_wgrad_bf16");
 }
+
+// ---------------------------------------------------------------------------
+// Max over the point axis of a (B, N, C) bf16 tensor with its argmax -- the
+// ShapeEncoder's global pooling h.max(dim=1) (reference models.py:156-187).
+// Lowest index on ties.  Stage 1: grid (P, B), 4 waves stride the part's rows,
+// lanes hold channel pairs (128 channels per pass); stage 2: per (b, c) over the P parts in order.
+// ---------------------------------------------------------------------------
+namespace pcfm {
+namespace {
+
+__device__ __forceinline__ bool max_better(float v, int i, float m, int mi) {
+  // NaN propagates as the maximum (torch.max); ties -> lower index
+  if (v != v) return m == m || i < mi;
+  return v > m || (v == m && i < mi);
+}
+
+__global__ void __launch_bounds__(256)
+    rows_max_part_kernel(const uint16_t* __restrict__ h, int N, int C, float* __restrict__ pv,
+                         int* __restrict__ pi) {
+  __shared__ float sv[4][128];
+  __shared__ int si[4][128];
+  const int b = blockIdx.y, p = blockIdx.x, P = gridDim.x;
+  const int chunk = (N + P - 1) / P, n0 = min(N, p * chunk), n1 = min(N, n0 + chunk);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int cb = 0; cb < C; cb += 128) {
+    const int c = cb + 2 * lane;  // channel pair (c, c + 1); C is even
+    float m0 = -INFINITY, m1 = -INFINITY;
+    int i0 = N, i1 = N;
+    if (c < C) {
+      for (int r = n0 + wave; r < n1; r += 4) {
+        const uint32_t u = *reinterpret_cast<const uint32_t*>(h + ((size_t)b * N + r) * C + c);
+        const float v0 = __uint_as_float(u << 16), v1 = __uint_as_float(u & 0xFFFF0000u);
+        if (max_better(v0, r, m0, i0)) { m0 = v0; i0 = r; }
+        if (max_better(v1, r, m1, i1)) { m1 = v1; i1 = r; }
+      }
+    }
+    sv[wave][2 * lane] = m0;
+    sv[wave][2 * lane + 1] = m1;
+    si[wave][2 * lane] = i0;
+    si[wave][2 * lane + 1] = i1;
+    __syncthreads();
+    if (threadIdx.x < 128) {
+      const int k = threadIdx.x, ck = cb + k;
+      float m = sv[0][k];
+      int mi = si[0][k];
+      for (int w = 1; w < 4; ++w)
+        if (max_better(sv[w][k], si[w][k], m, mi)) { m = sv[w][k]; mi = si[w][k]; }
+      if (ck < C) {
+        pv[((size_t)b * P + p) * C + ck] = m;
+        pi[((size_t)b * P + p) * C + ck] = mi;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+__global__ void __launch_bounds__(256)
+    rows_max_final_kernel(const float* __restrict__ pv, const int* __restrict__ pi, int P, int C,
+                          uint16_t* __restrict__ val, int* __restrict__ idx) {
+  const int b = blockIdx.y, c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  float m = -INFINITY;
+  int mi = 0x7FFFFFFF;
+  for (int p = 0; p < P; ++p) {
+    const float v = pv[((size_t)b * P + p) * C + c];
+    const int i = pi[((size_t)b * P + p) * C + c];
+    if (max_better(v, i, m, mi)) { m = v; mi = i; }
+  }
+  val[(size_t)b * C + c] = (uint16_t)(__float_as_uint(m) >> 16);
+  idx[(size_t)b * C + c] = mi;
+}
+
+constexpr int kMaxParts = 32;
+
+}  // namespace
+}  // namespace pcfm
+
+extern "C" size_t pcfm_rows_max_workspace_bytes(int b, int n, int c) {
+  if (b <= 0 || n <= 0 || c <= 0 || c % 2 != 0) return 0;
+  return (size_t)b * kMaxParts * c * (sizeof(float) + sizeof(int));
+}
+
+extern "C" int pcfm_rows_max_bf16(const void* h, int b, int n, int c, void* values, int* indices,
+                                  void* ws, size_t ws_bytes, void* stream) {
+  PCFM_CHECK_ARG(pcfm_rows_max_workspace_bytes(b, n, c) > 0,
+                 "rows_max_bf16: bad shape b=%d n=%d c=%d (c even, n > 0)", b, n, c);
+  PCFM_CHECK_ARG(ws_bytes >= pcfm_rows_max_workspace_bytes(b, n, c),
+                 "rows_max_bf16: workspace too small");
+  hipStream_t st = (hipStream_t)stream;
+  float* pv = (float*)ws;
+  int* pi = (int*)(pv + (size_t)b * kMaxParts * c);
+  hipLaunchKernelGGL(rows_max_part_kernel, dim3(kMaxParts, b), dim3(256), 0, st,
+                     (const uint16_t*)h, n, c, pv, pi);
+  hipLaunchKernelGGL(rows_max_final_kernel, dim3(ceil_div(c, 256), b), dim3(256), 0, st,
+                     (const float*)pv, (const int*)pi, kMaxParts, c, (uint16_t*)values, indices);
+  return check_launch("rows_max_bf16");
+}

@@ -200,6 +200,203 @@ __global__ void __launch_bounds__(256)
   reinterpret_cast<float4*>(dx)[i] = make_float4(o[0], o[1], o[2], o[3]);
 }
 
+// ---------------------------------------------------------------------------
+// GroupNorm + FiLM + residual of the hybrid backbone's PV blocks
+// (reference models.py:322-346 _FiLM1d with GroupNorm, :349-368 _PVBlock):
+//   out = x + (GN(x) * (1 + gamma[b]) + beta[b])
+//   GN(x)[b, c, n] = (x - mean[b, g]) * rstd[b, g] * w[c] + bias[c],  g = c / (C / G)
+// evaluated as torch does: y = x * a + s with a = rstd * w, s = bias - mean * a,
+// then y * (1 + gamma) + beta, then + x.
+// Backward with A2[b, c] = sum_n dout, A3[b, c] = sum_n dout * xhat:
+//   d beta = A2, d gamma = w A3 + bias A2, d w = sum_b (1+gamma) A3,
+//   d bias = sum_b (1+gamma) A2, and per group
+//   dx = dout + rstd (dout (1+gamma) w - mean_g(dy w) - xhat mean_g(dy w xhat)).
+// ---------------------------------------------------------------------------
+constexpr int kGnParts = 4;  // blocks per (b, group) row set / per (b, c) row
+
+// fwd stats: grid (G * kGnParts, B); part[(b*G + g)*P + p] = (sum (x-K), sum (x-K)^2)
+__global__ void __launch_bounds__(256)
+    gn_stats_kernel(const float* __restrict__ x, int C, int N, int G, float* __restrict__ part) {
+  __shared__ float sh[8];
+  const int b = blockIdx.y, g = blockIdx.x / kGnParts, p = blockIdx.x % kGnParts;
+  const int cpg = C / G, N4 = N / 4;
+  const float* base = x + ((size_t)b * C + (size_t)g * cpg) * N;  // cpg rows of N, contiguous
+  const float K = base[0];
+  const int tot = cpg * N4, chunk = (tot + kGnParts - 1) / kGnParts;
+  const int f0 = min(tot, p * chunk), f1 = min(tot, f0 + chunk);
+  const float4* x4 = reinterpret_cast<const float4*>(base);
+  float s = 0.0f, q = 0.0f;
+  for (int f = f0 + threadIdx.x; f < f1; f += 256) {
+    const float4 v = x4[f];
+    const float d0 = v.x - K, d1 = v.y - K, d2 = v.z - K, d3 = v.w - K;
+    s += (d0 + d1) + (d2 + d3);
+    q += (d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3);
+  }
+  block_sum2(s, q, sh);
+  if (threadIdx.x == 0) {
+    part[(((size_t)b * G + g) * kGnParts + p) * 2] = s;
+    part[(((size_t)b * G + g) * kGnParts + p) * 2 + 1] = q;
+  }
+}
+
+// one thread per (b, c): group stats -> a = rstd*w, s = bias - mean*a, g1 = 1 + gamma
+__global__ void __launch_bounds__(256)
+    gn_finalize_kernel(const float* __restrict__ part, const float* __restrict__ x,
+                       const float* __restrict__ w, const float* __restrict__ bias,
+                       const float* __restrict__ gamma, int B, int C, int N, int G, float eps,
+                       float* __restrict__ mean_o, float* __restrict__ rstd_o,
+                       float* __restrict__ coef) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= B * C) return;
+  const int b = i / C, c = i - b * C, cpg = C / G, g = c / cpg;
+  float s = 0.0f, q = 0.0f;
+  for (int p = 0; p < kGnParts; ++p) {
+    s += part[(((size_t)b * G + g) * kGnParts + p) * 2];
+    q += part[(((size_t)b * G + g) * kGnParts + p) * 2 + 1];
+  }
+  const double n = (double)cpg * N;
+  const float K = x[((size_t)b * C + (size_t)g * cpg) * N];
+  const float md = (float)(s / n);
+  const float var = fmaxf((float)(q / n) - md * md, 0.0f);
+  const float mean = K + md, rstd = rsqrtf(var + eps);
+  if (c % cpg == 0) {
+    mean_o[b * G + g] = mean;
+    rstd_o[b * G + g] = rstd;
+  }
+  const float a = rstd * w[c];
+  coef[3 * (size_t)i] = a;
+  coef[3 * (size_t)i + 1] = bias[c] - mean * a;
+  coef[3 * (size_t)i + 2] = 1.0f + gamma[i];
+}
+
+// out = x + ((x * a + s) * g1 + beta); grid (ceil(N4 / 256), B * C)
+__global__ void __launch_bounds__(256)
+    gn_film_apply_kernel(const float* __restrict__ x, const float* __restrict__ coef,
+                         const float* __restrict__ beta, int N4, float* __restrict__ out) {
+  const int n4 = blockIdx.x * 256 + threadIdx.x;
+  if (n4 >= N4) return;
+  const int row = blockIdx.y;
+  const float a = coef[3 * (size_t)row], s = coef[3 * (size_t)row + 1];
+  const float g1 = coef[3 * (size_t)row + 2], bt = beta[row];
+  const size_t i = (size_t)row * N4 + n4;
+  const float4 v = reinterpret_cast<const float4*>(x)[i];
+  float4 o;
+  o.x = v.x + (__builtin_fmaf(v.x, a, s) * g1 + bt);
+  o.y = v.y + (__builtin_fmaf(v.y, a, s) * g1 + bt);
+  o.z = v.z + (__builtin_fmaf(v.z, a, s) * g1 + bt);
+  o.w = v.w + (__builtin_fmaf(v.w, a, s) * g1 + bt);
+  reinterpret_cast<float4*>(out)[i] = o;
+}
+
+// bwd row sums: grid (kGnParts, B * C); part[row * P + p] = (sum dout, sum dout * xhat)
+__global__ void __launch_bounds__(256)
+    gn_bwd_stats_kernel(const float* __restrict__ dout, const float* __restrict__ x,
+                        const float* __restrict__ mean, const float* __restrict__ rstd, int C,
+                        int N, int G, float* __restrict__ part) {
+  __shared__ float sh[8];
+  const int row = blockIdx.y, p = blockIdx.x;
+  const int b = row / C, c = row - b * C, g = c / (C / G);
+  const float m = mean[b * G + g], rs = rstd[b * G + g];
+  const int N4 = N / 4, chunk = (N4 + kGnParts - 1) / kGnParts;
+  const int f0 = min(N4, p * chunk), f1 = min(N4, f0 + chunk);
+  const float4* x4 = reinterpret_cast<const float4*>(x) + (size_t)row * N4;
+  const float4* d4 = reinterpret_cast<const float4*>(dout) + (size_t)row * N4;
+  float a2 = 0.0f, a3 = 0.0f;
+  for (int f = f0 + threadIdx.x; f < f1; f += 256) {
+    const float4 v = x4[f], d = d4[f];
+    a2 += (d.x + d.y) + (d.z + d.w);
+    a3 += (d.x * ((v.x - m) * rs) + d.y * ((v.y - m) * rs)) +
+          (d.z * ((v.z - m) * rs) + d.w * ((v.w - m) * rs));
+  }
+  block_sum2(a2, a3, sh);
+  if (threadIdx.x == 0) {
+    part[((size_t)row * kGnParts + p) * 2] = a2;
+    part[((size_t)row * kGnParts + p) * 2 + 1] = a3;
+  }
+}
+
+// one block, C threads (C <= 1024): per batch element the group coefficients
+// k1 = mean_g(dy w), k2 = mean_g(dy w xhat) -> kc[b][c] = (rstd*g1*w, rstd*k1, rstd*k2)
+// and d gamma / d beta [b][c]; summed over b: d w, d bias [c].
+__global__ void __launch_bounds__(1024)
+    gn_bwd_finalize_kernel(const float* __restrict__ part, const float* __restrict__ w,
+                           const float* __restrict__ bias, const float* __restrict__ gamma,
+                           const float* __restrict__ rstd, int B, int C, int N, int G,
+                           float* __restrict__ kc, float* __restrict__ dgamma,
+                           float* __restrict__ dbeta, float* __restrict__ dw,
+                           float* __restrict__ dbias) {
+  __shared__ float s1[1024], s2[1024];
+  const int c = threadIdx.x, cpg = C / G;
+  float dws = 0.0f, dbs = 0.0f;
+  for (int b = 0; b < B; ++b) {
+    float a2 = 0.0f, a3 = 0.0f, g1 = 0.0f, t1 = 0.0f, t2 = 0.0f;
+    if (c < C) {
+      const size_t row = (size_t)b * C + c;
+      for (int p = 0; p < kGnParts; ++p) {
+        a2 += part[(row * kGnParts + p) * 2];
+        a3 += part[(row * kGnParts + p) * 2 + 1];
+      }
+      g1 = 1.0f + gamma[row];
+      dbeta[row] = a2;
+      dgamma[row] = w[c] * a3 + bias[c] * a2;
+      dws += g1 * a3;
+      dbs += g1 * a2;
+      t1 = w[c] * g1 * a2;  // sum_n dy w over this channel
+      t2 = w[c] * g1 * a3;  // sum_n dy w xhat
+    }
+    s1[c] = t1;
+    s2[c] = t2;
+    __syncthreads();
+    if (c < C) {
+      const int g0 = (c / cpg) * cpg;
+      float k1 = 0.0f, k2 = 0.0f;
+      for (int j = 0; j < cpg; ++j) {
+        k1 += s1[g0 + j];
+        k2 += s2[g0 + j];
+      }
+      const float inv_d = (float)(1.0 / ((double)cpg * N));
+      const float rs = rstd[b * G + c / cpg];
+      const size_t row = (size_t)b * C + c;
+      kc[3 * row] = rs * g1 * w[c];
+      kc[3 * row + 1] = rs * k1 * inv_d;
+      kc[3 * row + 2] = rs * k2 * inv_d;
+    }
+    __syncthreads();
+  }
+  if (c < C) {
+    dw[c] = dws;
+    dbias[c] = dbs;
+  }
+}
+
+// dx = dout + dout * kc0 - kc1 - xhat * kc2; grid (ceil(N4 / 256), B * C)
+__global__ void __launch_bounds__(256)
+    gn_film_bwd_apply_kernel(const float* __restrict__ dout, const float* __restrict__ x,
+                             const float* __restrict__ mean, const float* __restrict__ rstd,
+                             const float* __restrict__ kc, int C, int G, int N4,
+                             float* __restrict__ dx) {
+  const int n4 = blockIdx.x * 256 + threadIdx.x;
+  if (n4 >= N4) return;
+  const int row = blockIdx.y;
+  const int b = row / C, g = (row - b * C) / (C / G);
+  const float m = mean[b * G + g], rs = rstd[b * G + g];
+  const float k0 = kc[3 * (size_t)row], k1 = kc[3 * (size_t)row + 1], k2 = kc[3 * (size_t)row + 2];
+  const size_t i = (size_t)row * N4 + n4;
+  const float4 v = reinterpret_cast<const float4*>(x)[i];
+  const float4 d = reinterpret_cast<const float4*>(dout)[i];
+  float4 o;
+  o.x = d.x + ((d.x * k0 - k1) - ((v.x - m) * rs) * k2);
+  o.y = d.y + ((d.y * k0 - k1) - ((v.y - m) * rs) * k2);
+  o.z = d.z + ((d.z * k0 - k1) - ((v.z - m) * rs) * k2);
+  o.w = d.w + ((d.w * k0 - k1) - ((v.w - m) * rs) * k2);
+  reinterpret_cast<float4*>(dx)[i] = o;
+}
+
+bool gn_ok(int b, int c, int n, int g) {
+  return b > 0 && c > 0 && c <= 1024 && g > 0 && c % g == 0 && n > 0 && n % 4 == 0 &&
+         (long long)b * c < 65536 && (long long)(c / g) * n / 4 < (1LL << 31);
+}
+
 bool bn_ok(int b, int c, int s) {
   return b > 0 && c > 0 && s > 0 && s % 4 == 0 && (long long)b * c < 65536 &&
          (long long)b * c * s < (1LL << 40);
@@ -252,4 +449,53 @@ extern "C" int pcfm_bn_act_bwd(const float* dz, const float* x, const float* gam
                      x, mean, invstd, gamma, beta, (const float*)dgamma, (const float*)dbeta, c,
                      s / 4, (float)(1.0 / ((double)b * s)), slope, dx);
   return check_launch("bn_act_bwd");
+}
+
+extern "C" size_t pcfm_gn_film_workspace_bytes(int b, int c, int n, int groups) {
+  if (!gn_ok(b, c, n, groups)) return 0;
+  const size_t fwd = ((size_t)b * groups * kGnParts * 2 + 3 * (size_t)b * c) * sizeof(float);
+  const size_t bwd = ((size_t)b * c * kGnParts * 2 + 3 * (size_t)b * c) * sizeof(float);
+  return fwd > bwd ? fwd : bwd;
+}
+
+extern "C" int pcfm_gn_film_res_fwd(const float* x, const float* w, const float* bias,
+                                    const float* gamma, const float* beta, int b, int c, int n,
+                                    int groups, float eps, float* out, float* mean, float* rstd,
+                                    void* ws, size_t ws_bytes, void* stream) {
+  PCFM_CHECK_ARG(gn_ok(b, c, n, groups), "gn_film_res_fwd: bad shape b=%d c=%d n=%d groups=%d",
+                 b, c, n, groups);
+  PCFM_CHECK_ARG(ws_bytes >= pcfm_gn_film_workspace_bytes(b, c, n, groups),
+                 "gn_film_res_fwd: workspace too small");
+  hipStream_t st = (hipStream_t)stream;
+  float* part = (float*)ws;
+  float* coef = part + (size_t)b * groups * kGnParts * 2;
+  hipLaunchKernelGGL(gn_stats_kernel, dim3(groups * kGnParts, b), dim3(256), 0, st, x, c, n,
+                     groups, part);
+  hipLaunchKernelGGL(gn_finalize_kernel, dim3(ceil_div((long long)b * c, 256)), dim3(256), 0, st,
+                     (const float*)part, x, w, bias, gamma, b, c, n, groups, eps, mean, rstd,
+                     coef);
+  hipLaunchKernelGGL(gn_film_apply_kernel, dim3(ceil_div(n / 4, 256), b * c), dim3(256), 0, st,
+                     x, (const float*)coef, beta, n / 4, out);
+  return check_launch("gn_film_res_fwd");
+}
+
+extern "C" int pcfm_gn_film_res_bwd(const float* dout, const float* x, const float* w,
+                                    const float* bias, const float* gamma, const float* mean,
+                                    const float* rstd, int b, int c, int n, int groups, float* dx,
+                                    float* dw, float* dbias, float* dgamma, float* dbeta,
+                                    void* ws, size_t ws_bytes, void* stream) {
+  PCFM_CHECK_ARG(gn_ok(b, c, n, groups), "gn_film_res_bwd: bad shape b=%d c=%d n=%d groups=%d",
+                 b, c, n, groups);
+  PCFM_CHECK_ARG(ws_bytes >= pcfm_gn_film_workspace_bytes(b, c, n, groups),
+                 "gn_film_res_bwd: workspace too small");
+  hipStream_t st = (hipStream_t)stream;
+  float* part = (float*)ws;
+  float* kc = part + (size_t)b * c * kGnParts * 2;
+  hipLaunchKernelGGL(gn_bwd_stats_kernel, dim3(kGnParts, b * c), dim3(256), 0, st, dout, x, mean,
+                     rstd, c, n, groups, part);
+  hipLaunchKernelGGL(gn_bwd_finalize_kernel, dim3(1), dim3(1024), 0, st, (const float*)part, w,
+                     bias, gamma, rstd, b, c, n, groups, kc, dgamma, dbeta, dw, dbias);
+  hipLaunchKernelGGL(gn_film_bwd_apply_kernel, dim3(ceil_div(n / 4, 256), b * c), dim3(256), 0,
+                     st, dout, x, mean, rstd, (const float*)kc, c, groups, n / 4, dx);
+  return check_launch("gn_film_res_bwd");
 }

@@ -12,7 +12,7 @@ and the activation run as in the reference.
 import torch
 import torch.nn.functional as F
 
-__all__ = ["bn_act"]
+__all__ = ["bn_act", "gn_film_residual"]
 
 
 class _BNAct(torch.autograd.Function):
@@ -50,3 +50,36 @@ def bn_act(x: torch.Tensor, bn, slope: float) -> torch.Tensor:
                             float(bn.eps), float(bn.momentum), float(slope))
     y = bn(x)
     return F.relu(y, inplace=True) if slope == 0 else F.leaky_relu(y, slope, inplace=True)
+
+
+class _GNFiLMRes(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, gamma, beta, groups, eps):
+        from pcfm import ops
+        out, mean, rstd = ops.gn_film_res_forward(x, weight, bias, gamma, beta, groups, eps)
+        ctx.save_for_backward(x, weight, bias, gamma, mean, rstd)
+        ctx.groups = groups
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        from pcfm import ops
+        x, weight, bias, gamma, mean, rstd = ctx.saved_tensors
+        dx, dw, db, dg, dbt = ops.gn_film_res_backward(dout, x, weight, bias, gamma, mean, rstd,
+                                                       ctx.groups)
+        return dx, dw, db, dg, dbt, None, None
+
+
+def gn_film_residual(x: torch.Tensor, norm, gamma: torch.Tensor, beta: torch.Tensor):
+    """x + (norm(x) * (1 + gamma[:, :, None]) + beta[:, :, None]) for a GroupNorm
+    `norm` (reference models.py:322-368); fused on a HIP device in fp32."""
+    fused = (x.is_cuda and x.dtype == torch.float32 and x.dim() == 3
+             and isinstance(norm, torch.nn.GroupNorm) and norm.affine
+             and x.shape[2] % 4 == 0 and x.shape[1] <= 1024 and x.shape[0] * x.shape[1] < 65536
+             and gamma.dtype == torch.float32 and beta.dtype == torch.float32
+             and not torch.is_autocast_enabled("cuda"))
+    if fused:
+        return _GNFiLMRes.apply(x.contiguous(), norm.weight, norm.bias, gamma, beta,
+                                int(norm.num_groups), float(norm.eps))
+    y = norm(x)
+    return x + (y * (1.0 + gamma[:, :, None]) + beta[:, :, None])

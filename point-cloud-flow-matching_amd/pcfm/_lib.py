@@ -65,6 +65,8 @@ SIGNATURES = {
     "pcfm_pointwise_wgrad": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, _Z, _P]),
     "pcfm_rows_wgrad_workspace_bytes": (_Z, [_L, _I, _I]),
     "pcfm_rows_wgrad_bf16": (_I, [_P, _I, _P, _I, _L, _I, _I, _P, _P, _Z, _P]),
+    "pcfm_rows_max_workspace_bytes": (_Z, [_I, _I, _I]),
+    "pcfm_rows_max_bf16": (_I, [_P, _I, _I, _I, _P, _P, _P, _Z, _P]),
     "pcfm_head_film_fwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _F, _P, _P, _P, _P,
                                 _P]),
     "pcfm_head_silu_fwd": (_I, [_P, _P, _I, _I, _I, _P, _P]),
@@ -76,6 +78,11 @@ SIGNATURES = {
     "pcfm_bn_act_fwd": (_I, [_P, _P, _P, _I, _I, _I, _F, _F, _F, _P, _P, _P, _P, _P, _P, _Z,
                              _P]),
     "pcfm_bn_act_bwd": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _F, _P, _P, _P, _P, _Z, _P]),
+    "pcfm_gn_film_workspace_bytes": (_Z, [_I, _I, _I, _I]),
+    "pcfm_gn_film_res_fwd": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _F, _P, _P, _P, _P, _Z,
+                                  _P]),
+    "pcfm_gn_film_res_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P,
+                                  _P, _P, _Z, _P]),
 }
 
 ABI_VERSION = 6

@@ -168,3 +168,31 @@ def fused_trunk(trunk, h: torch.Tensor, emb: torch.Tensor, n: int) -> torch.Tens
     with torch.autocast("cuda", enabled=False):
         return _HeadTrunkBF16.apply(n, float(eps), x16, lin_in.weight.to(dt), lin_in.bias.to(dt),
                                     lin_out.weight.to(dt), lin_out.bias.to(dt), *blk)
+
+
+class _RowsMax(torch.autograd.Function):
+    """h.max(dim=1).values for (B, N, C) bf16 with torch.max's backward (the
+    gradient goes to the argmax row, zeros elsewhere)."""
+
+    @staticmethod
+    def forward(ctx, h):
+        from pcfm import ops
+        val, idx = ops.rows_max_bf16(h)
+        ctx.save_for_backward(idx)
+        ctx.shape = h.shape
+        return val
+
+    @staticmethod
+    def backward(ctx, gv):
+        (idx,) = ctx.saved_tensors
+        g = torch.zeros(ctx.shape, dtype=gv.dtype, device=gv.device)
+        g.scatter_(1, idx.long().unsqueeze(1), gv.unsqueeze(1))
+        return g
+
+
+def max_over_points(h: torch.Tensor) -> torch.Tensor:
+    """h.max(dim=1).values; the gfx950 kernel for contiguous (B, N, C) bf16 on a HIP device."""
+    if (h.is_cuda and h.dtype == torch.bfloat16 and h.dim() == 3 and h.is_contiguous()
+            and h.shape[1] > 0 and h.shape[2] % 2 == 0):
+        return _RowsMax.apply(h)
+    return h.max(dim=1).values

@@ -21,9 +21,10 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from modules.norm_act import gn_film_residual
 from modules.pvconv import PVConv
 from modules.shared_mlp import PointwiseConv1d, SharedMLP
-from pcfm.layers import RowsLinear, fused_trunk, fused_trunk_supported
+from pcfm.layers import RowsLinear, fused_trunk, fused_trunk_supported, max_over_points
 
 __all__ = [
     "timestep_embedding", "FiLMBlock", "VelocityNet", "ShapeEncoder",
@@ -178,7 +179,7 @@ class ShapeEncoder(nn.Module):
 
     def forward(self, pts_or_feats: torch.Tensor):
         h = self.mlp(pts_or_feats)
-        return self.head(h.max(dim=1).values), h
+        return self.head(max_over_points(h)), h
 
 
 class ConditionalLatentVelocityNet(_TimeCondEmbed):
@@ -287,7 +288,12 @@ class _PVBlock(nn.Module):
 
     def forward(self, feat_coords: Tuple[torch.Tensor, torch.Tensor], emb: torch.Tensor):
         f, c = self.post(self.pvconv(feat_coords))
-        return f + self.film(f, emb), c
+        film = self.film
+        if film.one_plus and isinstance(film.norm, nn.GroupNorm):
+            # f + GroupNorm(f) * (1 + gamma) + beta as one fused op (modules/norm_act.py)
+            gamma, beta = film.affine(emb.to(f.dtype)).chunk(2, dim=-1)
+            return gn_film_residual(f, film.norm, gamma, beta), c
+        return f + film(f, emb), c
 
 
 class _PVStage(nn.Module):

@@ -647,3 +647,53 @@ def bn_act_backward(dz: torch.Tensor, x: torch.Tensor, weight, bias, mean, invst
                   _ptr(invstd), b, c, s, float(slope), _ptr(dx), _ptr(dgb[0]), _ptr(dgb[1]),
                   _ptr(ws), ws.numel(), _stream(x))
     return dx, dgb[0], dgb[1]
+
+
+def rows_max_bf16(h: torch.Tensor):
+    """(values bf16 (B, C), indices int32 (B, C)) = max over dim 1 of h (B, N, C) bf16."""
+    _check_cuda(h, "h")
+    if h.dtype != torch.bfloat16 or h.dim() != 3 or not h.is_contiguous():
+        raise RuntimeError("rows_max_bf16: h must be a contiguous (B, N, C) bf16 tensor")
+    b, n, c = h.shape
+    val = torch.empty((b, c), dtype=torch.bfloat16, device=h.device)
+    idx = torch.empty((b, c), dtype=torch.int32, device=h.device)
+    ws = _workspace(_lib.query("pcfm_rows_max_workspace_bytes", b, n, c), h)
+    _lib.call("pcfm_rows_max_bf16", _ptr(h), b, n, c, _ptr(val), _ptr(idx), _ptr(ws), ws.numel(),
+              _stream(h))
+    return val, idx
+
+
+# --------------------------------------------------------------------------
+# GroupNorm + FiLM + residual (include/pcfm.h pcfm_gn_film_res_*)
+# --------------------------------------------------------------------------
+def gn_film_res_forward(x, weight, bias, gamma, beta, groups: int, eps: float):
+    """out = x + GroupNorm(x) * (1 + gamma[:, :, None]) + beta[:, :, None] -> (out, mean, rstd)"""
+    _check(x, "input", "f")
+    b, c, n = x.shape
+    gamma, beta = gamma.contiguous(), beta.contiguous()
+    out = torch.empty_like(x)
+    stats = torch.empty((2, b, groups), dtype=torch.float32, device=x.device)
+    ws = _workspace(_lib.query("pcfm_gn_film_workspace_bytes", b, c, n, groups), x)
+    with _timed("gn_film_res_fwd", 4 * 3 * x.numel(), x):
+        _lib.call("pcfm_gn_film_res_fwd", _ptr(x), _ptr(weight), _ptr(bias), _ptr(gamma),
+                  _ptr(beta), b, c, n, groups, float(eps), _ptr(out), _ptr(stats[0]),
+                  _ptr(stats[1]), _ptr(ws), ws.numel(), _stream(x))
+    return out, stats[0], stats[1]
+
+
+def gn_film_res_backward(dout, x, weight, bias, gamma, mean, rstd, groups: int):
+    """-> (dx, dweight, dbias, dgamma (B, C), dbeta (B, C))"""
+    dout = dout.contiguous()
+    b, c, n = x.shape
+    dx = torch.empty_like(x)
+    small = torch.empty((2 * c + 2 * b * c,), dtype=torch.float32, device=x.device)
+    dw, dbias = small[:c], small[c:2 * c]
+    dgamma = small[2 * c:2 * c + b * c].view(b, c)
+    dbeta = small[2 * c + b * c:].view(b, c)
+    ws = _workspace(_lib.query("pcfm_gn_film_workspace_bytes", b, c, n, groups), x)
+    with _timed("gn_film_res_bwd", 4 * 5 * x.numel(), x):
+        _lib.call("pcfm_gn_film_res_bwd", _ptr(dout), _ptr(x), _ptr(weight), _ptr(bias),
+                  _ptr(gamma.contiguous()), _ptr(mean), _ptr(rstd), b, c, n, groups, _ptr(dx),
+                  _ptr(dw), _ptr(dbias), _ptr(dgamma), _ptr(dbeta), _ptr(ws), ws.numel(),
+                  _stream(x))
+    return dx, dw, dbias, dgamma, dbeta

@@ -134,3 +134,22 @@ def test_fused_trunk_matches_torch_trunk(ops, width, n):
     assert set(g0) == set(g1)
     for k in g0:
         assert _relnorm(g1[k], g0[k]) < 2e-2, k
+
+
+@pytest.mark.parametrize("b,n,c", [(8, 20000, 128), (2, 777, 6), (3, 50, 384)])
+def test_rows_max_matches_torch(ops, b, n, c):
+    from pcfm.layers import max_over_points
+    g = torch.Generator(device="cuda").manual_seed(n + c)
+    h = torch.randn(b, n, c, device="cuda", generator=g).bfloat16()
+    h[0, 5:9, 0] = 100.0  # a tie: the lowest index wins
+    val, idx = ops.rows_max_bf16(h)
+    ref = h.max(dim=1).values
+    assert torch.equal(val, ref)
+    assert int(idx[0, 0]) == 5
+    assert torch.equal(h.gather(1, idx.long().unsqueeze(1)).squeeze(1), ref)
+    hh = h.clone().requires_grad_(True)
+    v = max_over_points(hh)
+    gv = torch.randn_like(v)
+    v.backward(gv)
+    exp = torch.zeros_like(h).scatter_(1, idx.long().unsqueeze(1), gv.unsqueeze(1))
+    assert torch.equal(hh.grad, exp)

@@ -64,3 +64,33 @@ def test_bn_act_falls_back_in_eval(ops):
     x = torch.randn(2, 16, 40, device="cuda")
     assert not _fusable(x, bn)
     torch.testing.assert_close(bn_act(x, bn, 0.0), torch.relu(bn(x)))
+
+
+@pytest.mark.parametrize("b,c,n,groups", [(8, 256, 20000, 32), (2, 128, 1000, 32), (3, 64, 36, 8)])
+def test_gn_film_residual_matches_torch(ops, b, c, n, groups):
+    """x + GroupNorm(x) * (1 + gamma) + beta (models.py _PVBlock / _FiLM1d) fused vs torch."""
+    from modules.norm_act import gn_film_residual
+    torch.manual_seed(1)
+    norm = torch.nn.GroupNorm(groups, c).cuda()
+    with torch.no_grad():
+        norm.weight.uniform_(0.5, 1.5)
+        norm.bias.uniform_(-0.5, 0.5)
+    x = torch.randn(b, c, n, device="cuda") * 1.5 + 2.0
+    gamma = (torch.randn(b, c, device="cuda") * 0.3).requires_grad_(True)
+    beta = (torch.randn(b, c, device="cuda") * 0.3).requires_grad_(True)
+    xa, xb = x.clone().requires_grad_(True), x.clone().requires_grad_(True)
+    ga, gb_ = gamma.detach().clone().requires_grad_(True), gamma.detach().clone().requires_grad_(True)
+    ba, bb = beta.detach().clone().requires_grad_(True), beta.detach().clone().requires_grad_(True)
+    ref = xa + (norm(xa) * (1.0 + ga[:, :, None]) + ba[:, :, None])
+    grads_ref = None
+    gy = torch.randn_like(ref)
+    ref.backward(gy)
+    grads_ref = [xa.grad, norm.weight.grad.clone(), norm.bias.grad.clone(), ga.grad, ba.grad]
+    norm.zero_grad()
+    out = gn_film_residual(xb, norm, gb_, bb)
+    torch.testing.assert_close(out, ref, rtol=1e-4, atol=1e-4)
+    out.backward(gy)
+    got = [xb.grad, norm.weight.grad, norm.bias.grad, gb_.grad, bb.grad]
+    for a, r in zip(got, grads_ref):
+        scale = r.abs().max().item()
+        torch.testing.assert_close(a, r, rtol=1e-4, atol=1e-4 * max(1.0, scale))
