@@ -341,11 +341,12 @@ int pcfm_bn_act_fwd(const float* x, const float* gamma, const float* beta, int b
                     size_t ws_bytes, void* stream);
 
 /* Backward of pcfm_bn_act_fwd given dz = dL/dy: dx [b][c][s] and
- * dgamma / dbeta [c] (all fully written). */
+ * dgamma / dbeta [c] (all fully written); if dbias_in is non-NULL it receives
+ * sum_{b,s} dx [c] -- the bias gradient of the convolution that produced x. */
 int pcfm_bn_act_bwd(const float* dz, const float* x, const float* gamma, const float* beta,
                     const float* mean, const float* invstd, int b, int c, int s, float slope,
-                    float* dx, float* dgamma, float* dbeta, void* ws, size_t ws_bytes,
-                    void* stream);
+                    float* dx, float* dgamma, float* dbeta, float* dbias_in, void* ws,
+                    size_t ws_bytes, void* stream);
 
 /* GroupNorm + FiLM + residual of the hybrid backbone's PV blocks
  * (models.py:322-346 _FiLM1d(norm="group"), :349-368 _PVBlock):

@@ -174,30 +174,54 @@ __global__ void __launch_bounds__(256)
   dgamma[c] = sgx;
 }
 
-// dx = gamma * invstd * (g - dbeta / n - xhat * dgamma / n)
+// dx = gamma * invstd * (g - dbeta / n - xhat * dgamma / n); grid (ceil(S4/256), B*C).
+// With rowpart: the block's sum of dx -> rowpart[row][block] (producer bias grad).
 __global__ void __launch_bounds__(256)
     bn_bwd_apply_kernel(const float* __restrict__ dz, const float* __restrict__ x,
                         const float* __restrict__ mean, const float* __restrict__ invstd,
                         const float* __restrict__ gamma, const float* __restrict__ beta,
                         const float* __restrict__ dgamma, const float* __restrict__ dbeta, int C,
-                        int S4, float inv_n, float slope, float* __restrict__ dx) {
+                        int S4, float inv_n, float slope, float* __restrict__ dx,
+                        float* __restrict__ rowpart) {
+  __shared__ float sh[8];
   const int s4 = blockIdx.x * 256 + threadIdx.x;
-  if (s4 >= S4) return;
+  const bool ok = s4 < S4;
   const int c = (int)(blockIdx.y % C);
-  const size_t i = (size_t)blockIdx.y * S4 + s4;
+  const size_t i = (size_t)blockIdx.y * S4 + (ok ? s4 : 0);
   const float m = mean[c], is = invstd[c], gm = gamma[c], bt = beta[c];
   const float mg = dbeta[c] * inv_n, mgx = dgamma[c] * inv_n, k = gm * is;
-  const float4 v = reinterpret_cast<const float4*>(x)[i];
-  const float4 d = reinterpret_cast<const float4*>(dz)[i];
-  const float xv[4] = {v.x, v.y, v.z, v.w}, dv[4] = {d.x, d.y, d.z, d.w};
-  float o[4];
+  float o[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  if (ok) {
+    const float4 v = reinterpret_cast<const float4*>(x)[i];
+    const float4 d = reinterpret_cast<const float4*>(dz)[i];
+    const float xv[4] = {v.x, v.y, v.z, v.w}, dv[4] = {d.x, d.y, d.z, d.w};
 #pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const float xh = (xv[e] - m) * is;
-    const float g = __builtin_fmaf(xh, gm, bt) > 0.0f ? dv[e] : dv[e] * slope;
-    o[e] = k * ((g - mg) - xh * mgx);
+    for (int e = 0; e < 4; ++e) {
+      const float xh = (xv[e] - m) * is;
+      const float g = __builtin_fmaf(xh, gm, bt) > 0.0f ? dv[e] : dv[e] * slope;
+      o[e] = k * ((g - mg) - xh * mgx);
+    }
+    reinterpret_cast<float4*>(dx)[i] = make_float4(o[0], o[1], o[2], o[3]);
   }
-  reinterpret_cast<float4*>(dx)[i] = make_float4(o[0], o[1], o[2], o[3]);
+  if (rowpart != nullptr) {  // block-uniform branch: every thread takes part
+    float t = (o[0] + o[1]) + (o[2] + o[3]), z = 0.0f;
+    block_sum2(t, z, sh);
+    if (threadIdx.x == 0) rowpart[(size_t)blockIdx.y * gridDim.x + blockIdx.x] = t;
+  }
+}
+
+// dbias[c] = sum over b, then over blocks, of rowpart[(b * C + c) * nch + k]
+__global__ void __launch_bounds__(256)
+    bn_bias_finalize_kernel(const float* __restrict__ rowpart, int B, int C, int nch,
+                            float* __restrict__ dbias) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  float s = 0.0f;
+  for (int b = 0; b < B; ++b) {
+    const float* p = rowpart + ((size_t)b * C + c) * nch;
+    for (int k = 0; k < nch; ++k) s += p[k];
+  }
+  dbias[c] = s;
 }
 
 // ---------------------------------------------------------------------------
@@ -409,7 +433,8 @@ using namespace pcfm;
 
 extern "C" size_t pcfm_bn_workspace_bytes(int b, int c, int s) {
   if (!bn_ok(b, c, s)) return 0;
-  return (size_t)c * bn_parts(b) * 2 * sizeof(float);
+  const size_t rowpart = (size_t)b * c * ceil_div(s / 4, 256);
+  return ((size_t)c * bn_parts(b) * 2 + rowpart) * sizeof(float);
 }
 
 extern "C" int pcfm_bn_act_fwd(const float* x, const float* gamma, const float* beta, int b, int c,
@@ -435,7 +460,7 @@ extern "C" int pcfm_bn_act_fwd(const float* x, const float* gamma, const float* 
 extern "C" int pcfm_bn_act_bwd(const float* dz, const float* x, const float* gamma,
                                const float* beta, const float* mean, const float* invstd, int b,
                                int c, int s, float slope, float* dx, float* dgamma, float* dbeta,
-                               void* ws, size_t ws_bytes, void* stream) {
+                               float* dbias_in, void* ws, size_t ws_bytes, void* stream) {
   PCFM_CHECK_ARG(bn_ok(b, c, s), "bn_act_bwd: bad shape b=%d c=%d s=%d (s %% 4 == 0 needed)", b,
                  c, s);
   PCFM_CHECK_ARG(ws_bytes >= pcfm_bn_workspace_bytes(b, c, s), "bn_act_bwd: workspace too small");
@@ -445,9 +470,14 @@ extern "C" int pcfm_bn_act_bwd(const float* dz, const float* x, const float* gam
                      invstd, gamma, beta, b, c, s, slope, part);
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(ceil_div(c, 256)), dim3(256), 0, st,
                      (const float*)part, c, bn_parts(b), dgamma, dbeta);
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(ceil_div(s / 4, 256), b * c), dim3(256), 0, st, dz,
-                     x, mean, invstd, gamma, beta, (const float*)dgamma, (const float*)dbeta, c,
-                     s / 4, (float)(1.0 / ((double)b * s)), slope, dx);
+  const int nch = ceil_div(s / 4, 256);
+  float* rowpart = dbias_in != nullptr ? part + (size_t)c * bn_parts(b) * 2 : nullptr;
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(nch, b * c), dim3(256), 0, st, dz, x, mean, invstd,
+                     gamma, beta, (const float*)dgamma, (const float*)dbeta, c, s / 4,
+                     (float)(1.0 / ((double)b * s)), slope, dx, rowpart);
+  if (dbias_in != nullptr)
+    hipLaunchKernelGGL(bn_bias_finalize_kernel, dim3(ceil_div(c, 256)), dim3(256), 0, st,
+                       (const float*)rowpart, b, c, nch, dbias_in);
   return check_launch("bn_act_bwd");
 }
 

@@ -12,7 +12,7 @@ and the activation run as in the reference.
 import torch
 import torch.nn.functional as F
 
-__all__ = ["bn_act", "gn_film_residual"]
+__all__ = ["bn_act", "conv_bn_act", "gn_film_residual"]
 
 
 class _BNAct(torch.autograd.Function):
@@ -29,7 +29,7 @@ class _BNAct(torch.autograd.Function):
     def backward(ctx, dy):
         from pcfm import ops
         x, weight, bias, mean, invstd = ctx.saved_tensors
-        dx, dgamma, dbeta = ops.bn_act_backward(dy, x, weight, bias, mean, invstd, ctx.slope)
+        dx, dgamma, dbeta, _ = ops.bn_act_backward(dy, x, weight, bias, mean, invstd, ctx.slope)
         return dx, dgamma, dbeta, None, None, None, None, None
 
 
@@ -50,6 +50,84 @@ def bn_act(x: torch.Tensor, bn, slope: float) -> torch.Tensor:
                             float(bn.eps), float(bn.momentum), float(slope))
     y = bn(x)
     return F.relu(y, inplace=True) if slope == 0 else F.leaky_relu(y, slope, inplace=True)
+
+
+class _PwBnAct(torch.autograd.Function):
+    """SharedMLP layer: act(BN(Conv1d_1x1(x))) in one autograd node, so the
+    conv's bias gradient comes out of the BN backward pass (sum of dBN/dy)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, gamma, beta, rmean, rvar, eps, momentum, slope):
+        from pcfm import ops
+        y = ops.pointwise_forward(x, w, b)
+        z, mean, invstd = ops.bn_act_forward(y, gamma, beta, eps, slope, momentum, rmean, rvar)
+        ctx.save_for_backward(x, w, y, gamma, beta, mean, invstd)
+        ctx.slope, ctx.has_bias = slope, b is not None
+        return z
+
+    @staticmethod
+    def backward(ctx, dz):
+        from pcfm import ops
+        x, w, y, gamma, beta, mean, invstd = ctx.saved_tensors
+        dy, dgamma, dbeta, db = ops.bn_act_backward(dz, y, gamma, beta, mean, invstd, ctx.slope,
+                                                    want_dbias_in=ctx.has_bias)
+        dx = ops.pointwise_backward_data(dy, w) if ctx.needs_input_grad[0] else None
+        dw = ops.pointwise_backward_weight(x, dy).view_as(w) if ctx.needs_input_grad[1] else None
+        return dx, dw, db, dgamma, dbeta, None, None, None, None, None
+
+
+class _Conv3dBnAct(torch.autograd.Function):
+    """PVConv voxel layer: act(BN3d(Conv3d(x))) in one autograd node: split(x)
+    kept for the weight gradient, the conv bias gradient from the BN backward."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, gamma, beta, rmean, rvar, eps, momentum, slope):
+        from pcfm import ops
+        bsz, cin, r = x.shape[0], x.shape[1], x.shape[2]
+        cout = w.shape[0]
+        xs = ops.conv3d_split(x)
+        y = ops.conv3d_igemm_split(xs, ops.conv3d_prep_weight(w, False), b, bsz, cin, cout, r,
+                                   "conv3d_fwd")
+        z, mean, invstd = ops.bn_act_forward(y, gamma, beta, eps, slope, momentum, rmean, rvar)
+        ctx.save_for_backward(xs, w, y, gamma, beta, mean, invstd)
+        ctx.slope, ctx.has_bias, ctx.dims = slope, b is not None, (bsz, cin, cout, r)
+        return z
+
+    @staticmethod
+    def backward(ctx, dz):
+        from pcfm import ops
+        xs, w, y, gamma, beta, mean, invstd = ctx.saved_tensors
+        bsz, cin, cout, r = ctx.dims
+        dy, dgamma, dbeta, db = ops.bn_act_backward(dz, y, gamma, beta, mean, invstd, ctx.slope,
+                                                    want_dbias_in=ctx.has_bias)
+        gys = ops.conv3d_split(dy)
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = ops.conv3d_igemm_split(gys, ops.conv3d_prep_weight(w, True), None, bsz, cout, cin,
+                                        r, "conv3d_bwd_data")
+        if ctx.needs_input_grad[1]:
+            dw = ops.conv3d_wgrad_split(xs, gys, bsz, cin, cout, r)
+        return dx, dw, db, dgamma, dbeta, None, None, None, None, None
+
+
+def conv_bn_act(conv, bn, x: torch.Tensor, slope: float) -> torch.Tensor:
+    """act(bn(conv(x))) for a PointwiseConv1d / VoxelConv3d `conv`: one fused
+    autograd node on the GPU path, the modules' own forwards otherwise."""
+    if _fusable_pre(bn) and hasattr(conv, "x3_ok") and conv.x3_ok(x) and conv.bias is not None:
+        out_shape_ok = x[0, 0].numel() % 4 == 0 and x.shape[0] * conv.out_channels < 65536
+        if out_shape_ok:
+            from modules.shared_mlp import PointwiseConv1d
+            fn = _PwBnAct if isinstance(conv, PointwiseConv1d) else _Conv3dBnAct
+            bn.num_batches_tracked.add_(1)
+            return fn.apply(x.contiguous(), conv.weight, conv.bias, bn.weight, bn.bias,
+                            bn.running_mean, bn.running_var, float(bn.eps), float(bn.momentum),
+                            float(slope))
+    return bn_act(conv(x), bn, slope)
+
+
+def _fusable_pre(bn) -> bool:
+    return (bn.training and bn.affine and bn.track_running_stats and bn.momentum is not None
+            and bn.running_mean is not None)
 
 
 class _GNFiLMRes(torch.autograd.Function):

@@ -11,7 +11,7 @@ point_features.layers.*) are the reference's.
 import torch.nn as nn
 
 import modules.functional as F
-from modules.norm_act import bn_act
+from modules.norm_act import conv_bn_act
 from modules.se import SE3d
 from modules.shared_mlp import SharedMLP
 from modules.voxel_conv import VoxelConv3d
@@ -48,8 +48,8 @@ class PVConv(nn.Module):
         features, coords = inputs
         grid, grid_coords = self.voxelization(features, coords)
         layers = self.voxel_layers  # Conv3d, BN3d, LeakyReLU, Conv3d, BN3d, LeakyReLU[, SE3d]
-        grid = bn_act(layers[0](grid), layers[1], layers[2].negative_slope)
-        grid = bn_act(layers[3](grid), layers[4], layers[5].negative_slope)
+        grid = conv_bn_act(layers[0], layers[1], grid, layers[2].negative_slope)
+        grid = conv_bn_act(layers[3], layers[4], grid, layers[5].negative_slope)
         if len(layers) > 6:
             grid = layers[6](grid)
         voxel_branch = F.trilinear_devoxelize(grid, grid_coords, self.resolution, self.training)

@@ -13,7 +13,7 @@ under autocast it stays a batched GEMM so torch's autocast casting applies.
 import torch
 import torch.nn as nn
 
-from modules.norm_act import bn_act
+from modules.norm_act import conv_bn_act
 
 __all__ = ["SharedMLP", "PointwiseConv1d"]
 
@@ -46,14 +46,20 @@ class PointwiseConv1d(nn.Conv1d):
 
     exact_fp32 = False
 
+    def _is_1x1(self) -> bool:
+        return (self.kernel_size == (1,) and self.groups == 1 and self.stride == (1,)
+                and self.padding in ((0,), "valid") and self.dilation == (1,))
+
+    def x3_ok(self, x) -> bool:
+        """True if forward(x) runs on the bf16x3 pointwise GEMM."""
+        return (self._is_1x1() and x.dim() == 3 and x.is_cuda and x.dtype == torch.float32
+                and self.weight.dtype == torch.float32 and not self.exact_fp32
+                and not torch.is_autocast_enabled("cuda"))
+
     def forward(self, x):
-        if self.kernel_size != (1,) or self.groups != 1 or self.stride != (1,) \
-                or self.padding not in ((0,), "valid") or self.dilation != (1,):
+        if not self._is_1x1() or x.dim() != 3:
             return super().forward(x)
-        if x.dim() != 3:
-            return super().forward(x)
-        if (x.is_cuda and x.dtype == torch.float32 and self.weight.dtype == torch.float32
-                and not self.exact_fp32 and not torch.is_autocast_enabled("cuda")):
+        if self.x3_ok(x):
             return _PointwiseX3.apply(x, self.weight, self.bias)
         # bmm against the batch-broadcast weight: the result is a contiguous
         # (B, C_out, N) tensor (torch.matmul(2-D, 3-D) returns a transposed view,
@@ -86,7 +92,7 @@ class SharedMLP(nn.Module):
         # (conv, BN, ReLU) triples; BN + ReLU fused on the GPU (modules/norm_act.py)
         layers = self.layers
         for i in range(0, len(layers), 3):
-            x = bn_act(layers[i](x), layers[i + 1], 0.0)
+            x = conv_bn_act(layers[i], layers[i + 1], x, 0.0)
         return x
 
     def forward(self, inputs):

@@ -56,13 +56,17 @@ class _Conv3dX3(torch.autograd.Function):
 class VoxelConv3d(nn.Conv3d):
     exact_fp32 = False
 
-    def forward(self, x):
+    def x3_ok(self, x) -> bool:
+        """True if forward(x) runs on the bf16x3 implicit GEMM."""
         if (self.exact_fp32 or not x.is_cuda or x.dtype != torch.float32
                 or self.kernel_size != (3, 3, 3) or self.stride != (1, 1, 1)
                 or self.padding != (1, 1, 1) or self.dilation != (1, 1, 1) or self.groups != 1
-                or self.padding_mode != "zeros"):
-            return super().forward(x)
+                or self.padding_mode != "zeros" or torch.is_autocast_enabled("cuda")):
+            return False
         from pcfm import ops
-        if not (ops.conv3d_supported(x, self.weight) and ops.conv3d_wgrad_supported(x, self.weight)):
+        return ops.conv3d_supported(x, self.weight) and ops.conv3d_wgrad_supported(x, self.weight)
+
+    def forward(self, x):
+        if not self.x3_ok(x):
             return super().forward(x)
         return _Conv3dX3.apply(x, self.weight, self.bias)

@@ -77,7 +77,8 @@ SIGNATURES = {
     "pcfm_bn_workspace_bytes": (_Z, [_I, _I, _I]),
     "pcfm_bn_act_fwd": (_I, [_P, _P, _P, _I, _I, _I, _F, _F, _F, _P, _P, _P, _P, _P, _P, _Z,
                              _P]),
-    "pcfm_bn_act_bwd": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _F, _P, _P, _P, _P, _Z, _P]),
+    "pcfm_bn_act_bwd": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _F, _P, _P, _P, _P, _P, _Z,
+                             _P]),
     "pcfm_gn_film_workspace_bytes": (_Z, [_I, _I, _I, _I]),
     "pcfm_gn_film_res_fwd": (_I, [_P, _P, _P, _P, _P, _I, _I, _I, _I, _F, _P, _P, _P, _P, _Z,
                                   _P]),

@@ -634,19 +634,21 @@ def bn_act_forward(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, ep
     return y, stats[0], stats[1]
 
 
-def bn_act_backward(dz: torch.Tensor, x: torch.Tensor, weight, bias, mean, invstd, slope: float):
-    """-> (dx, dgamma, dbeta)"""
+def bn_act_backward(dz: torch.Tensor, x: torch.Tensor, weight, bias, mean, invstd, slope: float,
+                    want_dbias_in: bool = False):
+    """-> (dx, dgamma, dbeta, dbias_in) with dbias_in = sum of dx over (b, s) per
+    channel (the producer's bias gradient) or None."""
     dz = dz.contiguous()
     b, c = x.shape[0], x.shape[1]
     s = x.numel() // max(1, b * c)
     dx = torch.empty_like(x)
-    dgb = torch.empty((2, c), dtype=torch.float32, device=x.device)
+    dgb = torch.empty((3, c), dtype=torch.float32, device=x.device)
     ws = _workspace(_lib.query("pcfm_bn_workspace_bytes", b, c, s), x)
     with _timed("bn_act_bwd", 4 * 5 * x.numel(), x):
         _lib.call("pcfm_bn_act_bwd", _ptr(dz), _ptr(x), _ptr(weight), _ptr(bias), _ptr(mean),
                   _ptr(invstd), b, c, s, float(slope), _ptr(dx), _ptr(dgb[0]), _ptr(dgb[1]),
-                  _ptr(ws), ws.numel(), _stream(x))
-    return dx, dgb[0], dgb[1]
+                  _ptr(dgb[2]) if want_dbias_in else None, _ptr(ws), ws.numel(), _stream(x))
+    return dx, dgb[0], dgb[1], (dgb[2] if want_dbias_in else None)
 
 
 def rows_max_bf16(h: torch.Tensor):

@@ -94,3 +94,45 @@ def test_gn_film_residual_matches_torch(ops, b, c, n, groups):
     for a, r in zip(got, grads_ref):
         scale = r.abs().max().item()
         torch.testing.assert_close(a, r, rtol=1e-4, atol=1e-4 * max(1.0, scale))
+
+
+@pytest.mark.parametrize("kind", ["pointwise", "voxel"])
+def test_conv_bn_act_fused_matches_modules(ops, kind):
+    """conv_bn_act (one fused autograd node, conv bias grad from the BN backward)
+    vs the conv module + torch BatchNorm + activation."""
+    from modules.norm_act import conv_bn_act
+    from modules.shared_mlp import PointwiseConv1d
+    from modules.voxel_conv import VoxelConv3d
+    torch.manual_seed(2)
+    if kind == "pointwise":
+        conv = PointwiseConv1d(128, 256, 1).cuda()
+        bn = torch.nn.BatchNorm1d(256).cuda()
+        x = torch.randn(4, 128, 3000, device="cuda")
+        slope = 0.0
+    else:
+        conv = VoxelConv3d(128, 128, 3, padding=1).cuda()
+        bn = torch.nn.BatchNorm3d(128, eps=1e-4).cuda()
+        x = torch.randn(2, 128, 16, 16, 16, device="cuda")
+        slope = 0.1
+    conv2, bn2 = copy.deepcopy(conv), copy.deepcopy(bn)
+    xa, xb = x.clone().requires_grad_(True), x.clone().requires_grad_(True)
+    act = torch.nn.ReLU() if slope == 0 else torch.nn.LeakyReLU(slope)
+    za = act(bn(conv(xa)))
+    zb = conv_bn_act(conv2, bn2, xb, slope)
+    assert zb.grad_fn is not None and "BnAct" in type(zb.grad_fn).__name__
+    torch.testing.assert_close(zb, za, rtol=1e-3, atol=1e-3)
+    gz = torch.randn_like(za)
+    za.backward(gz)
+    zb.backward(gz)
+
+    def rel(a, b):
+        return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+    assert rel(xb.grad, xa.grad) < 1e-3
+    assert rel(conv2.weight.grad, conv.weight.grad) < 1e-3
+    # the conv bias feeds a BatchNorm: its exact gradient is 0 (sum of a centred
+    # quantity); both sides are fp32 round-off of that zero
+    assert conv2.bias.grad.abs().max() < 1e-2 and conv.bias.grad.abs().max() < 1e-2
+    assert rel(bn2.weight.grad, bn.weight.grad) < 1e-3
+    assert rel(bn2.bias.grad, bn.bias.grad) < 1e-3
+    torch.testing.assert_close(bn2.running_mean, bn.running_mean, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(bn2.running_var, bn.running_var, rtol=1e-4, atol=1e-5)
