@@ -225,7 +225,9 @@ def main():
                     "avg_launch_ms": d["ms"] / d["launches"]}
 
         roofline = roof(max(summary, key=lambda k: summary[k]["ms"])) if summary else None
-        hbm_ops = [k for k in summary if summary[k]["kind"] == "hbm"]
+        voxel_ops = ("avg_voxelize_fwd", "avg_voxelize_bwd", "trilinear_devoxelize_fwd",
+                     "trilinear_devoxelize_bwd")  # the PVConv scatter/gather
+        hbm_ops = [k for k in summary if k in voxel_ops]
         roofline_scatter = roof(max(hbm_ops, key=lambda k: summary[k]["ms"])) if hbm_ops else None
         log(f"{ms:.2f} ms/step, {value / 1e6:.3f} M points/s; losses {loss_p:.4f} {loss_z:.4f}")
         cham = None
