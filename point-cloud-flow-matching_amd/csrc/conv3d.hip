@@ -126,22 +126,6 @@ __device__ __forceinline__ void tile_mfma_k(const uint16_t* buf, int wr, int wc,
   }
 }
 
-// Staging registers as one vector value per operand image (an array of uint4
-// captured by the load/store lambdas is placed in scratch by hipcc).
-template <int Q>
-using StageVec = unsigned int __attribute__((ext_vector_type(4 * Q)));
-template <int Q>
-__device__ __forceinline__ void sv_put(StageVec<Q>& v, int q, uint4 x) {
-  v[4 * q] = x.x;
-  v[4 * q + 1] = x.y;
-  v[4 * q + 2] = x.z;
-  v[4 * q + 3] = x.w;
-}
-template <int Q>
-__device__ __forceinline__ uint4 sv_get(const StageVec<Q>& v, int q) {
-  return uint4{v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
-}
-
 template <int TM, int TN, int KT>
 __global__ void __launch_bounds__(256)
     conv3_igemm_cl_kernel(const uint16_t* __restrict__ xh, const uint16_t* __restrict__ xl,

@@ -110,6 +110,22 @@ __device__ __forceinline__ void store_split(const float (&v)[N], uint16_t* dh, u
 }
 
 
+// Staging registers as one vector value per operand image (an array of uint4
+// captured by the load/store lambdas is placed in scratch by hipcc).
+template <int Q>
+using StageVec = unsigned int __attribute__((ext_vector_type(4 * Q)));
+template <int Q>
+__device__ __forceinline__ void sv_put(StageVec<Q>& v, int q, uint4 x) {
+  v[4 * q] = x.x;
+  v[4 * q + 1] = x.y;
+  v[4 * q + 2] = x.z;
+  v[4 * q + 3] = x.w;
+}
+template <int Q>
+__device__ __forceinline__ uint4 sv_get(const StageVec<Q>& v, int q) {
+  return uint4{v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
+}
+
 // ---------------------------------------------------------------------------
 // Transposed-read images (cdna_hip_programming.md T10): a [rows][128] bf16
 // tile stored as it lies in memory (256-B rows, 16-B chunks XOR-swizzled) and
