@@ -75,7 +75,7 @@ __global__ void __launch_bounds__(256)
 
 // ---------------------------------------------------------------------------
 // Forward / backward-data implicit GEMM over the channels-last split input.
-// grid = (V / TN, M / TM, B); K-steps s = tap * (K / KT) + channel chunk.
+// grid = (V / TN) * (M / TM) * B (1-D); K-steps s = tap * (K / KT) + channel chunk.
 // A = pre-split weights W'[tap][m][k], B = pre-split input rows xs[b][v][k]:
 // every staging access is a 16-B copy (no per-tap split arithmetic).  KT = 64
 // channels per step: 48 MFMAs per wave between barriers (TM = TN = 128).
@@ -115,14 +115,22 @@ __device__ __forceinline__ void tile_mfma_k(const uint16_t* buf, int wr, int wc,
       bh[j] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(sBh + o));
       bl[j] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(sBl + o));
     }
+    // product-major order: consecutive MFMAs write different accumulators
 #pragma unroll
     for (int i = 0; i < T::SI; ++i)
 #pragma unroll
-      for (int j = 0; j < T::SJ; ++j) {
+      for (int j = 0; j < T::SJ; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < T::SI; ++i)
+#pragma unroll
+      for (int j = 0; j < T::SJ; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < T::SI; ++i)
+#pragma unroll
+      for (int j = 0; j < T::SJ; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
-      }
   }
 }
 
@@ -135,7 +143,19 @@ __global__ void __launch_bounds__(256)
   using T = TileK<TM, TN, KT>;
   __shared__ __attribute__((aligned(16))) uint16_t lds[T::BUF];
   const int V = R * R * R, R2 = R * R;
-  const int b = blockIdx.z, m0 = blockIdx.y * TM, v0 = blockIdx.x * TN;
+  // 1-D grid of (m tile, voxel tile, b) items, m fastest, dealt to the 8 XCDs
+  // in contiguous runs (T1 remap): an XCD sweeps a contiguous slab of the grid,
+  // so the 27 taps' neighbour rows of concurrently resident blocks overlap in
+  // its L2 instead of streaming from the Infinity Cache.
+  int id = (int)blockIdx.x;
+  {
+    const int nwg = (int)gridDim.x, q = nwg / 8, rr = nwg % 8, xcd = id % 8;
+    id = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + id / 8;
+  }
+  const int nmt = M / TM, nvt = V / TN;
+  const int m0 = (id % nmt) * TM;
+  id /= nmt;
+  const int v0 = (id % nvt) * TN, b = id / nvt;
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   const int wr = w >> 1, wc = w & 1, r = lane & 31, h = lane >> 5;
@@ -331,11 +351,18 @@ __global__ void __launch_bounds__(256)
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
+        for (int j = 0; j < 2; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
-        }
     }
     __syncthreads();
     if (ks + 1 < k1) store();
@@ -502,11 +529,13 @@ extern "C" int pcfm_conv3d_igemm_cl(const void* xs, const void* wsplit, const fl
   hipStream_t st = (hipStream_t)stream;
   const long long big_blocks = (long long)(V / 128) * (cout / 128) * b;
   if (big_blocks >= 2 * kCUs) {
-    hipLaunchKernelGGL((conv3_igemm_cl_kernel<128, 128, PCFM_CONV_KT>), dim3(V / 128, cout / 128, b),
-                       dim3(256), 0, st, xh, xl, wh, wh + total, bias, y, cin, cout, r);
+    hipLaunchKernelGGL((conv3_igemm_cl_kernel<128, 128, PCFM_CONV_KT>),
+                       dim3((V / 128) * (cout / 128) * b), dim3(256), 0, st, xh, xl, wh, wh + total,
+                       bias, y, cin, cout, r);
   } else {
-    hipLaunchKernelGGL((conv3_igemm_cl_kernel<64, 64, PCFM_CONV_KT>), dim3(V / 64, cout / 64, b),
-                       dim3(256), 0, st, xh, xl, wh, wh + total, bias, y, cin, cout, r);
+    hipLaunchKernelGGL((conv3_igemm_cl_kernel<64, 64, PCFM_CONV_KT>),
+                       dim3((V / 64) * (cout / 64) * b), dim3(256), 0, st, xh, xl, wh, wh + total,
+                       bias, y, cin, cout, r);
   }
   return check_launch("conv3d_igemm_cl");
 }
