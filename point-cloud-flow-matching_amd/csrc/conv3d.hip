@@ -21,6 +21,7 @@
 // LDS as bf16 hi/lo rows; D[m][voxel] leaves with lanes along voxels, i.e.
 // coalesced into the NCDHW output.  Out-of-grid neighbours read as 0 (padding).
 #include <algorithm>
+#include <mutex>
 
 #include "mfma_x3.hpp"
 
@@ -176,7 +177,7 @@ __global__ void __launch_bounds__(256)
   StageVec<T::QA> rah, ral;
   StageVec<T::QB> rbh, rbl;
   auto load = [&](int s) {
-    const int tap = s / nck, c0 = (s - tap * nck) * KT;
+    const int c0 = (s / 27) * KT, tap = s - (s / 27) * 27;  // chunk-major (L2 reuse)
 #pragma unroll
     for (int q = 0; q < T::QA; ++q) {
       const int row = (t + 256 * q) / T::CPR;
@@ -239,6 +240,173 @@ __global__ void __launch_bounds__(256)
       for (int e = 0; e < 16; ++e) {
         const int m = m0 + wr * (TM / 2) + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
         const int v = v0 + wc * (TN / 2) + j * 32 + r;
+        yb[(size_t)m * V + v] = acc[i][j][e] + (bias != nullptr ? bias[m] : 0.0f);
+      }
+}
+
+// ---------------------------------------------------------------------------
+// Forward / backward-data implicit GEMM, LDS-DMA pipelined form (the large
+// grids: r = 32 and r = 16).  128 (m) x 256 (voxel) tile, 8 waves of 64 x 64,
+// K-steps of 32 channels, THREE LDS stages filled by global_load_lds_dwordx4
+// (cdna_hip_programming.md section 5 "Async global->LDS copy"): the loads of
+// step s+2 are in flight while step s computes; one raw s_barrier per step,
+// counted s_waitcnt vmcnt (never 0 inside the loop).  An LDS-DMA writes
+// lane-linear 16-B pieces, so the bank swizzle is applied on the SOURCE side:
+// physical chunk p of row r holds logical k-chunk p ^ ((r >> 2) & 3), which
+// makes the ds_read_b128 fragment reads conflict-free (64-B rows).  A
+// neighbour outside the grid reads from a zero row (the padding).
+// ---------------------------------------------------------------------------
+constexpr int kGM = 128, kGN = 256, kGK = 32, kGStages = 3;
+constexpr int kGA = kGM * kGK * 2;               // bytes per A image (hi or lo)
+constexpr int kGB = kGN * kGK * 2;               // bytes per B image
+constexpr int kGStage = 2 * kGA + 2 * kGB;       // 48 KiB
+
+__device__ __forceinline__ int gswz(int row) { return (row >> 2) & 3; }
+
+__device__ __forceinline__ void glds16(const void* g, uint8_t* l) {
+  __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)g,
+                                   (void __attribute__((address_space(3)))*)l, 16, 0, 0);
+}
+
+__global__ void __launch_bounds__(512)
+    conv3_igemm_glds_kernel(const uint16_t* __restrict__ xh, const uint16_t* __restrict__ xl,
+                            const uint16_t* __restrict__ wh, const uint16_t* __restrict__ wl,
+                            const uint16_t* __restrict__ zrow, const float* __restrict__ bias,
+                            float* __restrict__ y, int K, int M, int R) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kGStages * kGStage];
+  const int V = R * R * R, R2 = R * R;
+  int id = (int)blockIdx.x;
+  {
+    const int nwg = (int)gridDim.x, q = nwg / 8, rr = nwg % 8, xcd = id % 8;
+    id = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + id / 8;
+  }
+  const int nmt = M / kGM, nvt = V / kGN;
+  const int m0 = (id % nmt) * kGM;
+  id /= nmt;
+  const int v0 = (id % nvt) * kGN, b = id / nvt;
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wr = w >> 2, wc = w & 3, r = lane & 31, h = lane >> 5;
+  const int nck = K / kGK, nsteps = 27 * nck;
+  const size_t bV = (size_t)b * V;
+
+  // A pieces: I = 2w + q -> image I >> 3, rows ((I & 7) << 4) + lane / 4.
+  // Per-piece element offsets are fixed; a step adds the uniform tap / chunk offset.
+  const uint16_t* abase[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int I = 2 * w + q;
+    const int row = ((I & 7) << 4) + (lane >> 2);
+    abase[q] = ((I >> 3) ? wl : wh) + (size_t)(m0 + row) * K + (((lane & 3) ^ gswz(row)) << 3);
+  }
+  // B pieces: I = 4w + q -> image I >> 4 (waves 0-3: hi, 4-7: lo), rows ((I & 15) << 4) + lane / 4
+  const uint16_t* __restrict__ ximg = (w >= 4) ? xl : xh;
+  const uint16_t* bbase[4];
+  const uint16_t* zbase[4];
+  int bxyz[4];  // x | y << 10 | z << 20 of the piece's voxel
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int I = 4 * w + q;
+    const int row = ((I & 15) << 4) + (lane >> 2);
+    const int v = v0 + row;
+    const int cofs = ((lane & 3) ^ gswz(row)) << 3;
+    bbase[q] = ximg + (bV + v) * K + cofs;
+    zbase[q] = zrow + cofs;
+    bxyz[q] = (v / R2) | (((v / R) % R) << 10) | ((v % R) << 20);
+  }
+
+  auto issue = [&](int s, int buf) {
+    // channel-chunk-major: the 27 taps of one chunk are consecutive, so the
+    // neighbour rows they re-read stay in L2 (tap-major measured slower)
+    const int c0 = (s / 27) * kGK, tap = s - (s / 27) * 27;
+    uint8_t* base = lds + buf * kGStage;
+    const size_t aofs = (size_t)tap * M * K + c0;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int I = 2 * w + q;
+      glds16(abase[q] + aofs, base + (I >> 3) * kGA + (I & 7) * 1024);
+    }
+    const int dx = tap / 9 - 1, dy = (tap / 3) % 3 - 1, dz = tap % 3 - 1;
+    const long long bofs = (long long)(dx * R2 + dy * R + dz) * K + c0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int I = 4 * w + q;
+      const int x = bxyz[q] & 1023, yy = (bxyz[q] >> 10) & 1023, z = bxyz[q] >> 20;
+      const bool inb = (unsigned)(x + dx) < (unsigned)R && (unsigned)(yy + dy) < (unsigned)R &&
+                       (unsigned)(z + dz) < (unsigned)R;
+      glds16(inb ? bbase[q] + bofs : zbase[q], base + 2 * kGA + (I >> 4) * kGB + (I & 15) * 1024);
+    }
+  };
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
+
+  issue(0, 0);
+  if (nsteps > 1) issue(1, 1);
+  for (int s = 0; s < nsteps; ++s) {
+    // stage s landed (this wave's 6 pieces of it): leave stage s+1's 6 in flight
+    if (s + 1 < nsteps) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // everyone's stage s landed; stage s-1 reads done
+#ifndef PCFM_EXP_NOLOAD
+    if (s + 2 < nsteps) issue(s + 2, (s + 2) % kGStages);
+#endif
+    const uint8_t* base = lds + (s % kGStages) * kGStage;
+#pragma unroll
+    for (int kk = 0; kk < kGK / 16; ++kk) {
+      const int kc = 2 * kk + h;
+      bf16x8 ah[2], al[2], bh[2], bl[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int row = wr * 64 + i * 32 + r;
+        const int off = row * 64 + ((kc ^ gswz(row)) << 4);
+        ah[i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(base + off));
+        al[i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(base + kGA + off));
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int row = wc * 64 + j * 32 + r;
+        const int off = 2 * kGA + row * 64 + ((kc ^ gswz(row)) << 4);
+        bh[j] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(base + off));
+        bl[j] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(base + kGB + off));
+      }
+#ifdef PCFM_EXP_NOMFMA
+      acc[0][0][kk] += (float)(ah[0][0] + al[0][1] + ah[1][2] + al[1][3] + bh[0][4] + bl[0][5] +
+                               bh[1][6] + bl[1][7]);
+      continue;
+#endif
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  float* __restrict__ yb = y + (size_t)b * M * V;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int m = m0 + wr * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+        const int v = v0 + wc * 64 + j * 32 + r;
         yb[(size_t)m * V + v] = acc[i][j][e] + (bias != nullptr ? bias[m] : 0.0f);
       }
 }
@@ -453,6 +621,22 @@ extern "C" int pcfm_conv3d_supported(int b, int cin, int cout, int r) {
 #define PCFM_CONV_KT 64
 #endif
 
+// One 256-B zero buffer per device (the LDS-DMA source of out-of-grid rows).
+static const uint16_t* zero_row() {
+  static std::mutex mu;
+  static const uint16_t* rows[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  std::lock_guard<std::mutex> lock(mu);
+  if (rows[dev] == nullptr) {
+    void* p = nullptr;
+    if (hipMalloc(&p, 256) != hipSuccess) return nullptr;
+    if (hipMemset(p, 0, 256) != hipSuccess) return nullptr;
+    rows[dev] = (const uint16_t*)p;
+  }
+  return rows[dev];
+}
+
 extern "C" size_t pcfm_conv3d_igemm_workspace_bytes(int b, int cin, int cout, int r) {
   if (!conv3_shape_ok(b, cin, cout, r) || cin % 64 != 0) return 0;
   return (size_t)2 * b * r * r * r * cin * sizeof(uint16_t);
@@ -528,6 +712,19 @@ extern "C" int pcfm_conv3d_igemm_cl(const void* xs, const void* wsplit, const fl
   const uint16_t* xl = xh + (size_t)b * V * cin;
   hipStream_t st = (hipStream_t)stream;
   const long long big_blocks = (long long)(V / 128) * (cout / 128) * b;
+#ifndef PCFM_CONV_NOGLDS
+  const long long glds_blocks = (long long)(V / kGN) * (cout / kGM) * b;
+  if (V % kGN == 0 && V >= 4096 && cout % kGM == 0) {  // r >= 16 (r = 8: 64x64 tiles)
+    const uint16_t* zrow = zero_row();  // 64 B of zeros: the padding row
+    if (zrow == nullptr) {
+      set_error("conv3d_igemm_cl: zero-row allocation failed");
+      return (int)hipErrorOutOfMemory;
+    }
+    hipLaunchKernelGGL(conv3_igemm_glds_kernel, dim3((unsigned)glds_blocks), dim3(512), 0, st, xh,
+                       xl, wh, wh + total, zrow, bias, y, cin, cout, r);
+    return check_launch("conv3d_igemm_cl");
+  }
+#endif
   if (big_blocks >= 2 * kCUs) {
     hipLaunchKernelGGL((conv3_igemm_cl_kernel<128, 128, PCFM_CONV_KT>),
                        dim3((V / 128) * (cout / 128) * b), dim3(256), 0, st, xh, xl, wh, wh + total,
