@@ -216,8 +216,11 @@ def main():
                         "frac": achieved / BF16_DENSE_TF, "traffic": None,
                         "algorithmic_flops_per_launch": d["amount"] / d["launches"],
                         "avg_launch_ms": d["ms"] / d["launches"]}
+            traffic = measured_traffic(op)
             return {"kernel": op, "bound": "mfma", "achieved": achieved, "peak": BF16X3_PEAK_TF,
-                    "unit": "TFLOP/s", "frac": achieved / BF16X3_PEAK_TF, "traffic": None,
+                    "unit": "TFLOP/s", "frac": achieved / BF16X3_PEAK_TF, "traffic": traffic,
+                    "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE + WRITE_SIZE, "
+                                    "profiles/r01_traffic.json)" if traffic else None,
                     "note": "achieved = algorithmic fp32 conv FLOPs / time; each is 3 bf16 "
                             "MFMA products, so peak = dense bf16 2500 TF / 3; raw bf16 MFMA "
                             f"utilisation = {3 * achieved / BF16_DENSE_TF:.3f}",

@@ -1,4 +1,6 @@
-"""HBM traffic per launch of the four PVConv voxel ops at the bench's stage
+"""HBM traffic per launch of the four PVConv voxel ops and the three voxel-conv
+GEMMs (forward, backward-data, weight gradient; split operands as the train
+step runs them) at the bench's stage
 shapes, from rocprofv3 PMC counters (MI355X_MICROARCH.md, HBM section).
 
 Two passes, one counter each (FETCH_SIZE and WRITE_SIZE cannot share a pass):
@@ -28,7 +30,7 @@ sys.path[:0] = [REPO, os.path.join(REPO, "point-cloud-flow-matching_amd")]
 B, N, K = 8, 20000, 5
 STAGES = [(128, 32), (256, 16), (256, 8)]
 OPS = ["avg_voxelize_fwd", "avg_voxelize_bwd", "trilinear_devoxelize_fwd",
-       "trilinear_devoxelize_bwd"]
+       "trilinear_devoxelize_bwd", "conv3d_fwd", "conv3d_bwd_data", "conv3d_wgrad"]
 
 
 def run():
@@ -49,7 +51,14 @@ def run():
         grid = torch.randn(B, c, r ** 3, device="cuda", generator=g)
         _, ind, cnt = ops.avg_voxelize_forward(feat, vc, r)
         _, inds, wgts = ops.trilinear_devoxelize_forward(r, True, nc, grid)
+        vg = torch.randn(B, c, r, r, r, device="cuda", generator=g)
+        wt = torch.randn(c, c, 3, 3, 3, device="cuda", generator=g) * (1.0 / (27 * c) ** 0.5)
+        xs, gys = ops.conv3d_split(vg), ops.conv3d_split(vg * 0.5)
+        img_f, img_b = ops.conv3d_prep_weight(wt, False), ops.conv3d_prep_weight(wt, True)
         calls = {
+            "conv3d_fwd": lambda: ops.conv3d_igemm_split(xs, img_f, None, B, c, c, r, "f"),
+            "conv3d_bwd_data": lambda: ops.conv3d_igemm_split(gys, img_b, None, B, c, c, r, "b"),
+            "conv3d_wgrad": lambda: ops.conv3d_wgrad_split(xs, gys, B, c, c, r),
             "avg_voxelize_fwd": lambda: ops.avg_voxelize_forward(feat, vc, r),
             "avg_voxelize_bwd": lambda: ops.avg_voxelize_backward(grid, ind, cnt),
             "trilinear_devoxelize_fwd": lambda: ops.trilinear_devoxelize_forward(r, True, nc, grid),
@@ -96,19 +105,20 @@ def _segments(rows):
 
 def summarize(dfetch, dwrite):
     fetch, write = _segments(_rows(dfetch)), _segments(_rows(dwrite))
-    # calibration: seg_transpose reads exactly B*C*N*4 bytes per launch
+    # calibration: seg_rows (the channels-last copy of the segment sum) reads the
+    # (B, C, N) input once: B*C*N*4 bytes per launch (+ small rank/key arrays)
     labels = [(c, r, op) for c, r in STAGES for op in OPS]
     res, calib = {}, []
     for (c, r, op), fs, ws in zip(labels, fetch, write):
         for name, val in fs:
-            if "seg_transpose" in name:
+            if "seg_rows" in name:
                 calib.append(B * c * N * 4 / val)
     corr = sum(calib) / len(calib) if calib else 2.0
     for (c, r, op), fs, ws in zip(labels, fetch, write):
         fb = sum(v for _, v in fs) / K * corr
         wb = sum(v for _, v in ws) / K
         res[f"{op}@C{c}R{r}"] = {"fetch_bytes": fb, "write_bytes": wb, "traffic_bytes": fb + wb}
-    return {"fetch_correction": corr, "calibration": "seg_transpose reads B*C*N*4 bytes",
+    return {"fetch_correction": corr, "calibration": "seg_rows reads B*C*N*4 bytes",
             "shapes": f"B={B} N={N} randn coords through Voxelization normalisation",
             "ops": res}
 
