@@ -37,7 +37,8 @@ extern "C" {
 
 /* ABI version: bumped on any signature change (4: voxel and pointwise convolution;
  * 5: per-point head kernels; 6: conv3d_igemm workspace,
- * split-operand convolution entry points; fused BatchNorm + activation). */
+ * split-operand convolution entry points; fused BatchNorm + activation;
+ * 7: channel-segmented pointwise GEMMs, SE3d folded into the devoxelization). */
 int pcfm_abi_version(void);
 /* Thread-local text of the last non-zero return code. */
 const char* pcfm_last_error(void);
@@ -77,6 +78,23 @@ int pcfm_avg_voxelize_bwd(const float* grad_y, const int* ind, const int* cnt, i
 int pcfm_trilinear_devoxelize_fwd(const float* coords, const float* feat, int b, int c,
                                   int n, int r, int training, float* out, int* inds,
                                   float* wgts, void* stream);
+
+/* out = scale[b, c] * devox(feat)[b, c, i] + add[b, c, i] (either may be NULL):
+ * SE3d (modules/se.py:6-17) and the point-branch sum of PVConv.forward
+ * (pvconv.py:35-39) folded into the devoxelization; inds/wgts as above. */
+int pcfm_trilinear_devoxelize_scale_add_fwd(const float* coords, const float* feat,
+                                            const float* scale, const float* add, int b, int c,
+                                            int n, int r, int training, float* out, int* inds,
+                                            float* wgts, void* stream);
+
+/* out[r] = scale * sum_v a[r][v] * b[r][v] (b NULL: plain row sum), rows of
+ * `len` floats; deterministic.  (SE3d pooling and its scale gradient.) */
+int pcfm_rows_dot(const float* a, const float* b, long long rows, int len, float scale,
+                  float* out, void* stream);
+
+/* x[r][v] = s[r] * x[r][v] + t[r] in place (t may be NULL); len % 4 == 0. */
+int pcfm_rows_affine(float* x, const float* s, const float* t, long long rows, int len,
+                     void* stream);
 
 size_t pcfm_trilinear_devoxelize_bwd_workspace_bytes(int b, int c, int n, int r);
 
@@ -254,6 +272,23 @@ size_t pcfm_pointwise_wgrad_workspace_bytes(int b, int cin, int cout, int n);
 /* grad_w f32 [cout][cin] = sum_{b, p} grad_y[b, co, p] * x[b, ci, p]; fully written. */
 int pcfm_pointwise_wgrad(const float* x, const float* grad_y, int b, int cin, int cout, int n,
                          float* grad_w, void* ws, size_t ws_bytes, void* stream);
+
+/* Channel-segmented variants (ContextNet's head_pre over the channel concat of
+ * the stage outputs, models.py:460-466, read in place instead of torch.cat).
+ * Input part i is an f32 (b, xw[i], n) tensor holding channels
+ * [sum xw[<i], sum xw[<=i]) of the logical input; 1..4 parts, every width but
+ * the last a multiple of 32.  Output parts likewise, widths a multiple of 128.
+ * bias_per_batch = 1: bias is f32 [b][cout] (a per-cloud bias, e.g. the
+ * global-feature columns of the weight applied to the broadcast feature). */
+int pcfm_pointwise_gemm_parts(int nx, const float* const* x, const int* xw, const void* wsplit,
+                              const float* bias, int bias_per_batch, int b, int n, int ny,
+                              float* const* y, const int* yw, void* stream);
+
+/* grad_w f32 [cout][sum xw] over a segmented x (any part widths); workspace
+ * as pcfm_pointwise_wgrad_workspace_bytes(b, sum xw, cout, n). */
+int pcfm_pointwise_wgrad_parts(int nx, const float* const* x, const int* xw, const float* grad_y,
+                               int b, int cout, int n, float* grad_w, void* ws, size_t ws_bytes,
+                               void* stream);
 
 /* ------------------------------------------------------------------------
  * Per-point head (models.py:62-153, 546-601: the Linear layers of

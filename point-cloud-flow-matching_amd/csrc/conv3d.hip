@@ -502,10 +502,21 @@ __global__ void __launch_bounds__(256)
   }
   __syncthreads();
   for (long long ks = k0; ks < k1; ++ks) {
+#ifndef PCFM_EXP_WG_NOLOAD
     if (ks + 1 < k1) load(ks + 1);
+#endif
 #pragma unroll
     for (int kk = 0; kk < kWV / 16; ++kk) {
       bf16x8 ah[2], al[2], bh[2], bl[2];
+#ifdef PCFM_EXP_WG_NOLDSREAD
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        ah[i] = __builtin_bit_cast(bf16x8, sv_get<4>(rah, i));
+        al[i] = __builtin_bit_cast(bf16x8, sv_get<4>(ral, i));
+        bh[i] = __builtin_bit_cast(bf16x8, sv_get<4>(rbh, i));
+        bl[i] = __builtin_bit_cast(bf16x8, sv_get<4>(rbl, i));
+      }
+#else
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         ah[i] = tr_operand(iAh, kk, wr * 64 + i * 32, lane);
@@ -515,6 +526,215 @@ __global__ void __launch_bounds__(256)
       for (int j = 0; j < 2; ++j) {
         bh[j] = tr_operand(iBh, kk, wc * 64 + j * 32, lane);
         bl[j] = tr_operand(iBl, kk, wc * 64 + j * 32, lane);
+      }
+#endif
+#ifdef PCFM_EXP_WG_NOMFMA
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j][kk] += (float)ah[i][kk] + (float)bh[j][kk] + (float)al[i][kk] + (float)bl[j][kk];
+      continue;
+#endif
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
+    }
+#ifndef PCFM_EXP_WG_NOLOAD
+    __syncthreads();
+    if (ks + 1 < k1) store();
+    __syncthreads();
+#endif
+  }
+  float* pb = part + ((size_t)sp * 27 + tap) * cout * cin;
+  const int h = lane >> 5, r = lane & 31;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int co = co0 + wr * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+        const int ci = ci0 + wc * 64 + j * 32 + r;
+        pb[(size_t)co * cin + ci] = acc[i][j][e];
+      }
+}
+
+// ---------------------------------------------------------------------------
+// Weight gradient, three taps per block.  The three taps (dx, dy, dz = -1..1)
+// of one (dx, dy) read the SAME dY rows and X rows shifted by one voxel, so a
+// block stages dY[v0, v0 + 64) and X[v0 + off - 1, v0 + off + 65) once (66
+// rows: the z halo) and its 12 waves -- (dz, 64x64 quadrant) each -- read their
+// X operand at row offset 1 + dz.  Global loads and LDS writes per tap drop 3x
+// against conv3_wgrad_cl_kernel.  A voxel whose tap leaves the volume has its
+// X operand elements zeroed in registers: a lane's 8 K-elements are 8
+// consecutive voxels of one z-row (R % 8 == 0), so only x/y validity and the
+// first / last element for dz = -1 / +1 matter.  Double-buffered LDS (2 x 65
+// KiB), one barrier per step; partials in conv3_wgrad_cl_kernel's layout.
+// ---------------------------------------------------------------------------
+constexpr int kW3Threads = 768;
+constexpr int kW3ARows = kWV;                       // dY rows per step
+constexpr int kW3BRows = kWV + 4;                   // X rows: z halo (66), padded to 4-row pieces
+constexpr int kW3AImg = kW3ARows * 256;             // bytes of one hi/lo image
+constexpr int kW3BImg = kW3BRows * 256;
+constexpr int kW3Buf = 2 * kW3AImg + 2 * kW3BImg;   // Ah | Al | Bh | Bl
+constexpr int kW3APieces = kW3ARows / 4, kW3BPieces = kW3BRows / 4;  // 1-KiB LDS-DMA pieces
+constexpr int kW3Pieces = 2 * kW3APieces + 2 * kW3BPieces;           // 66 per step
+constexpr int kW3Q = (kW3Pieces + kW3Threads / 64 - 1) / (kW3Threads / 64);
+
+// tr_operand with an arbitrary first row (row0 + 8 * (lane / 32) ...)
+__device__ __forceinline__ bf16x8 tr_operand_rows(const uint8_t* img, int row0, int col0,
+                                                  int lane) {
+  const int g = lane >> 4, i16 = lane & 15, q4 = i16 >> 2, p4 = i16 & 3;
+  const int row = row0 + 8 * (g >> 1) + q4;
+  const int col = col0 + (g & 1) * 16 + 4 * p4;
+  const v4s_tr x0 = tr_read16(img, swz256(row, col >> 3) + 8 * (p4 & 1));
+  const v4s_tr x1 = tr_read16(img, swz256(row + 4, col >> 3) + 8 * (p4 & 1));
+  return __builtin_bit_cast(bf16x8, __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+
+// LDS-DMA as inline asm: hipcc does not see it, so it inserts no vmcnt(0)
+// before the step's LDS reads (it does for __builtin_amdgcn_global_load_lds
+// here, which serialises the prefetch with the compute); completion is waited
+// for by hand.  M0 is set and restored inside the statement.
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+__device__ __forceinline__ void glds16_asm(const void* g, uint32_t lds) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(g), "s"(lds)
+      : "memory");
+}
+
+__device__ __forceinline__ bf16x8 mask_k8(bf16x8 v, uint32_t m0, uint32_t m12, uint32_t m3) {
+  uint4 u = __builtin_bit_cast(uint4, v);
+  u.x &= m0;
+  u.y &= m12;
+  u.z &= m12;
+  u.w &= m3;
+  return __builtin_bit_cast(bf16x8, u);
+}
+
+__global__ void __launch_bounds__(kW3Threads)
+    conv3_wgrad3_kernel(const uint16_t* __restrict__ xh, const uint16_t* __restrict__ xl,
+                        const uint16_t* __restrict__ gh, const uint16_t* __restrict__ gl,
+                        int B, int cin, int cout, int R, int S, float* __restrict__ part) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int V = R * R * R, R2 = R * R;
+  const int nco = cout / kMT;
+  int id = (int)blockIdx.x;
+  {
+    const int nwg = (int)gridDim.x, q = nwg / 8, rr = nwg % 8, xcd = id % 8;
+    id = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + id / 8;
+  }
+  const int pair = id % 9;
+  id /= 9;
+  const int sp = id % S;
+  id /= S;
+  const int co0 = (id % nco) * kMT;
+  const int ci0 = (id / nco) * kMT;
+  const long long nsteps = (long long)B * V / kWV;
+  const long long k0 = nsteps * sp / S, k1 = nsteps * (sp + 1) / S;
+  const int dx = pair / 3 - 1, dy_ = pair % 3 - 1;
+  const int off = dx * R2 + dy_ * R;
+
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);  // 0..11
+  const int dz = w / 4 - 1;
+  const int wr = (w >> 1) & 1, wc = w & 1;
+  const int h = lane >> 5;
+
+  // LDS-DMA pieces of this wave: I = w + 12 q; lane -> (row 4P + lane / 16,
+  // physical chunk lane % 16 = logical chunk ^ swizzle): the swz256 image is
+  // produced by choosing the source chunk.
+  auto issue = [&](int b, int v0, uint8_t* buf) {
+    const size_t base = (size_t)b * V;
+#pragma unroll
+    for (int q = 0; q < kW3Q; ++q) {
+      const int I = w + (kW3Threads / 64) * q;
+      if (I < 2 * kW3APieces) {
+        const int img = I / kW3APieces, P = I % kW3APieces;
+        const int row = 4 * P + (lane >> 4);
+        const int ch = (lane & 15) ^ (((row & 3) << 2) | ((row >> 2) & 3));
+        const uint16_t* src = (img ? gl : gh) + (base + v0 + row) * cout + co0 + ch * 8;
+        glds16_asm(src, lds_addr(buf + img * kW3AImg + P * 1024));
+      } else if (I < kW3Pieces) {
+        const int I2 = I - 2 * kW3APieces;
+        const int img = I2 / kW3BPieces, P = I2 % kW3BPieces;
+        const int row = 4 * P + (lane >> 4);
+        const int ch = (lane & 15) ^ (((row & 3) << 2) | ((row >> 2) & 3));
+        int gv = v0 + off - 1 + row;
+        gv = gv < 0 ? 0 : (gv >= V ? V - 1 : gv);  // out-of-volume rows are masked at use
+        const uint16_t* src = (img ? xl : xh) + (base + gv) * cin + ci0 + ch * 8;
+        glds16_asm(src, lds_addr(buf + 2 * kW3AImg + img * kW3BImg + P * 1024));
+      }
+    }
+  };
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
+
+  // (batch, first voxel) of the current step, advanced incrementally (V % 64 == 0)
+  int cb = (int)(k0 * kWV / V), cv0 = (int)(k0 * kWV - (long long)cb * V);
+  const int lgR = 31 - __builtin_clz(R);  // R is a power of two here
+  if (k0 < k1) issue(cb, cv0, lds);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const int nst = (int)(k1 - k0);
+  for (int st = 0; st < nst; ++st) {
+    __builtin_amdgcn_s_barrier();  // step st landed everywhere; step st-1 reads done
+    const uint8_t* cur = lds + (st & 1) * kW3Buf;
+    const int v0 = cv0;
+    cv0 += kWV;
+    if (cv0 == V) cv0 = 0, ++cb;
+#ifndef PCFM_EXP_WG_NOLOAD
+    if (st + 1 < nst) issue(cb, cv0, lds + ((st + 1) & 1) * kW3Buf);
+#endif
+    const uint8_t* iAh = cur;
+    const uint8_t* iAl = cur + kW3AImg;
+    const uint8_t* iBh = cur + 2 * kW3AImg;
+    const uint8_t* iBl = iBh + kW3BImg;
+#pragma unroll
+    for (int kk = 0; kk < kWV / 16; ++kk) {
+      // validity of this lane's 8 voxels for tap (dx, dy, dz)
+      const int vk = v0 + kk * 16 + 8 * h;
+      const int xq = vk >> (2 * lgR), yq = (vk >> lgR) & (R - 1), z0 = vk & (R - 1);
+      const bool xyok = (unsigned)(xq + dx) < (unsigned)R && (unsigned)(yq + dy_) < (unsigned)R;
+      const uint32_t mall = xyok ? 0xFFFFFFFFu : 0u;
+      const uint32_t m0 = (dz < 0 && z0 == 0) ? (mall & 0xFFFF0000u) : mall;
+      const uint32_t m3 = (dz > 0 && z0 + 8 == R) ? (mall & 0x0000FFFFu) : mall;
+      bf16x8 ah[2], al[2], bh[2], bl[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        ah[i] = tr_operand_rows(iAh, kk * 16, wr * 64 + i * 32, lane);
+        al[i] = tr_operand_rows(iAl, kk * 16, wr * 64 + i * 32, lane);
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        bh[j] = mask_k8(tr_operand_rows(iBh, kk * 16 + 1 + dz, wc * 64 + j * 32, lane), m0, mall,
+                        m3);
+        bl[j] = mask_k8(tr_operand_rows(iBl, kk * 16 + 1 + dz, wc * 64 + j * 32, lane), m0, mall,
+                        m3);
       }
 #pragma unroll
       for (int i = 0; i < 2; ++i)
@@ -532,12 +752,12 @@ __global__ void __launch_bounds__(256)
         for (int j = 0; j < 2; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
     }
-    __syncthreads();
-    if (ks + 1 < k1) store();
-    __syncthreads();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // step ks+1 landed (this wave's pieces)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
+  const int tap = pair * 3 + (dz + 1);
   float* pb = part + ((size_t)sp * 27 + tap) * cout * cin;
-  const int h = lane >> 5, r = lane & 31;
+  const int r = lane & 31;
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -578,7 +798,36 @@ __global__ void __launch_bounds__(256)
 #ifndef PCFM_WGRAD_OCC
 #define PCFM_WGRAD_OCC 4
 #endif
+#ifndef PCFM_WGRAD3_BLOCKS
+#define PCFM_WGRAD3_BLOCKS 2  // blocks per CU the three-tap split aims for
+#endif
+bool conv3_wgrad3_ok(int R) {
+#ifdef PCFM_WGRAD_NO3
+  return false;
+#else
+  return R >= 8 && (R & (R - 1)) == 0;  // 8-voxel z runs, shift-decoded voxel index
+#endif
+}
+
 int conv3_wgrad_splits(int B, int cin, int cout, int R) {
+  if (conv3_wgrad3_ok(R)) {
+    // one 768-thread block per CU: pick the split minimising
+    // (rounds of blocks over the CUs) x (K-steps per block), i.e. no lone tail round
+    const long long items = 9LL * (cout / kMT) * (cin / kMT);
+    const long long steps = (long long)B * R * R * R / kWV;
+    const long long smax = std::min(64LL, std::max(1LL, steps / 8));
+    // model: ~4 us per K-step; each split adds its partial (27 cout cin fp32),
+    // written then read by the reduce, at ~5 TB/s
+    const double part_us = 2.0 * 27.0 * cout * cin * 4.0 / 5.0e6;
+    long long best = 1;
+    double best_cost = -1.0;
+    for (long long s = 1; s <= smax; ++s) {
+      const long long rounds = (items * s + kCUs - 1) / kCUs;
+      const double cost = 4.0 * rounds * ((steps + s - 1) / s) + part_us * s;
+      if (best_cost < 0 || cost < best_cost) best = s, best_cost = cost;
+    }
+    return (int)best;
+  }
   const long long tiles = 27LL * (cout / kMT) * (cin / kMT);
   const long long steps = (long long)B * R * R * R / kWV;
   // blocks per CU the split aims for (one block's staging overlaps another's MFMAs)
@@ -750,9 +999,17 @@ extern "C" int pcfm_conv3d_wgrad_cl(const void* xs, const void* gys, int b, int 
   const int tiles = 27 * (cout / kMT) * (cin / kMT);
   const uint16_t* xh = (const uint16_t*)xs;
   const uint16_t* gh = (const uint16_t*)gys;
-  hipLaunchKernelGGL(conv3_wgrad_cl_kernel, dim3(tiles * S), dim3(256), 0, st, xh,
-                     xh + (size_t)b * V * cin, gh, gh + (size_t)b * V * cout, b, cin, cout, r, S,
-                     (float*)ws);
+  if (conv3_wgrad3_ok(r)) {
+    const int e = allow_big_lds((const void*)conv3_wgrad3_kernel);
+    if (e) return e;
+    hipLaunchKernelGGL(conv3_wgrad3_kernel, dim3(tiles / 3 * S), dim3(kW3Threads), 2 * kW3Buf, st,
+                       xh, xh + (size_t)b * V * cin, gh, gh + (size_t)b * V * cout, b, cin, cout, r,
+                       S, (float*)ws);
+  } else {
+    hipLaunchKernelGGL(conv3_wgrad_cl_kernel, dim3(tiles * S), dim3(256), 0, st, xh,
+                       xh + (size_t)b * V * cin, gh, gh + (size_t)b * V * cout, b, cin, cout, r, S,
+                       (float*)ws);
+  }
   const size_t total = (size_t)27 * cout * cin;
   hipLaunchKernelGGL(conv3_wgrad_reduce_kernel, dim3(ceil_div((long long)total, 256)), dim3(256),
                      0, st, (const float*)ws, cout, cin, S, grad_w);

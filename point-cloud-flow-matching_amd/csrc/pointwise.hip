@@ -16,6 +16,32 @@ namespace {
 
 inline int pad_to(int x, int m) { return (x + m - 1) / m * m; }
 
+// A channel-segmented (B, C, N) tensor: channels [off[i], off[i+1]) live in
+// their own (B, off[i+1] - off[i], N) tensor p[i] -- ContextNet's head input
+// is the channel concat of the stage outputs, read in place instead of copied.
+// Segment boundaries are multiples of 32 (inputs) / 128 (outputs).
+constexpr int kMaxParts = 4;
+struct Parts {
+  float* p[kMaxParts];
+  int off[kMaxParts + 1];
+  int n;
+  __device__ __forceinline__ float* row(int b, int c, int N) const {
+    int i = 0;
+#pragma unroll
+    for (int k = 1; k < kMaxParts; ++k) i += (k < n && c >= off[k]) ? 1 : 0;
+    const int w = off[i + 1] - off[i];
+    return p[i] + ((size_t)b * w + (c - off[i])) * N;
+  }
+};
+inline Parts one_part(const float* x, int c) {
+  Parts q{};
+  q.p[0] = const_cast<float*>(x);
+  q.off[0] = 0;
+  q.off[1] = c;
+  q.n = 1;
+  return q;
+}
+
 // W [cout][cin] -> image [Mpad][Kpad] bf16 hi, lo; transpose: [cin][cout]
 __global__ void __launch_bounds__(256)
     pw_wsplit_kernel(const float* __restrict__ w, int cout, int cin, int transpose, int Mpad,
@@ -36,19 +62,18 @@ __global__ void __launch_bounds__(256)
 // grid = (ceil(N / TN), Mpad / TM, B), 256 threads.
 template <int TM, int TN>
 __global__ void __launch_bounds__(256)
-    pw_gemm_kernel(const float* __restrict__ x, const uint16_t* __restrict__ wh,
-                   const uint16_t* __restrict__ wl, const float* __restrict__ bias,
-                   float* __restrict__ y, int K, int M, int N, int Kpad) {
+    pw_gemm_kernel(const Parts x, const uint16_t* __restrict__ wh,
+                   const uint16_t* __restrict__ wl, const float* __restrict__ bias, int bias_bstride,
+                   const Parts y, int K, int M, int N, int Kpad) {
   using T = Tile<TM, TN>;
   __shared__ __attribute__((aligned(16))) uint16_t lds[T::BUF];
   const int b = blockIdx.z, m0 = blockIdx.y * TM, p0 = blockIdx.x * TN;
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   const int wr = w >> 1, wc = w & 1, r = lane & 31, h = lane >> 5;
-  const float* __restrict__ xb = x + (size_t)b * K * N;
-
   constexpr int CPT = kKT * TN / 256;  // channels per thread per K-step
-  const int sp = t % TN, ch = (t / TN) * CPT;
+  // TN >= 64: a wave's threads share one channel group (uniform -> SGPR row pointers)
+  const int sp = t % TN, ch = __builtin_amdgcn_readfirstlane((t / TN) * CPT);
   const int pt = p0 + sp;
   const bool pok = pt < N;
   const int ptc = pok ? pt : N - 1;  // clamped: always a valid address
@@ -69,11 +94,14 @@ __global__ void __launch_bounds__(256)
       ra3 = *reinterpret_cast<const uint4*>(wl + g + 8);
     }
     rmask = 0u;
+    // the CPT channels are consecutive and inside one part (parts are 32-aligned)
+    const int cb = min(c0 + ch, K - 1);
+    const float* __restrict__ xr = x.row(b, cb, N);
 #pragma unroll
     for (int q = 0; q < CPT; ++q) {
       const int c = c0 + ch + q;
       const bool ok = pok && c < K;
-      rb[q] = xb[(size_t)(c < K ? c : K - 1) * N + ptc];
+      rb[q] = xr[(size_t)(c < K ? c - cb : 0) * N + ptc];
       rmask |= ok ? 0u : (1u << q);
     }
   };
@@ -110,24 +138,28 @@ __global__ void __launch_bounds__(256)
     if (s + 1 < nsteps) store(lds);
     __syncthreads();
   }
-  float* __restrict__ yb = y + (size_t)b * M * N;
+  const int bo = b * bias_bstride;  // per-cloud bias row (0: one shared bias)
 #pragma unroll
-  for (int i = 0; i < T::SI; ++i)
+  for (int i = 0; i < T::SI; ++i) {
+    // a 32-row group lies inside one output part (parts are 128-aligned)
+    const int mg = m0 + wr * (TM / 2) + i * 32;
+    float* __restrict__ yr = y.row(b, min(mg, M - 1), N);
 #pragma unroll
     for (int j = 0; j < T::SJ; ++j)
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
-        const int m = m0 + wr * (TM / 2) + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+        const int dm = (e & 3) + 8 * (e >> 2) + 4 * h;
+        const int m = mg + dm;
         const int p = p0 + wc * (TN / 2) + j * 32 + r;
-        if (m < M && p < N)
-          yb[(size_t)m * N + p] = acc[i][j][e] + (bias != nullptr ? bias[m] : 0.0f);
+        if (m < M && p < N) yr[(size_t)dm * N + p] = acc[i][j][e] + (bias != nullptr ? bias[bo + m] : 0.0f);
       }
+  }
 }
 
 // dW partials: grid = (ceil(Cout/128) * ceil(Cin/128), S); K-steps of 32
 // points (a step never crosses a batch element).  part [S][Cout][Cin].
 __global__ void __launch_bounds__(256)
-    pw_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ dy, int B, int cin,
+    pw_wgrad_kernel(const Parts x, const float* __restrict__ dy, int B, int cin,
                     int cout, int N, int S, float* __restrict__ part) {
   using T = Tile<128, 128>;
   __shared__ __attribute__((aligned(16))) uint16_t lds[T::BUF];
@@ -145,6 +177,9 @@ __global__ void __launch_bounds__(256)
   const bool cook = co < cout, ciok = ci < cin;
   const int coc = cook ? co : cout - 1, cic = ciok ? ci : cin - 1;
   const bool vec = (N & 3) == 0;  // rows 16-B aligned (the runs start at multiples of 16)
+  // this thread's x row of batch 0 and the batch stride of its part
+  const float* __restrict__ xrow = x.row(0, cic, N);
+  const size_t xbstride = (size_t)(x.row(1, cic, N) - xrow);
 
   float ra[16], rb[16];
   uint32_t amask = 0u, bmask = 0u;
@@ -152,7 +187,7 @@ __global__ void __launch_bounds__(256)
     const int b = (int)(ks / steps_per_b);
     const int p0 = (int)(ks - (long long)b * steps_per_b) * kKT + shalf;
     const float* as = dy + ((size_t)b * cout + coc) * N;
-    const float* bs = x + ((size_t)b * cin + cic) * N;
+    const float* bs = xrow + (size_t)b * xbstride;
     amask = cook ? 0u : 0xFFFFu;
     bmask = ciok ? 0u : 0xFFFFu;
     if (vec && p0 + 16 <= N) {  // whole 16-point run: four 16-B loads per operand
@@ -275,24 +310,78 @@ extern "C" int pcfm_pointwise_prep_weight(const float* w, int cout, int cin, int
   return check_launch("pointwise_prep_weight");
 }
 
+static int pw_gemm_launch(const Parts& x, const void* wsplit, const float* bias, int bias_bstride,
+                          int b, int cin, int cout, int n, const Parts& y, hipStream_t st) {
+  const int Mpad = pad_to(cout, 128), Kpad = pad_to(cin, kKT);
+  const size_t total = (size_t)Mpad * Kpad;
+  const uint16_t* wh = (const uint16_t*)wsplit;
+  const long long big = (long long)ceil_div(n, 128) * (Mpad / 128) * b;
+  if (big >= 2 * kCUs) {
+    hipLaunchKernelGGL((pw_gemm_kernel<128, 128>), dim3(ceil_div(n, 128), Mpad / 128, b),
+                       dim3(256), 0, st, x, wh, wh + total, bias, bias_bstride, y, cin, cout, n,
+                       Kpad);
+  } else {
+    hipLaunchKernelGGL((pw_gemm_kernel<64, 64>), dim3(ceil_div(n, 64), Mpad / 64, b), dim3(256),
+                       0, st, x, wh, wh + total, bias, bias_bstride, y, cin, cout, n, Kpad);
+  }
+  return check_launch("pointwise_gemm");
+}
+
+// host arrays -> Parts; every width a multiple of `align` (the last may be ragged)
+static bool make_parts(int np, float* const* ptr, const int* width, int align, Parts& q,
+                       int& total) {
+  if (np < 1 || np > kMaxParts || ptr == nullptr || width == nullptr) return false;
+  q = Parts{};
+  q.n = np;
+  total = 0;
+  for (int i = 0; i < np; ++i) {
+    if (width[i] <= 0 || ptr[i] == nullptr) return false;
+    if (i + 1 < np && width[i] % align != 0) return false;
+    q.p[i] = ptr[i];
+    q.off[i] = total;
+    total += width[i];
+  }
+  q.off[np] = total;
+  for (int i = np + 1; i <= kMaxParts; ++i) q.off[i] = total;
+  return true;
+}
+
 extern "C" int pcfm_pointwise_gemm(const float* x, const void* wsplit, const float* bias, int b,
                                    int cin, int cout, int n, float* y, void* stream) {
   PCFM_CHECK_ARG(pw_ok(b, cin, cout, n), "pointwise_gemm: bad shape b=%d cin=%d cout=%d n=%d", b,
                  cin, cout, n);
   if (b == 0 || n == 0) return PCFM_OK;
-  const int Mpad = pad_to(cout, 128), Kpad = pad_to(cin, kKT);
-  const size_t total = (size_t)Mpad * Kpad;
-  const uint16_t* wh = (const uint16_t*)wsplit;
-  hipStream_t st = (hipStream_t)stream;
-  const long long big = (long long)ceil_div(n, 128) * (Mpad / 128) * b;
-  if (big >= 2 * kCUs) {
-    hipLaunchKernelGGL((pw_gemm_kernel<128, 128>), dim3(ceil_div(n, 128), Mpad / 128, b),
-                       dim3(256), 0, st, x, wh, wh + total, bias, y, cin, cout, n, Kpad);
-  } else {
-    hipLaunchKernelGGL((pw_gemm_kernel<64, 64>), dim3(ceil_div(n, 64), Mpad / 64, b), dim3(256),
-                       0, st, x, wh, wh + total, bias, y, cin, cout, n, Kpad);
-  }
-  return check_launch("pointwise_gemm");
+  return pw_gemm_launch(one_part(x, cin), wsplit, bias, 0, b, cin, cout, n, one_part(y, cout),
+                        (hipStream_t)stream);
+}
+
+extern "C" int pcfm_pointwise_gemm_parts(int nx, const float* const* x, const int* xw,
+                                         const void* wsplit, const float* bias, int bias_per_batch,
+                                         int b, int n, int ny, float* const* y, const int* yw,
+                                         void* stream) {
+  Parts px, py;
+  int cin = 0, cout = 0;
+  PCFM_CHECK_ARG(make_parts(nx, const_cast<float* const*>(x), xw, kKT, px, cin),
+                 "pointwise_gemm_parts: bad input parts (1..%d, widths %% %d)", kMaxParts, kKT);
+  PCFM_CHECK_ARG(make_parts(ny, y, yw, 128, py, cout),
+                 "pointwise_gemm_parts: bad output parts (1..%d, widths %% 128)", kMaxParts);
+  PCFM_CHECK_ARG(pw_ok(b, cin, cout, n), "pointwise_gemm_parts: bad shape b=%d cin=%d cout=%d n=%d",
+                 b, cin, cout, n);
+  if (b == 0 || n == 0) return PCFM_OK;
+  return pw_gemm_launch(px, wsplit, bias, bias_per_batch ? cout : 0, b, cin, cout, n, py,
+                        (hipStream_t)stream);
+}
+
+static int pw_wgrad_launch(const Parts& x, const float* grad_y, int b, int cin, int cout, int n,
+                           float* grad_w, void* ws, hipStream_t st) {
+  const size_t total = (size_t)cout * cin;
+  const int S = pw_wgrad_splits(b, cin, cout, n);
+  const int tiles = ((cout + 127) / 128) * ((cin + 127) / 128);
+  hipLaunchKernelGGL(pw_wgrad_kernel, dim3(tiles, S), dim3(256), 0, st, x, grad_y, b, cin, cout,
+                     n, S, (float*)ws);
+  hipLaunchKernelGGL(pw_wgrad_reduce_kernel, dim3(ceil_div((long long)total, 256)), dim3(256), 0,
+                     st, (const float*)ws, total, S, grad_w);
+  return check_launch("pointwise_wgrad");
 }
 
 extern "C" size_t pcfm_pointwise_wgrad_workspace_bytes(int b, int cin, int cout, int n) {
@@ -317,11 +406,20 @@ extern "C" int pcfm_pointwise_wgrad(const float* x, const float* grad_y, int b, 
   }
   const size_t need = pcfm_pointwise_wgrad_workspace_bytes(b, cin, cout, n);
   PCFM_CHECK_ARG(ws_bytes >= need, "pointwise_wgrad: workspace %zu < %zu bytes", ws_bytes, need);
-  const int S = pw_wgrad_splits(b, cin, cout, n);
-  const int tiles = ((cout + 127) / 128) * ((cin + 127) / 128);
-  hipLaunchKernelGGL(pw_wgrad_kernel, dim3(tiles, S), dim3(256), 0, st, x, grad_y, b, cin, cout,
-                     n, S, (float*)ws);
-  hipLaunchKernelGGL(pw_wgrad_reduce_kernel, dim3(ceil_div((long long)total, 256)), dim3(256), 0,
-                     st, (const float*)ws, total, S, grad_w);
-  return check_launch("pointwise_wgrad");
+  return pw_wgrad_launch(one_part(x, cin), grad_y, b, cin, cout, n, grad_w, ws, st);
+}
+
+extern "C" int pcfm_pointwise_wgrad_parts(int nx, const float* const* x, const int* xw,
+                                          const float* grad_y, int b, int cout, int n,
+                                          float* grad_w, void* ws, size_t ws_bytes, void* stream) {
+  Parts px;
+  int cin = 0;
+  PCFM_CHECK_ARG(make_parts(nx, const_cast<float* const*>(x), xw, 1, px, cin),
+                 "pointwise_wgrad_parts: bad input parts (1..%d)", kMaxParts);
+  PCFM_CHECK_ARG(pw_ok(b, cin, cout, n) && b > 0 && n > 0,
+                 "pointwise_wgrad_parts: bad shape b=%d cin=%d cout=%d n=%d", b, cin, cout, n);
+  const size_t need = pcfm_pointwise_wgrad_workspace_bytes(b, cin, cout, n);
+  PCFM_CHECK_ARG(ws_bytes >= need, "pointwise_wgrad_parts: workspace %zu < %zu bytes", ws_bytes,
+                 need);
+  return pw_wgrad_launch(px, grad_y, b, cin, cout, n, grad_w, ws, (hipStream_t)stream);
 }

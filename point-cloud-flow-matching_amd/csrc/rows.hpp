@@ -155,12 +155,20 @@ __device__ __forceinline__ float tap_sum(const float* __restrict__ s, const int 
   }
 }
 
+// Optional epilogue of a gather: out = scale[b, c] * sum + add[b, c, i]
+// (either pointer may be null).  Used to fold a squeeze-excitation channel
+// scale of the rows and the residual point branch into the devoxelization.
+struct GatherEpi {
+  const float* scale = nullptr;  // [B][C]
+  const float* add = nullptr;    // [B][C][NI]
+};
+
 // grid = (item splits, channel groups, b).  USE_LDS stages the block's
 // `cpb` rows (cpb * V floats) in LDS first.
 template <class Prov, bool USE_LDS>
 __global__ void __launch_bounds__(1024)
     gather_rows_kernel(const float* __restrict__ rows, float* __restrict__ out, int C, int V,
-                       int NI, int cpb, Prov prov) {
+                       int NI, int cpb, Prov prov, GatherEpi epi) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   constexpr int T = Prov::TAPS;
   const int b = blockIdx.z;
@@ -183,15 +191,52 @@ __global__ void __launch_bounds__(1024)
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < NI; i += gridDim.x * blockDim.x) {
     int id[T];
     float w[T];
-    prov.get(b, i, primary, id, w);
-    for (int cc = 0; cc < nc; ++cc) {
-      float acc;
-      if constexpr (USE_LDS) {
-        acc = tap_sum<T>(lds + (size_t)cc * V, id, w);
-      } else {
-        acc = tap_sum<T>(rb + (size_t)cc * V, id, w);
+    if (epi.scale == nullptr && epi.add == nullptr) {
+      prov.get(b, i, primary, id, w);
+      for (int cc = 0; cc < nc; ++cc) {
+        float acc;
+        if constexpr (USE_LDS) {
+          acc = tap_sum<T>(lds + (size_t)cc * V, id, w);
+        } else {
+          acc = tap_sum<T>(rb + (size_t)cc * V, id, w);
+        }
+        ob[(size_t)cc * NI + i] = acc;
       }
-      ob[(size_t)cc * NI + i] = acc;
+    } else {
+      // epilogue operands of 4 channels at a time, the first 4 fetched before
+      // the taps so their latency overlaps the index computation
+      const float* __restrict__ ab =
+          epi.add != nullptr ? epi.add + ((size_t)b * C + c0) * NI + i : nullptr;
+      const float* __restrict__ sb = epi.scale != nullptr ? epi.scale + (size_t)b * C + c0 : nullptr;
+      float ad[4], sc[4];
+      auto fetch = [&](int cq) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int cc = min(cq + k, nc - 1);
+          ad[k] = ab != nullptr ? __builtin_nontemporal_load(ab + (size_t)cc * NI) : 0.0f;
+          sc[k] = sb != nullptr ? sb[cc] : 1.0f;
+        }
+      };
+      fetch(0);
+      prov.get(b, i, primary, id, w);
+      for (int cq = 0; cq < nc; cq += 4) {
+        if (cq > 0) fetch(cq);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int cc = cq + k;
+          if (cc < nc) {
+            float acc;
+            if constexpr (USE_LDS) {
+              acc = tap_sum<T>(lds + (size_t)cc * V, id, w);
+            } else {
+              acc = tap_sum<T>(rb + (size_t)cc * V, id, w);
+            }
+            if (sb != nullptr) acc *= sc[k];
+            if (ab != nullptr) acc += ad[k];
+            ob[(size_t)cc * NI + i] = acc;
+          }
+        }
+      }
     }
   }
 }
@@ -331,9 +376,9 @@ inline bool prov_has_side_outputs(const ProvDevox& p) { return p.inds_out != nul
 
 template <class Prov>
 inline int launch_gather(const float* rows, float* out, int B, int C, int V, int NI, Prov prov,
-                         hipStream_t st, const char* what) {
+                         hipStream_t st, const char* what, GatherEpi epi = GatherEpi{}) {
   if (B == 0 || NI == 0) return PCFM_OK;
-  if (V == 0 && C > 0) {  // empty rows: every tap is out of range -> zeros
+  if (V == 0 && C > 0 && epi.add == nullptr) {  // empty rows: every tap is out of range -> zeros
     hipError_t e = hipMemsetAsync(out, 0, (size_t)B * C * NI * sizeof(float), st);
     if (e != hipSuccess) {
       set_error("%s: hipMemsetAsync: %s", what, hipGetErrorString(e));
@@ -347,10 +392,10 @@ inline int launch_gather(const float* rows, float* out, int B, int C, int V, int
     int e = allow_big_lds((const void*)gather_rows_kernel<Prov, true>);
     if (e) return e;
     hipLaunchKernelGGL((gather_rows_kernel<Prov, true>), grid, dim3(p.threads), p.lds_bytes, st,
-                       rows, out, C, V, NI, p.cpb, prov);
+                       rows, out, C, V, NI, p.cpb, prov, epi);
   } else {
     hipLaunchKernelGGL((gather_rows_kernel<Prov, false>), grid, dim3(p.threads), 0, st, rows,
-                       out, C, V, NI, p.cpb, prov);
+                       out, C, V, NI, p.cpb, prov, epi);
   }
   return check_launch(what);
 }

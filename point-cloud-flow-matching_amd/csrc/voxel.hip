@@ -27,6 +27,61 @@ bool cube_fits(int r, int* s) {
   return true;
 }
 
+// out[r] = scale * sum_v a[r][v] * (b ? b[r][v] : 1): one block per row,
+// fixed per-thread order + tree, deterministic.
+__global__ void __launch_bounds__(256)
+    rows_dot_kernel(const float* __restrict__ a, const float* __restrict__ b, int len, float scale,
+                    float* __restrict__ out) {
+  const size_t r = blockIdx.x;
+  const float* ar = a + r * len;
+  const float* br = b != nullptr ? b + r * len : nullptr;
+  float acc = 0.0f;
+  if ((len & 3) == 0) {
+    const float4* a4 = reinterpret_cast<const float4*>(ar);
+    const float4* b4 = reinterpret_cast<const float4*>(br);
+    for (int v = threadIdx.x; v < (len >> 2); v += 256) {
+      const float4 x = a4[v];
+      if (br != nullptr) {
+        const float4 y = b4[v];
+        acc = __builtin_fmaf(x.x, y.x, acc);
+        acc = __builtin_fmaf(x.y, y.y, acc);
+        acc = __builtin_fmaf(x.z, y.z, acc);
+        acc = __builtin_fmaf(x.w, y.w, acc);
+      } else {
+        acc += (x.x + x.y) + (x.z + x.w);
+      }
+    }
+  } else {
+    for (int v = threadIdx.x; v < len; v += 256)
+      acc = br != nullptr ? __builtin_fmaf(ar[v], br[v], acc) : acc + ar[v];
+  }
+  __shared__ float red[256];
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[r] = red[0] * scale;
+}
+
+// x[r][v] = s[r] * x[r][v] + t[r]  (in place; t may be null)
+__global__ void __launch_bounds__(256)
+    rows_affine_kernel(float* __restrict__ x, const float* __restrict__ s,
+                       const float* __restrict__ t, int len4, int per_row_blocks) {
+  const size_t r = blockIdx.x / per_row_blocks;
+  const int v = (blockIdx.x % per_row_blocks) * 256 + threadIdx.x;
+  if (v >= len4) return;
+  const float sv = s[r], tv = t != nullptr ? t[r] : 0.0f;
+  float4* x4 = reinterpret_cast<float4*>(x) + r * len4;
+  float4 q = x4[v];
+  q.x = __builtin_fmaf(sv, q.x, tv);
+  q.y = __builtin_fmaf(sv, q.y, tv);
+  q.z = __builtin_fmaf(sv, q.z, tv);
+  q.w = __builtin_fmaf(sv, q.w, tv);
+  x4[v] = q;
+}
+
 }  // namespace
 }  // namespace pcfm
 
@@ -102,4 +157,50 @@ extern "C" int pcfm_trilinear_devoxelize_bwd(const float* grad_y, const int* ind
   // (trilinear_devox.cu:64-75), so both placements add the same zeros.
   return seg_scatter<8>(grad_y, inds, 8LL * n, false, wgts, r, b, c, n, s, nullptr, grad_x, ws,
                         (hipStream_t)stream, "trilinear_devoxelize_bwd");
+}
+
+// ---------------------------------------------------------------------------
+// SE3d folded into the devoxelization (modules/se.py over pvconv.py:35-39):
+// devox(grid * s) + point branch == s * devox(grid) + point branch, so the
+// scaled grid is never written.  Backward: g = devox_bwd(dout) then
+// d grid = s * g + d mean / V (rows_affine) and d s = sum_v grid * g (rows_dot).
+// ---------------------------------------------------------------------------
+extern "C" int pcfm_trilinear_devoxelize_scale_add_fwd(const float* coords, const float* feat,
+                                                       const float* scale, const float* add,
+                                                       int b, int c, int n, int r, int training,
+                                                       float* out, int* inds, float* wgts,
+                                                       void* stream) {
+  int s = 0;
+  PCFM_CHECK_ARG(b >= 0 && c >= 0 && n >= 0, "trilinear_devoxelize_scale_add_fwd: negative size");
+  PCFM_CHECK_ARG(cube_fits(r, &s), "trilinear_devoxelize_scale_add_fwd: bad resolution %d", r);
+  PCFM_CHECK_ARG(!training || (long long)b * n == 0 || (inds != nullptr && wgts != nullptr),
+                 "trilinear_devoxelize_scale_add_fwd: training needs inds/wgts buffers");
+  ProvDevox prov{coords, n, r, r * r, s, training ? inds : nullptr, training ? wgts : nullptr};
+  GatherEpi epi;
+  epi.scale = scale;
+  epi.add = add;
+  return launch_gather(feat, out, b, c, s, n, prov, (hipStream_t)stream,
+                       "trilinear_devoxelize_scale_add_fwd", epi);
+}
+
+extern "C" int pcfm_rows_dot(const float* a, const float* b, long long rows, int len, float scale,
+                             float* out, void* stream) {
+  PCFM_CHECK_ARG(rows >= 0 && rows < (1LL << 31) && len >= 0, "rows_dot: bad size %lld x %d",
+                 rows, len);
+  if (rows == 0) return PCFM_OK;
+  hipLaunchKernelGGL(rows_dot_kernel, dim3((unsigned)rows), dim3(256), 0, (hipStream_t)stream, a,
+                     b, len, scale, out);
+  return check_launch("rows_dot");
+}
+
+extern "C" int pcfm_rows_affine(float* x, const float* s, const float* t, long long rows, int len,
+                                void* stream) {
+  PCFM_CHECK_ARG(rows >= 0 && len >= 0 && (len & 3) == 0, "rows_affine: bad size %lld x %d",
+                 rows, len);
+  if (rows == 0 || len == 0) return PCFM_OK;
+  const int per = ceil_div(len / 4, 256);
+  PCFM_CHECK_ARG(rows * per < (1LL << 31), "rows_affine: too many rows %lld", rows);
+  hipLaunchKernelGGL(rows_affine_kernel, dim3((unsigned)(rows * per)), dim3(256), 0,
+                     (hipStream_t)stream, x, s, t, len / 4, per);
+  return check_launch("rows_affine");
 }

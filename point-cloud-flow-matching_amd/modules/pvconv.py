@@ -8,7 +8,9 @@ created in the reference's order, so a given torch seed yields the same
 initial weights, and the state_dict keys (voxel_layers.{0,1,3,4,6.fc.*},
 point_features.layers.*) are the reference's.
 """
+import torch
 import torch.nn as nn
+import torch.nn.functional as TF
 
 import modules.functional as F
 from modules.norm_act import conv_bn_act
@@ -26,6 +28,60 @@ def _conv_bn_lrelu(cin, cout, kernel_size):
         nn.BatchNorm3d(cout, eps=1e-4),
         nn.LeakyReLU(0.1, True),
     ]
+
+
+def _se_scale(m, w1, w2):
+    return torch.sigmoid(TF.linear(TF.relu(TF.linear(m, w1)), w2))
+
+
+class _SEDevoxAdd(torch.autograd.Function):
+    """devox(SE3d(grid)) + point branch in one gather (pcfm_trilinear_devoxelize_
+    scale_add_fwd): SE's channel scale is linear in the grid, so it is applied to
+    the devoxelized values, and the SE-scaled grid is never materialised.
+
+    Backward: g = devox_bwd(dout); ds = sum_v grid * g (rows_dot) feeds the SE
+    MLP's gradient; d grid = s * g + d mean / V in place (rows_affine)."""
+
+    @staticmethod
+    def forward(ctx, grid, coords, pf, w1, w2, r, training):
+        from pcfm import ops
+        b, c = grid.shape[0], grid.shape[1]
+        v = grid[0, 0].numel()
+        rows = grid.contiguous().view(b * c, v)
+        m = ops.rows_dot(rows, None, 1.0 / v).view(b, c)
+        s = _se_scale(m, w1, w2).contiguous()
+        out, inds, wgts = ops.trilinear_devoxelize_scale_add(r, training, coords, rows.view(
+            b, c, v), s, pf)
+        if training:
+            ctx.save_for_backward(rows, inds, wgts, m, s, w1, w2)
+            ctx.r, ctx.shape = r, grid.shape
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        from pcfm import ops
+        rows, inds, wgts, m, s, w1, w2 = ctx.saved_tensors
+        dout = dout.contiguous()
+        g = ops.trilinear_devoxelize_backward(dout, inds, wgts, ctx.r).view_as(rows)
+        ds = ops.rows_dot(rows, g, 1.0).view_as(s)
+        with torch.enable_grad():
+            m_ = m.detach().requires_grad_(True)
+            w1_ = w1.detach().requires_grad_(True)
+            w2_ = w2.detach().requires_grad_(True)
+            dm, dw1, dw2 = torch.autograd.grad(_se_scale(m_, w1_, w2_), [m_, w1_, w2_], ds)
+        ops.rows_affine_(g, s.view(-1), (dm / rows.shape[1]).contiguous().view(-1))
+        return g.view(ctx.shape), None, dout, dw1, dw2, None, None
+
+
+def _se_devox_ok(se, grid, pf) -> bool:
+    if not (grid.is_cuda and grid.dtype == torch.float32 and pf.dtype == torch.float32
+            and isinstance(se, SE3d)):
+        return False
+    fc = se.fc
+    return (len(fc) == 4 and isinstance(fc[0], nn.Linear) and fc[0].bias is None
+            and isinstance(fc[1], nn.ReLU) and isinstance(fc[2], nn.Linear)
+            and fc[2].bias is None and isinstance(fc[3], nn.Sigmoid)
+            and grid[0, 0].numel() % 4 == 0 and not torch.is_autocast_enabled("cuda"))
 
 
 class PVConv(nn.Module):
@@ -50,7 +106,14 @@ class PVConv(nn.Module):
         layers = self.voxel_layers  # Conv3d, BN3d, LeakyReLU, Conv3d, BN3d, LeakyReLU[, SE3d]
         grid = conv_bn_act(layers[0], layers[1], grid, layers[2].negative_slope)
         grid = conv_bn_act(layers[3], layers[4], grid, layers[5].negative_slope)
+        pf = self.point_features(features)
+        if (len(layers) > 6 and _se_devox_ok(layers[6], grid, pf)
+                and (self.training or not torch.is_grad_enabled())):
+            fc = layers[6].fc
+            out = _SEDevoxAdd.apply(grid, grid_coords, pf, fc[0].weight, fc[2].weight,
+                                    self.resolution, self.training)
+            return out, coords
         if len(layers) > 6:
             grid = layers[6](grid)
         voxel_branch = F.trilinear_devoxelize(grid, grid_coords, self.resolution, self.training)
-        return voxel_branch + self.point_features(features), coords
+        return voxel_branch + pf, coords

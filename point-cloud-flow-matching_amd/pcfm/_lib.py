@@ -63,6 +63,12 @@ SIGNATURES = {
     "pcfm_pointwise_gemm": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P]),
     "pcfm_pointwise_wgrad_workspace_bytes": (_Z, [_I, _I, _I, _I]),
     "pcfm_pointwise_wgrad": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, _Z, _P]),
+    "pcfm_trilinear_devoxelize_scale_add_fwd": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P,
+                                                     _P, _P]),
+    "pcfm_rows_dot": (_I, [_P, _P, _L, _I, _F, _P, _P]),
+    "pcfm_rows_affine": (_I, [_P, _P, _P, _L, _I, _P]),
+    "pcfm_pointwise_gemm_parts": (_I, [_I, _P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P]),
+    "pcfm_pointwise_wgrad_parts": (_I, [_I, _P, _P, _P, _I, _I, _I, _P, _P, _Z, _P]),
     "pcfm_rows_wgrad_workspace_bytes": (_Z, [_L, _I, _I]),
     "pcfm_rows_wgrad_bf16": (_I, [_P, _I, _P, _I, _L, _I, _I, _P, _P, _Z, _P]),
     "pcfm_rows_max_workspace_bytes": (_Z, [_I, _I, _I]),
@@ -86,7 +92,7 @@ SIGNATURES = {
                                   _P, _P, _Z, _P]),
 }
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 _lock = threading.Lock()
 _lib = None

@@ -316,6 +316,31 @@ class _PVStage(nn.Module):
         return f, c
 
 
+class _PointwiseParts(torch.autograd.Function):
+    """y = W cat(xs, 1) + bias[b] on the segmented bf16x3 GEMMs (ops.pointwise_*_parts)."""
+
+    @staticmethod
+    def forward(ctx, weight, bias_b, *xs):
+        from pcfm import ops
+        ctx.save_for_backward(weight, *xs)
+        return ops.pointwise_forward_parts(xs, weight, bias_b.contiguous(), bias_per_batch=True)
+
+    @staticmethod
+    def backward(ctx, gy):
+        from pcfm import ops
+        weight, *xs = ctx.saved_tensors
+        gy = gy.contiguous()
+        gw = gb = None
+        gxs = [None] * len(xs)
+        if any(ctx.needs_input_grad[2:]):
+            gxs = ops.pointwise_backward_data_parts(gy, weight, [int(x.shape[1]) for x in xs])
+        if ctx.needs_input_grad[0]:
+            gw = ops.pointwise_backward_weight_parts(xs, gy)
+        if ctx.needs_input_grad[1]:
+            gb = gy.sum(dim=2)
+        return (gw, gb, *gxs)
+
+
 class ContextNet(_TimeCondEmbed):
     """Multi-resolution PVConv pyramid -> per-point context (B, N, ctx_dim), blended with a
     (t, cond)-only context by a sigmoid gate in t (models.py:392-543)."""
@@ -376,6 +401,28 @@ class ContextNet(_TimeCondEmbed):
         c_in = x.new_zeros((x.shape[0], 1)) if cond is None or cond.numel() == 0 else cond
         return F.silu(self.c_proj(c_in))
 
+    def _head_pre(self, scales: List[torch.Tensor], g: Optional[torch.Tensor]) -> torch.Tensor:
+        """head_pre(cat(scales | g broadcast over points)) (models.py:460-466).
+
+        On the bf16x3 path the concat is never built: the segmented GEMM reads
+        the stage outputs in place, and the global feature's columns of the
+        weight collapse to a per-cloud bias W_g g + b (the broadcast columns
+        are constant along the points)."""
+        pre = self.head_pre
+        widths = [int(s.shape[1]) for s in scales]
+        if (pre.x3_ok(scales[-1]) and len(scales) <= 4 and pre.bias is not None
+                and all(w % 128 == 0 for w in widths[:-1])):
+            w = pre.weight[:, :, 0]
+            cs = sum(widths)
+            if g is not None:
+                bias_b = torch.addmm(pre.bias, g, w[:, cs:].t())
+            else:
+                bias_b = pre.bias.expand(scales[0].shape[0], -1)
+            return _PointwiseParts.apply(w[:, :cs], bias_b, *scales)
+        if g is not None:
+            scales = scales + [g[:, :, None].expand_as(scales[-1])]
+        return pre(torch.cat(scales, dim=1))
+
     def forward(self, x: torch.Tensor, t: torch.Tensor, cond: Optional[torch.Tensor]):
         b, n, d = x.shape
         coords = x[..., :3].permute(0, 2, 1).contiguous()
@@ -394,10 +441,8 @@ class ContextNet(_TimeCondEmbed):
             for stage in self.stages:
                 f, c = stage(f, c, emb32)
                 scales.append(f)
-            if self.with_global:
-                g = self.global_mlp(f.max(dim=-1).values)
-                scales.append(g[:, :, None].expand_as(f))
-            h = self.head_act(self.head_norm(self.head_pre(torch.cat(scales, dim=1))))
+            g = self.global_mlp(f.max(dim=-1).values) if self.with_global else None
+            h = self.head_act(self.head_norm(self._head_pre(scales, g)))
             ctx = self.head_out(h).permute(0, 2, 1)
             if self.use_t_gate:
                 ctx_glb = self.ctx_from_emb(emb32)[:, None, :].expand(b, n, -1)

@@ -13,6 +13,7 @@ every element, so the reference's torch::zeros pre-fill is not needed).
 """
 from __future__ import annotations
 
+import ctypes
 import types
 
 import torch
@@ -167,6 +168,76 @@ def trilinear_devoxelize_forward(r: int, is_training: bool, coords: torch.Tensor
         _lib.call("pcfm_trilinear_devoxelize_fwd", _ptr(coords), _ptr(features), b, c, n, r,
                   1 if is_training else 0, _ptr(outs), pi, pw, _stream(features))
     return [outs, inds, wgts]
+
+
+def trilinear_devoxelize_scale_add(r: int, is_training: bool, coords: torch.Tensor,
+                                   features: torch.Tensor, scale, add):
+    """scale[b, c] * devox(features) + add (either None): SE3d and the PVConv
+    point-branch sum folded into the devoxelization -> [outs, inds, wgts]."""
+    _check(features, "features", "f")
+    _check(coords, "coords", "f")
+    b, c = features.shape[0], features.shape[1]
+    n = coords.shape[2]
+    r = int(r)
+    dev = features.device
+    if scale is not None:
+        scale = scale.contiguous()
+        _check(scale, "scale", "f")
+        if scale.numel() != b * c:
+            raise ValueError("trilinear_devoxelize_scale_add: scale must be (B, C)")
+    if add is not None:
+        add = add.contiguous()
+        _check(add, "add", "f")
+        if tuple(add.shape) != (b, c, n):
+            raise ValueError("trilinear_devoxelize_scale_add: add must be (B, C, N)")
+    outs = torch.empty((b, c, n), dtype=torch.float32, device=dev)
+    if is_training:
+        inds = torch.empty((b, 8, n), dtype=torch.int32, device=dev)
+        wgts = torch.empty((b, 8, n), dtype=torch.float32, device=dev)
+        pi, pw = _ptr(inds), _ptr(wgts)
+    else:
+        inds = torch.zeros((1,), dtype=torch.int32, device=dev)
+        wgts = torch.zeros((1,), dtype=torch.float32, device=dev)
+        pi, pw = None, None
+    nbytes = 4 * b * (3 * n + c * r ** 3 + c * n * (2 if add is not None else 1)
+                      + (16 * n if is_training else 0))
+    with _timed("trilinear_devoxelize_fwd", nbytes, features):
+        _lib.call("pcfm_trilinear_devoxelize_scale_add_fwd", _ptr(coords), _ptr(features),
+                  _ptr(scale) if scale is not None else None,
+                  _ptr(add) if add is not None else None, b, c, n, r, 1 if is_training else 0,
+                  _ptr(outs), pi, pw, _stream(features))
+    return [outs, inds, wgts]
+
+
+def rows_dot(a: torch.Tensor, b, scale: float = 1.0) -> torch.Tensor:
+    """scale * sum over the last axis of a * b (b None: of a) for 2-D (rows, len)."""
+    _check(a, "a", "f")
+    if b is not None:
+        _check(b, "b", "f")
+        if b.shape != a.shape:
+            raise ValueError("rows_dot: shape mismatch")
+    rows, length = a.shape
+    out = torch.empty((rows,), dtype=torch.float32, device=a.device)
+    nbytes = 4 * rows * length * (2 if b is not None else 1)
+    with _timed("rows_dot", nbytes, a):
+        _lib.call("pcfm_rows_dot", _ptr(a), _ptr(b) if b is not None else None, rows, length,
+                  float(scale), _ptr(out), _stream(a))
+    return out
+
+
+def rows_affine_(x: torch.Tensor, s: torch.Tensor, t) -> torch.Tensor:
+    """x[r, :] = s[r] * x[r, :] + t[r] in place, x (rows, len) with len % 4 == 0."""
+    _check(x, "x", "f")
+    _check(s, "s", "f")
+    if t is not None:
+        _check(t, "t", "f")
+    rows, length = x.shape
+    if s.numel() != rows or (t is not None and t.numel() != rows):
+        raise ValueError("rows_affine_: per-row parameters must have one value per row")
+    with _timed("rows_affine", 8 * rows * length, x):
+        _lib.call("pcfm_rows_affine", _ptr(x), _ptr(s), _ptr(t) if t is not None else None, rows,
+                  length, _stream(x))
+    return x
 
 
 def trilinear_devoxelize_backward(grad_y: torch.Tensor, indices: torch.Tensor,
@@ -523,6 +594,78 @@ def pointwise_backward_weight(x: torch.Tensor, grad_y: torch.Tensor) -> torch.Te
     with _timed("pointwise_wgrad", 2 * b * n * cin * cout, x, "mfma"):
         _lib.call("pcfm_pointwise_wgrad", _ptr(x), _ptr(g), b, cin, cout, n, _ptr(dw), _ptr(ws),
                   ws.numel(), _stream(x))
+    return dw
+
+
+def _parts(ts):
+    """Host pointer / width arrays of a channel-segmented tensor list."""
+    ptrs = (ctypes.c_void_p * len(ts))(*[_ptr(t) for t in ts])
+    widths = (ctypes.c_int * len(ts))(*[int(t.shape[1]) for t in ts])
+    return ptrs, widths
+
+
+def pointwise_forward_parts(xs, weight: torch.Tensor, bias, bias_per_batch: bool = False):
+    """y = W cat(xs, 1) + bias without materialising the concat; xs (B, C_i, N)
+    fp32 (every C_i but the last a multiple of 32), bias (Cout,) or, with
+    bias_per_batch, (B, Cout)."""
+    xs = [x.contiguous() for x in xs]
+    for x in xs:
+        _check(x, "input", "f")
+    b, _, n = xs[0].shape
+    cin = sum(int(x.shape[1]) for x in xs)
+    cout = weight.shape[0]
+    weight = weight.reshape(cout, -1).contiguous()
+    if weight.shape[1] != cin:
+        raise ValueError("pointwise_forward_parts: weight does not match the parts")
+    img = pointwise_prep_weight(weight, False)
+    y = torch.empty((b, cout, n), dtype=torch.float32, device=xs[0].device)
+    bias_c = bias.contiguous() if bias is not None else None
+    xp, xw = _parts(xs)
+    yp, yw = _parts([y])
+    with _timed("pointwise_fwd", 2 * b * n * cin * cout, xs[0], "mfma"):
+        _lib.call("pcfm_pointwise_gemm_parts", len(xs), ctypes.addressof(xp), ctypes.addressof(xw),
+                  _ptr(img), _ptr(bias_c) if bias_c is not None else None, int(bias_per_batch),
+                  b, n, 1, ctypes.addressof(yp), ctypes.addressof(yw), _stream(xs[0]))
+    return y
+
+
+def pointwise_backward_data_parts(grad_y: torch.Tensor, weight: torch.Tensor, widths):
+    """dx parts (B, w_i, N) of y = W cat(parts); every width but the last % 128."""
+    _check(grad_y, "grad_output", "f")
+    g = grad_y.contiguous()
+    b, cout, n = g.shape
+    weight = weight.reshape(cout, -1).contiguous()
+    cin = weight.shape[1]
+    if sum(widths) != cin:
+        raise ValueError("pointwise_backward_data_parts: widths do not match the weight")
+    img = pointwise_prep_weight(weight, True)
+    dxs = [torch.empty((b, w, n), dtype=torch.float32, device=g.device) for w in widths]
+    gp, gw = _parts([g])
+    dp, dw = _parts(dxs)
+    with _timed("pointwise_bwd_data", 2 * b * n * cin * cout, g, "mfma"):
+        _lib.call("pcfm_pointwise_gemm_parts", 1, ctypes.addressof(gp), ctypes.addressof(gw),
+                  _ptr(img), None, 0, b, n, len(dxs), ctypes.addressof(dp), ctypes.addressof(dw),
+                  _stream(g))
+    return dxs
+
+
+def pointwise_backward_weight_parts(xs, grad_y: torch.Tensor) -> torch.Tensor:
+    """dL/dW (Cout, sum C_i) of y = W cat(xs, 1)."""
+    xs = [x.contiguous() for x in xs]
+    for x in xs:
+        _check(x, "input", "f")
+    _check(grad_y, "grad_output", "f")
+    g = grad_y.contiguous()
+    b, _, n = xs[0].shape
+    cin = sum(int(x.shape[1]) for x in xs)
+    cout = g.shape[1]
+    ws = _workspace(_lib.query("pcfm_pointwise_wgrad_workspace_bytes", b, cin, cout, n), g)
+    dw = torch.empty((cout, cin), dtype=torch.float32, device=g.device)
+    xp, xw = _parts(xs)
+    with _timed("pointwise_wgrad", 2 * b * n * cin * cout, g, "mfma"):
+        _lib.call("pcfm_pointwise_wgrad_parts", len(xs), ctypes.addressof(xp),
+                  ctypes.addressof(xw), _ptr(g), b, cout, n, _ptr(dw), _ptr(ws), ws.numel(),
+                  _stream(g))
     return dw
 
 

@@ -26,7 +26,8 @@ def ops():
 
 
 @pytest.mark.parametrize("b,cin,cout,r", [(2, 128, 128, 8), (1, 128, 256, 8), (1, 256, 128, 8),
-                                          (2, 128, 128, 16), (1, 256, 256, 8), (1, 128, 128, 32)])
+                                          (2, 128, 128, 16), (1, 256, 256, 8), (1, 128, 128, 32),
+                                          (1, 128, 128, 24)])
 def test_conv3d_fwd_bwd_vs_fp64(ops, b, cin, cout, r):
     g = torch.Generator(device="cuda").manual_seed(b * 1000 + cin + r)
     x = torch.randn(b, cin, r, r, r, device="cuda", generator=g)
@@ -59,6 +60,21 @@ def test_conv3d_padding_is_zero(ops):
     n1 = 3 - (idx == 0).int() - (idx == r - 1).int()
     cnt = (n1[:, None, None] * n1[None, :, None] * n1[None, None, :]).float() * c
     assert torch.equal(y[0, 0], cnt) and torch.equal(y[0, c - 1], cnt)
+
+
+@pytest.mark.parametrize("b,r", [(2, 16), (1, 8), (1, 24)])
+def test_conv3d_wgrad_padding_counts(ops, b, r):
+    """All-ones x and grad_y: dW[co, ci, tap] = b * prod over axes of (r - |d|) exactly
+    (the three-tap kernel's halo rows and z/y/x edge masking)."""
+    c = 128
+    x = torch.ones(b, c, r, r, r, device="cuda")
+    gy = torch.ones(b, c, r, r, r, device="cuda")
+    xs, gys = ops.conv3d_split(x), ops.conv3d_split(gy)
+    dw = ops.conv3d_wgrad_split(xs, gys, b, c, c, r).view(c, c, 3, 3, 3)
+    n = torch.tensor([r - 1, r, r - 1], dtype=torch.float32, device="cuda")
+    want = b * n[:, None, None] * n[None, :, None] * n[None, None, :]
+    assert torch.equal(dw[0, 0], want) and torch.equal(dw[c - 1, 5], want)
+    assert torch.equal(dw, want.expand_as(dw))
 
 
 def test_conv3d_unsupported_shape_rejected(ops):

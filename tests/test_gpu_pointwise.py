@@ -64,3 +64,50 @@ def test_pointwise_module_keeps_autocast(ops):
     with torch.autocast("cuda", dtype=torch.bfloat16):
         assert mod(x).dtype == torch.bfloat16
     assert mod(x).dtype == torch.float32
+
+
+@pytest.mark.parametrize("widths,cout,n", [((128, 256, 256), 256, 2000), ((128, 96), 64, 333),
+                                           ((32, 32, 32, 7), 130, 65)])
+def test_pointwise_parts_vs_fp64(ops, widths, cout, n):
+    """Channel-segmented GEMMs (ContextNet head_pre without the concat)."""
+    b = 2
+    g = torch.Generator(device="cuda").manual_seed(sum(widths) + cout + n)
+    xs = [torch.randn(b, w, n, device="cuda", generator=g) for w in widths]
+    cin = sum(widths)
+    w = torch.randn(cout, cin, device="cuda", generator=g) / cin ** 0.5
+    bias_b = torch.randn(b, cout, device="cuda", generator=g)
+    gy = torch.randn(b, cout, n, device="cuda", generator=g)
+    x64 = torch.cat(xs, 1).double().cpu()
+    w64, g64 = w.double().cpu(), gy.double().cpu()
+    y64 = torch.einsum("oc,bcn->bon", w64, x64) + bias_b.double().cpu()[:, :, None]
+    assert _rel(ops.pointwise_forward_parts(xs, w, bias_b, bias_per_batch=True), y64) < TOL
+    dx64 = torch.einsum("oc,bon->bcn", w64, g64)
+    if all(v % 128 == 0 for v in widths[:-1]):
+        dxs = ops.pointwise_backward_data_parts(gy, w, list(widths))
+        assert [d.shape[1] for d in dxs] == list(widths)
+        assert _rel(torch.cat(dxs, 1), dx64) < TOL
+    dw64 = torch.einsum("bon,bcn->oc", g64, x64)
+    assert _rel(ops.pointwise_backward_weight_parts(xs, gy), dw64) < TOL
+
+
+def test_context_head_pre_parts_matches_concat(ops):
+    from pcfm.models import ContextNet
+    torch.manual_seed(3)
+    net = ContextNet(3, 0, emb_dim=32, ctx_dim=16).cuda()
+    b, n = 2, 1500
+    scales = [torch.randn(b, c, n, device="cuda", requires_grad=True) for c in net.stage_channels]
+    g = torch.randn(b, net.stage_channels[-1], device="cuda", requires_grad=True)
+    y = net._head_pre(scales, g)
+    gy = torch.randn_like(y)
+    grads = torch.autograd.grad(y, [*scales, g, net.head_pre.weight, net.head_pre.bias], gy)
+    ref_in = torch.cat([s.detach().double() for s in scales]
+                       + [g.detach().double()[:, :, None].expand(b, -1, n)], 1).requires_grad_(True)
+    w64 = net.head_pre.weight.detach().double().requires_grad_(True)
+    b64 = net.head_pre.bias.detach().double().requires_grad_(True)
+    y64 = torch.nn.functional.conv1d(ref_in, w64, b64)
+    r = torch.autograd.grad(y64, [ref_in, w64, b64], gy.double())
+    cs = sum(net.stage_channels)
+    refs = list(torch.split(r[0][:, :cs], net.stage_channels, 1)) + [r[0][:, cs:].sum(2), r[1], r[2]]
+    assert _rel(y, y64.detach().cpu()) < TOL
+    for a, ref in zip(grads, refs):
+        assert _rel(a, ref.detach().cpu()) < 2 * TOL

@@ -1,4 +1,5 @@
-"""Time conv3d wgrad at the PVConv shapes (dev tool; run with PCFM_LIB variants)."""
+"""Probe: split-operand voxel-conv weight gradient time at the PVConv shapes
+(dev tool; run against measurement variants via PCFM_LIB)."""
 import os
 import sys
 import time
@@ -9,16 +10,24 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [REPO, os.path.join(REPO, "point-cloud-flow-matching_amd")]
 from pcfm import ops  # noqa: E402
 
-for b, c, r in [(8, 128, 32), (8, 256, 16), (8, 256, 8)]:
-    x = torch.randn(b, c, r, r, r, device="cuda")
-    gy = torch.randn(b, c, r, r, r, device="cuda")
-    for _ in range(2):
-        ops.conv3d_backward_weight(x, gy)
+
+def timeit(fn, iters=20):
+    for _ in range(3):
+        fn()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(10):
-        ops.conv3d_backward_weight(x, gy)
+    for _ in range(iters):
+        fn()
     torch.cuda.synchronize()
-    ms = (time.perf_counter() - t0) * 100
-    print(os.environ.get("PCFM_LIB", "default").split("/")[-1], f"C{c}R{r} wgrad {ms:.3f} ms "
-          f"{2 * b * r ** 3 * c * c * 27 / ms / 1e9:.0f} TF", flush=True)
+    return (time.perf_counter() - t0) * 1e3 / iters
+
+
+tag = os.environ.get("PCFM_LIB", "default").split("/")[-1]
+for b, c, r in [(8, 128, 32), (8, 256, 16), (8, 256, 8)]:
+    g = torch.Generator(device="cuda").manual_seed(0)
+    x = torch.randn(b, c, r, r, r, device="cuda", generator=g)
+    gy = torch.randn(b, c, r, r, r, device="cuda", generator=g)
+    xs, gys = ops.conv3d_split(x), ops.conv3d_split(gy)
+    flop = 2 * b * r ** 3 * c * c * 27
+    t = timeit(lambda: ops.conv3d_wgrad_split(xs, gys, b, c, c, r))
+    print(f"{tag} C{c}R{r}: wgrad {t:.3f} ms ({flop / t / 1e9:.0f} TF fp32-equiv)", flush=True)
