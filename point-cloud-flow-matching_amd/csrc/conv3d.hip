@@ -412,6 +412,216 @@ __global__ void __launch_bounds__(512)
 }
 
 // ---------------------------------------------------------------------------
+// Forward / backward-data, THREE taps per step: the dz = -1, 0, +1 taps of one
+// (dx, dy) read X rows shifted by one voxel, so a step stages the 256-voxel
+// tile's X rows once with a one-row halo each side (258 rows, K = 16 channels)
+// plus the three taps' weight slices, and every wave reads its B operand at row
+// offset 1 + dz.  X traffic per output drops 3x against conv3_igemm_glds_kernel
+// (which is L2-bandwidth bound at these shapes).  32-B LDS rows, 16-B halves
+// swapped on odd 8-row blocks (conflict-free ds_read_b128 of both operands),
+// applied on the source side of the lane-linear LDS-DMA; out-of-volume
+// neighbours are zeroed in registers.  3 stages, counted vmcnt, raw barrier,
+// inline-asm LDS-DMA (hipcc adds no waits for it).
+// ---------------------------------------------------------------------------
+// LDS-DMA as inline asm: hipcc does not see it, so it inserts no vmcnt(0)
+// before the step's LDS reads (it does for __builtin_amdgcn_global_load_lds
+// here, which serialises the prefetch with the compute); completion is waited
+// for by hand.  M0 is set and restored inside the statement.
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+__device__ __forceinline__ void glds16_asm(const void* g, uint32_t lds) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(g), "s"(lds)
+      : "memory");
+}
+
+constexpr int kHM = 128, kHN = 256, kHK = 16, kHStages = 3;
+constexpr int kHRow = kHK * 2;                    // bytes per LDS row (hi or lo)
+constexpr int kHAImg = kHM * kHRow;               // 4 KiB: one tap's weight slice
+constexpr int kHBRows = 288;                      // 258 rows used, 32-row pieces
+constexpr int kHBImg = kHBRows * kHRow;           // 9 KiB
+constexpr int kHStage = 6 * kHAImg + 2 * kHBImg;  // 42 KiB
+constexpr int kHAPieces = kHAImg / 1024, kHBPieces = kHBImg / 1024;
+constexpr int kHPieces = 6 * kHAPieces + 2 * kHBPieces;  // 42
+constexpr int kHQ = (kHPieces + 7) / 8;                    // pieces per wave (<=)
+constexpr int kHQmin = kHPieces / 8;                       // pieces per wave (>=)
+
+__device__ __forceinline__ int hswz(int row) { return (row >> 3) & 1; }
+
+__device__ __forceinline__ bf16x8 zero_unless(bool ok, bf16x8 v) {
+  uint4 u = __builtin_bit_cast(uint4, v);
+  u.x = ok ? u.x : 0u;
+  u.y = ok ? u.y : 0u;
+  u.z = ok ? u.z : 0u;
+  u.w = ok ? u.w : 0u;
+  return __builtin_bit_cast(bf16x8, u);
+}
+
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2)))
+    conv3_igemm_glds3_kernel(const uint16_t* __restrict__ xh, const uint16_t* __restrict__ xl,
+                             const uint16_t* __restrict__ wh, const uint16_t* __restrict__ wl,
+                             const float* __restrict__ bias, float* __restrict__ y, int K, int M,
+                             int R) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kHStages * kHStage];
+  const int V = R * R * R, R2 = R * R;
+  int id = (int)blockIdx.x;
+  {
+    const int nwg = (int)gridDim.x, q = nwg / 8, rr = nwg % 8, xcd = id % 8;
+    id = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + id / 8;
+  }
+  const int nmt = M / kHM, nvt = V / kHN;
+  const int m0 = (id % nmt) * kHM;
+  id /= nmt;
+  const int v0 = (id % nvt) * kHN, b = id / nvt;
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wr = w >> 2, wc = w & 3, r = lane & 31, h = lane >> 5;
+  const int nsteps = 9 * (K / kHK);
+  const size_t bV = (size_t)b * V;
+
+  // coordinates of this lane's two output voxels (B-operand rows)
+  int vx[2], vy[2], vz[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int v = v0 + wc * 64 + j * 32 + r;
+    vx[j] = v / R2;
+    vy[j] = (v / R) % R;
+    vz[j] = v % R;
+  }
+  // this lane's place in a 1-KiB piece: row lane / 2, physical half lane & 1
+  const int prow = lane >> 1, phalf = lane & 1;
+
+  auto issue = [&](int s, int buf) {
+    const int c0 = (s / 9) * kHK, pair = s - (s / 9) * 9;
+    const int dx = pair / 3 - 1, dy = pair % 3 - 1;
+    const int off = dx * R2 + dy * R;
+    uint8_t* base = lds + buf * kHStage;
+#pragma unroll
+    for (int q = 0; q < kHQ; ++q) {
+      const int I = w + 8 * q;
+      if (I < 6 * kHAPieces) {  // weights: image a = 2 * dz-index + (hi|lo)
+        const int a = I / kHAPieces, P = I % kHAPieces;
+        const int row = 32 * P + prow;
+        const int tap = pair * 3 + (a >> 1);
+        const uint16_t* src = ((a & 1) ? wl : wh) + ((size_t)tap * M + m0 + row) * K + c0 +
+                              8 * (phalf ^ hswz(row));
+        glds16_asm(src, lds_addr(base + a * kHAImg + P * 1024));
+      } else if (I < kHPieces) {  // X rows v0 + off - 1 + row
+        const int I2 = I - 6 * kHAPieces;
+        const int hl = I2 / kHBPieces, P = I2 % kHBPieces;
+        const int row = 32 * P + prow;
+        int gv = v0 + off - 1 + row;
+        gv = gv < 0 ? 0 : (gv >= V ? V - 1 : gv);  // out-of-volume rows are zeroed at use
+        const uint16_t* src = (hl ? xl : xh) + (bV + gv) * K + c0 + 8 * (phalf ^ hswz(row));
+        glds16_asm(src, lds_addr(base + 6 * kHAImg + hl * kHBImg + P * 1024));
+      }
+    }
+  };
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
+
+  issue(0, 0);
+  if (nsteps > 1) issue(1, 1);
+  for (int s = 0; s < nsteps; ++s) {
+    // stage s landed (this wave's pieces): stage s+1's (>= kHQmin) stay in flight
+    if (s + 1 < nsteps) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kHQmin) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // everyone's stage s landed; stage s-1 reads done
+#ifndef PCFM_EXP_NOLOAD
+    if (s + 2 < nsteps) issue(s + 2, (s + 2) % kHStages);
+#endif
+    const uint8_t* base = lds + (s % kHStages) * kHStage;
+    const int pair = s % 9;
+    const int dx = pair / 3 - 1, dy = pair % 3 - 1;
+    bool okxy[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      okxy[j] = (unsigned)(vx[j] + dx) < (unsigned)R && (unsigned)(vy[j] + dy) < (unsigned)R;
+    // operands of tap tz+1 are read before tap tz's MFMAs (register double
+    // buffer), so only the first tap of a step waits for LDS latency
+    bf16x8 op[2][8];  // [buffer][ah0 ah1 al0 al1 bh0 bh1 bl0 bl1]
+    auto read_ops = [&](int tz, bf16x8 (&o)[8]) {
+      const int dz = tz - 1;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int row = wr * 64 + i * 32 + r;
+        const int a = (2 * tz) * kHAImg + row * kHRow + ((h ^ hswz(row)) << 4);
+        o[i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(base + a));
+        o[2 + i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(base + a + kHAImg));
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int row = wc * 64 + j * 32 + r + 1 + dz;
+        const int a = 6 * kHAImg + row * kHRow + ((h ^ hswz(row)) << 4);
+        const bool ok = okxy[j] && (unsigned)(vz[j] + dz) < (unsigned)R;
+        o[4 + j] = zero_unless(ok, __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(base + a)));
+        o[6 + j] = zero_unless(
+            ok, __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(base + a + kHBImg)));
+      }
+    };
+    read_ops(0, op[0]);
+#pragma unroll
+    for (int tz = 0; tz < 3; ++tz) {
+      if (tz < 2) read_ops(tz + 1, op[(tz + 1) & 1]);
+      const bf16x8(&o)[8] = op[tz & 1];
+#ifdef PCFM_EXP_NOMFMA
+      acc[0][0][tz] += (float)(o[0][0] + o[2][1] + o[1][2] + o[3][3] + o[4][4] + o[6][5] +
+                               o[5][6] + o[7][7]);
+      continue;
+#endif
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(o[i], o[4 + j], acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(o[i], o[6 + j], acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(o[2 + i], o[4 + j], acc[i][j], 0, 0, 0);
+#ifndef PCFM_EXP_NOSCHED
+      if (tz < 2) {  // spread the next tap's 8 operand reads over this tap's 12 MFMAs
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+      }
+#endif
+    }
+  }
+  float* __restrict__ yb = y + (size_t)b * M * V;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int m = m0 + wr * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+        const int v = v0 + wc * 64 + j * 32 + r;
+        yb[(size_t)m * V + v] = acc[i][j][e] + (bias != nullptr ? bias[m] : 0.0f);
+      }
+}
+
+// ---------------------------------------------------------------------------
 // Weight gradient over the channels-last split operands (the forward's split
 // input xs and the backward-data pass's split dY): per tap a GEMM reducing over
 // voxels, dW[co][ci] = sum_v dY[v][co] * X[v + off][ci], both operands
@@ -603,23 +813,6 @@ __device__ __forceinline__ bf16x8 tr_operand_rows(const uint8_t* img, int row0, 
   const v4s_tr x0 = tr_read16(img, swz256(row, col >> 3) + 8 * (p4 & 1));
   const v4s_tr x1 = tr_read16(img, swz256(row + 4, col >> 3) + 8 * (p4 & 1));
   return __builtin_bit_cast(bf16x8, __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7));
-}
-
-// LDS-DMA as inline asm: hipcc does not see it, so it inserts no vmcnt(0)
-// before the step's LDS reads (it does for __builtin_amdgcn_global_load_lds
-// here, which serialises the prefetch with the compute); completion is waited
-// for by hand.  M0 is set and restored inside the statement.
-__device__ __forceinline__ uint32_t lds_addr(const void* p) {
-  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
-}
-__device__ __forceinline__ void glds16_asm(const void* g, uint32_t lds) {
-  unsigned keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(g), "s"(lds)
-      : "memory");
 }
 
 __device__ __forceinline__ bf16x8 mask_k8(bf16x8 v, uint32_t m0, uint32_t m12, uint32_t m3) {
@@ -969,6 +1162,13 @@ extern "C" int pcfm_conv3d_igemm_cl(const void* xs, const void* wsplit, const fl
       set_error("conv3d_igemm_cl: zero-row allocation failed");
       return (int)hipErrorOutOfMemory;
     }
+#ifdef PCFM_CONV_GLDS3  // three-tap variant: 3x less X traffic, measured equal speed
+    if (cin % kHK == 0) {
+      hipLaunchKernelGGL(conv3_igemm_glds3_kernel, dim3((unsigned)glds_blocks), dim3(512), 0, st,
+                         xh, xl, wh, wh + total, bias, y, cin, cout, r);
+      return check_launch("conv3d_igemm_cl");
+    }
+#endif
     hipLaunchKernelGGL(conv3_igemm_glds_kernel, dim3((unsigned)glds_blocks), dim3(512), 0, st, xh,
                        xl, wh, wh + total, zrow, bias, y, cin, cout, r);
     return check_launch("conv3d_igemm_cl");

@@ -210,18 +210,22 @@ __global__ void __launch_bounds__(256)
   }
 }
 
-// dbias[c] = sum over b, then over blocks, of rowpart[(b * C + c) * nch + k]
+// dbias[c] = sum over (b, k) of rowpart[(b * C + c) * nch + k]: one wave per
+// channel, lane-strided in a fixed order, then a fixed xor tree (deterministic)
 __global__ void __launch_bounds__(256)
     bn_bias_finalize_kernel(const float* __restrict__ rowpart, int B, int C, int nch,
                             float* __restrict__ dbias) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= C) return;
+  const int c = blockIdx.x * 4 + (int)(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (c >= C) return;  // wave-uniform
   float s = 0.0f;
-  for (int b = 0; b < B; ++b) {
-    const float* p = rowpart + ((size_t)b * C + c) * nch;
-    for (int k = 0; k < nch; ++k) s += p[k];
+  const int tot = B * nch;
+  for (int e = lane; e < tot; e += 64) {
+    const int b = e / nch, k = e - b * nch;
+    s += rowpart[((size_t)b * C + c) * nch + k];
   }
-  dbias[c] = s;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+  if (lane == 0) dbias[c] = s;
 }
 
 // ---------------------------------------------------------------------------
@@ -476,7 +480,7 @@ extern "C" int pcfm_bn_act_bwd(const float* dz, const float* x, const float* gam
                      gamma, beta, (const float*)dgamma, (const float*)dbeta, c, s / 4,
                      (float)(1.0 / ((double)b * s)), slope, dx, rowpart);
   if (dbias_in != nullptr)
-    hipLaunchKernelGGL(bn_bias_finalize_kernel, dim3(ceil_div(c, 256)), dim3(256), 0, st,
+    hipLaunchKernelGGL(bn_bias_finalize_kernel, dim3(ceil_div(c, 4)), dim3(256), 0, st,
                        (const float*)rowpart, b, c, nch, dbias_in);
   return check_launch("bn_act_bwd");
 }

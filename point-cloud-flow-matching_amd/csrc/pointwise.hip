@@ -156,6 +156,121 @@ __global__ void __launch_bounds__(256)
   }
 }
 
+// Wide form for Mpad % 256 == 0: a 256 (m) x 128 (point) tile, 8 waves of
+// 64 x 64 (4 x 2), 512 threads, 60 KiB LDS (two blocks per CU).  Every output
+// channel of a point tile comes from one block, so x is read from HBM once
+// (the 128-row tile above reads it Mpad / 128 times).
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4)))
+    pw_gemm256_kernel(const Parts x, const uint16_t* __restrict__ wh,
+                      const uint16_t* __restrict__ wl, const float* __restrict__ bias,
+                      int bias_bstride, const Parts y, int K, int M, int N, int Kpad) {
+  constexpr int TM = 256, TN = 128;
+  constexpr int A_ELEMS = TM * kLDR, B_ELEMS = TN * kLDR;
+  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * A_ELEMS + 2 * B_ELEMS];
+  const int b = blockIdx.z, m0 = blockIdx.y * TM, p0 = blockIdx.x * TN;
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wr = w >> 1, wc = w & 1, r = lane & 31, h = lane >> 5;
+  constexpr int CPT = kKT * TN / 512;  // 8 channels per thread per K-step
+  const int sp = t % TN, ch = __builtin_amdgcn_readfirstlane((t / TN) * CPT);
+  const int pt = p0 + sp;
+  const bool pok = pt < N;
+  const int ptc = pok ? pt : N - 1;
+  const int arow = t >> 1, ahalf = (t & 1) * 16;
+  const int nsteps = Kpad / kKT;
+
+  uint4 ra0 = {}, ra1 = {}, ra2 = {}, ra3 = {};
+  float rb[CPT];
+  uint32_t rmask = 0u;
+  auto load = [&](int s) {
+    const int c0 = s * kKT;
+    const size_t g = (size_t)(m0 + arow) * Kpad + c0 + ahalf;
+    ra0 = *reinterpret_cast<const uint4*>(wh + g);
+    ra1 = *reinterpret_cast<const uint4*>(wh + g + 8);
+    ra2 = *reinterpret_cast<const uint4*>(wl + g);
+    ra3 = *reinterpret_cast<const uint4*>(wl + g + 8);
+    rmask = 0u;
+    const int cb = min(c0 + ch, K - 1);
+    const float* __restrict__ xr = x.row(b, cb, N);
+#pragma unroll
+    for (int q = 0; q < CPT; ++q) {
+      const int c = c0 + ch + q;
+      const bool ok = pok && c < K;
+      rb[q] = xr[(size_t)(c < K ? c - cb : 0) * N + ptc];
+      rmask |= ok ? 0u : (1u << q);
+    }
+  };
+  auto store = [&]() {
+    uint16_t* dh = lds + arow * kLDR + ahalf;
+    uint16_t* dl = lds + A_ELEMS + arow * kLDR + ahalf;
+    *reinterpret_cast<uint4*>(dh) = ra0;
+    *reinterpret_cast<uint4*>(dh + 8) = ra1;
+    *reinterpret_cast<uint4*>(dl) = ra2;
+    *reinterpret_cast<uint4*>(dl + 8) = ra3;
+#pragma unroll
+    for (int q = 0; q < CPT; ++q) rb[q] = (rmask >> q) & 1u ? 0.0f : rb[q];
+    uint16_t* bh = lds + 2 * A_ELEMS + sp * kLDR + ch;
+    store_split<CPT>(rb, bh, bh + B_ELEMS);
+  };
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
+
+  load(0);
+  store();
+  __syncthreads();
+  for (int s = 0; s < nsteps; ++s) {
+    if (s + 1 < nsteps) load(s + 1);
+#pragma unroll
+    for (int kk = 0; kk < kKT / 16; ++kk) {
+      bf16x8 ah[2], al[2], bh[2], bl[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int o = (wr * 64 + i * 32 + r) * kLDR + kk * 16 + 8 * h;
+        ah[i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(lds + o));
+        al[i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(lds + A_ELEMS + o));
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int o = 2 * A_ELEMS + (wc * 64 + j * 32 + r) * kLDR + kk * 16 + 8 * h;
+        bh[j] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(lds + o));
+        bl[j] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(lds + B_ELEMS + o));
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
+        }
+    }
+    __syncthreads();
+    if (s + 1 < nsteps) store();
+    __syncthreads();
+  }
+  const int bo = b * bias_bstride;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int mg = m0 + wr * 64 + i * 32;
+    float* __restrict__ yr = y.row(b, min(mg, M - 1), N);
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int dm = (e & 3) + 8 * (e >> 2) + 4 * h;
+        const int m = mg + dm;
+        const int p = p0 + wc * 64 + j * 32 + r;
+        if (m < M && p < N) yr[(size_t)dm * N + p] = acc[i][j][e] + (bias != nullptr ? bias[bo + m] : 0.0f);
+      }
+  }
+}
+
 // dW partials: grid = (ceil(Cout/128) * ceil(Cin/128), S); K-steps of 32
 // points (a step never crosses a batch element).  part [S][Cout][Cin].
 __global__ void __launch_bounds__(256)
@@ -316,6 +431,13 @@ static int pw_gemm_launch(const Parts& x, const void* wsplit, const float* bias,
   const size_t total = (size_t)Mpad * Kpad;
   const uint16_t* wh = (const uint16_t*)wsplit;
   const long long big = (long long)ceil_div(n, 128) * (Mpad / 128) * b;
+#ifndef PCFM_PW_NO256
+  if (Mpad % 256 == 0 && big / 2 >= 2 * kCUs) {
+    hipLaunchKernelGGL(pw_gemm256_kernel, dim3(ceil_div(n, 128), Mpad / 256, b), dim3(512), 0, st,
+                       x, wh, wh + total, bias, bias_bstride, y, cin, cout, n, Kpad);
+    return check_launch("pointwise_gemm");
+  }
+#endif
   if (big >= 2 * kCUs) {
     hipLaunchKernelGGL((pw_gemm_kernel<128, 128>), dim3(ceil_div(n, 128), Mpad / 128, b),
                        dim3(256), 0, st, x, wh, wh + total, bias, bias_bstride, y, cin, cout, n,

@@ -66,11 +66,12 @@ def test_pointwise_module_keeps_autocast(ops):
     assert mod(x).dtype == torch.float32
 
 
-@pytest.mark.parametrize("widths,cout,n", [((128, 256, 256), 256, 2000), ((128, 96), 64, 333),
-                                           ((32, 32, 32, 7), 130, 65)])
-def test_pointwise_parts_vs_fp64(ops, widths, cout, n):
-    """Channel-segmented GEMMs (ContextNet head_pre without the concat)."""
-    b = 2
+@pytest.mark.parametrize("widths,cout,n,b", [((128, 256, 256), 256, 2000, 2), ((128, 96), 64, 333, 2),
+                                             ((32, 32, 32, 7), 130, 65, 2),
+                                             ((128, 256, 256), 256, 20000, 4)])
+def test_pointwise_parts_vs_fp64(ops, widths, cout, n, b):
+    """Channel-segmented GEMMs (ContextNet head_pre without the concat); the last
+    case is large enough for the 256-row tile."""
     g = torch.Generator(device="cuda").manual_seed(sum(widths) + cout + n)
     xs = [torch.randn(b, w, n, device="cuda", generator=g) for w in widths]
     cin = sum(widths)

@@ -30,4 +30,8 @@ for b, c, r in [(8, 128, 32), (8, 256, 16), (8, 256, 8)]:
     xs, gys = ops.conv3d_split(x), ops.conv3d_split(gy)
     flop = 2 * b * r ** 3 * c * c * 27
     t = timeit(lambda: ops.conv3d_wgrad_split(xs, gys, b, c, c, r))
-    print(f"{tag} C{c}R{r}: wgrad {t:.3f} ms ({flop / t / 1e9:.0f} TF fp32-equiv)", flush=True)
+    w = torch.randn(c, c, 3, 3, 3, device="cuda", generator=g)
+    img = ops.conv3d_prep_weight(w, False)
+    tf = timeit(lambda: ops.conv3d_igemm_split(xs, img, None, b, c, c, r, "fwd"))
+    print(f"{tag} C{c}R{r}: wgrad {t:.3f} ms ({flop / t / 1e9:.0f} TF fp32-equiv)  fwd {tf:.3f} ms "
+          f"({flop / tf / 1e9:.0f} TF)", flush=True)
