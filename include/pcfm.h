@@ -38,7 +38,8 @@ extern "C" {
 /* ABI version: bumped on any signature change (4: voxel and pointwise convolution;
  * 5: per-point head kernels; 6: conv3d_igemm workspace,
  * split-operand convolution entry points; fused BatchNorm + activation;
- * 7: channel-segmented pointwise GEMMs, SE3d folded into the devoxelization). */
+ * 7: channel-segmented pointwise GEMMs, SE3d folded into the devoxelization;
+ * 8: per-batch input bias of the head FiLM kernels). */
 int pcfm_abi_version(void);
 /* Thread-local text of the last non-zero return code. */
 const char* pcfm_last_error(void);
@@ -321,12 +322,14 @@ int pcfm_rows_max_bf16(const void* h, int b, int n, int c, void* values, int* in
  * bf16 tensors are passed as void* (raw 16-bit bf16 bits).
  * h of a block = h16 (bf16 [b*n][w], the input Linear's output) if non-NULL,
  * else uprev + gprev (fp32 + bf16: the previous block's residual sum).
+ * hbias (f32 [b][w], may be NULL, used with h16 only): h = bf16(h16 + hbias[b]),
+ * the input Linear's batch-constant embedding columns folded out of its GEMM.
  * Forward of one FiLM block:
  *   y = LayerNorm(h; gamma, beta, eps)   u = y * sp1[b] + shift[b]
  *   (sp1 = bf16(1 + scale), shift: bf16 [b][w], per batch element)
  *   writes u f32 [b*n][w], a = bf16(SiLU(u)) [b*n][w], mean/rstd f32 [b*n]. */
-int pcfm_head_film_fwd(const void* h16, const float* uprev, const void* gprev,
-                       const float* gamma, const float* beta, const void* sp1,
+int pcfm_head_film_fwd(const void* h16, const float* hbias, const float* uprev,
+                       const void* gprev, const float* gamma, const float* beta, const void* sp1,
                        const void* shift, int b, int n, int w, float eps, float* u, void* a,
                        float* mean, float* rstd, void* stream);
 
@@ -341,14 +344,15 @@ size_t pcfm_head_bwd_workspace_bytes(int b, int n, int w);
  *   du = dh_next + da * SiLU'(u);  d sp1[b] = sum_rows du*y;  d shift[b] = sum du;
  *   dy = du * sp1;  d gamma = sum dy*xhat;  d beta = sum dy;
  *   dh = LayerNorm backward (f32, written if dh != NULL) and bf16(dh) -> dh16;
- *   dbias = sum_rows bf16(dh) (the bias gradient of the Linear that produced h).
- * dsp1/dshift f32 [b][w], dgamma/dbeta/dbias f32 [w]; any may be NULL. */
+ *   dbias = sum_rows bf16(dh) (the bias gradient of the Linear that produced h),
+ *   dbias_b[b] = the same sum per batch element (the hbias rows' gradient).
+ * dsp1/dshift/dbias_b f32 [b][w], dgamma/dbeta/dbias f32 [w]; any may be NULL. */
 int pcfm_head_film_bwd(const float* dh_next, const void* da16, const float* u, const void* h16,
-                       const float* uprev, const void* gprev, const float* mean,
-                       const float* rstd, const float* gamma, const float* beta,
-                       const void* sp1, int b, int n, int w, float* dh, void* dh16,
-                       float* dsp1, float* dshift, float* dgamma, float* dbeta, float* dbias,
-                       void* ws, size_t ws_bytes, void* stream);
+                       const float* hbias, const float* uprev, const void* gprev,
+                       const float* mean, const float* rstd, const float* gamma,
+                       const float* beta, const void* sp1, int b, int n, int w, float* dh,
+                       void* dh16, float* dsp1, float* dshift, float* dgamma, float* dbeta,
+                       float* dbias, float* dbias_b, void* ws, size_t ws_bytes, void* stream);
 
 /* Backward of a = bf16(SiLU(uprev + gprev)): dh = da * SiLU'(h) -> dh (f32),
  * dh16 (bf16), dbias = sum_rows bf16(dh). */

@@ -26,7 +26,9 @@
 //                             FiLM backward -> dh (fp32) and bf16(dh)
 //                             !FILM: dh = da * SiLU'(h)
 // with h given either as a bf16 tensor (h_1) or as u_prev + g_prev, the
-// residual sum recomputed instead of stored.
+// residual sum recomputed instead of stored.  h_1 may carry a per-batch fp32
+// bias row hb[b] (the input Linear's columns that see the batch-constant
+// embedding, folded out of the GEMM): h_1 = bf16(h16 + hb[b]).
 #include <algorithm>
 
 #include "pcfm_common.hpp"
@@ -98,9 +100,15 @@ template <int NV>
 __device__ __forceinline__ void load_h(const uint16_t* __restrict__ h16,
                                        const float* __restrict__ uprev,
                                        const uint16_t* __restrict__ gprev, size_t off, int lane,
-                                       float (&x)[NV][4]) {
+                                       float (&x)[NV][4], bool has_hb, const float (&hb)[NV][4]) {
   if (h16 != nullptr) {
     ld_bf16<NV>(h16 + off, lane, x);
+    if (has_hb) {
+#pragma unroll
+      for (int j = 0; j < NV; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) x[j][e] = bf2f(f2bf(x[j][e] + hb[j][e]));
+    }
   } else {
     float g[NV][4];
     ld_f32<NV>(uprev + off, lane, x);
@@ -125,14 +133,16 @@ __global__ void __launch_bounds__(256)
     film_fwd_kernel(const uint16_t* __restrict__ h16, const float* __restrict__ uprev,
                     const uint16_t* __restrict__ gprev, const float* __restrict__ gamma,
                     const float* __restrict__ beta, const uint16_t* __restrict__ sp1,
-                    const uint16_t* __restrict__ shift, int n, float eps,
-                    float* __restrict__ u, uint16_t* __restrict__ a,
+                    const uint16_t* __restrict__ shift, const float* __restrict__ hbias, int n,
+                    float eps, float* __restrict__ u, uint16_t* __restrict__ a,
                     float* __restrict__ mean_o, float* __restrict__ rstd_o) {
   constexpr int W = 256 * NV;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int b = blockIdx.y;
   const int i0 = blockIdx.x * kRowsPerBlock, i1 = min(n, i0 + kRowsPerBlock);
-  float gm[NV][4], bt[NV][4], sp[NV][4], sh[NV][4];
+  float gm[NV][4], bt[NV][4], sp[NV][4], sh[NV][4], hb[NV][4];
+  const bool has_hb = hbias != nullptr;
+  if (has_hb) ld_f32<NV>(hbias + (size_t)b * W, lane, hb);
   if (FILM) {
     ld_f32<NV>(gamma, lane, gm);
     ld_f32<NV>(beta, lane, bt);
@@ -143,7 +153,7 @@ __global__ void __launch_bounds__(256)
     const size_t row = (size_t)b * n + i;
     const size_t off = row * W;
     float x[NV][4];
-    load_h<NV>(h16, uprev, gprev, off, lane, x);
+    load_h<NV>(h16, uprev, gprev, off, lane, x, has_hb, hb);
     float o[NV][4];
     if (FILM) {
       float s = 0.0f;
@@ -193,14 +203,16 @@ __global__ void __launch_bounds__(256)
                     const float* __restrict__ uprev, const uint16_t* __restrict__ gprev,
                     const float* __restrict__ mean_i, const float* __restrict__ rstd_i,
                     const float* __restrict__ gamma, const float* __restrict__ beta,
-                    const uint16_t* __restrict__ sp1, int n, float* __restrict__ dh,
-                    uint16_t* __restrict__ dh16, float* __restrict__ part) {
+                    const uint16_t* __restrict__ sp1, const float* __restrict__ hbias, int n,
+                    float* __restrict__ dh, uint16_t* __restrict__ dh16, float* __restrict__ part) {
   constexpr int W = 256 * NV;
   __shared__ float red[4][kSums][W];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int b = blockIdx.y;
   const int i0 = blockIdx.x * kRowsPerBlock, i1 = min(n, i0 + kRowsPerBlock);
-  float gm[NV][4], bt[NV][4], sp[NV][4];
+  float gm[NV][4], bt[NV][4], sp[NV][4], hb[NV][4];
+  const bool has_hb = hbias != nullptr;
+  if (has_hb) ld_f32<NV>(hbias + (size_t)b * W, lane, hb);
   float acc[kSums][NV][4];
 #pragma unroll
   for (int k = 0; k < kSums; ++k)
@@ -218,7 +230,7 @@ __global__ void __launch_bounds__(256)
     const size_t off = row * W;
     float da[NV][4], x[NV][4], g[NV][4];
     ld_bf16<NV>(da16 + off, lane, da);
-    load_h<NV>(h16, uprev, gprev, off, lane, x);
+    load_h<NV>(h16, uprev, gprev, off, lane, x, has_hb, hb);
     if (FILM) {
       float du[NV][4], uu[NV][4];
       ld_f32<NV>(dhn + off, lane, du);
@@ -320,8 +332,9 @@ bool film_ok(int b, int n, int w) {
 
 template <bool FILM>
 int launch_fwd(const void* h16, const float* uprev, const void* gprev, const float* gamma,
-               const float* beta, const void* sp1, const void* shift, int b, int n, int w,
-               float eps, float* u, void* a, float* mean, float* rstd, hipStream_t st) {
+               const float* beta, const void* sp1, const void* shift, const float* hbias, int b,
+               int n, int w, float eps, float* u, void* a, float* mean, float* rstd,
+               hipStream_t st) {
   const dim3 grid(ceil_div(n, kRowsPerBlock), b), blk(256);
   const uint16_t* H = (const uint16_t*)h16;
   const uint16_t* G = (const uint16_t*)gprev;
@@ -331,11 +344,11 @@ int launch_fwd(const void* h16, const float* uprev, const void* gprev, const flo
   switch (w) {
     case 256:
       hipLaunchKernelGGL((film_fwd_kernel<1, FILM>), grid, blk, 0, st, H, uprev, G, gamma, beta,
-                         S1, SH, n, eps, u, A, mean, rstd);
+                         S1, SH, hbias, n, eps, u, A, mean, rstd);
       break;
     default:
       hipLaunchKernelGGL((film_fwd_kernel<2, FILM>), grid, blk, 0, st, H, uprev, G, gamma, beta,
-                         S1, SH, n, eps, u, A, mean, rstd);
+                         S1, SH, hbias, n, eps, u, A, mean, rstd);
   }
   return check_launch(FILM ? "head_film_fwd" : "head_silu_fwd");
 }
@@ -343,9 +356,9 @@ int launch_fwd(const void* h16, const float* uprev, const void* gprev, const flo
 template <bool FILM>
 int launch_bwd(const float* dhn, const void* da16, const float* u, const void* h16,
                const float* uprev, const void* gprev, const float* mean, const float* rstd,
-               const float* gamma, const float* beta, const void* sp1, int b, int n, int w,
-               float* dh, void* dh16, float* dsp1, float* dshift, float* dgamma,
-               float* dbeta, float* dbias, void* ws, hipStream_t st) {
+               const float* gamma, const float* beta, const void* sp1, const float* hbias, int b,
+               int n, int w, float* dh, void* dh16, float* dsp1, float* dshift, float* dgamma,
+               float* dbeta, float* dbias, float* dbias_b, void* ws, hipStream_t st) {
   const int chunks = ceil_div(n, kRowsPerBlock);
   const dim3 grid(chunks, b), blk(256);
   const uint16_t* DA = (const uint16_t*)da16;
@@ -357,17 +370,25 @@ int launch_bwd(const float* dhn, const void* da16, const float* u, const void* h
   switch (w) {
     case 256:
       hipLaunchKernelGGL((film_bwd_kernel<1, FILM>), grid, blk, 0, st, dhn, DA, u, H, uprev, G,
-                         mean, rstd, gamma, beta, S1, n, dh, D16, part);
+                         mean, rstd, gamma, beta, S1, hbias, n, dh, D16, part);
       break;
     default:
       hipLaunchKernelGGL((film_bwd_kernel<2, FILM>), grid, blk, 0, st, dhn, DA, u, H, uprev, G,
-                         mean, rstd, gamma, beta, S1, n, dh, D16, part);
+                         mean, rstd, gamma, beta, S1, hbias, n, dh, D16, part);
   }
   float* perb = part + (size_t)b * chunks * kSums * w;
   hipLaunchKernelGGL(film_bwd_reduce_kernel, dim3(ceil_div(w, 64), kSums, b), dim3(256), 0, st,
                      (const float*)part, b, chunks, w, dsp1, dshift, perb);
   hipLaunchKernelGGL(film_bwd_reduce2_kernel, dim3(ceil_div(w, 64), 3), dim3(64), 0, st,
                      (const float*)perb, b, w, dgamma, dbeta, dbias);
+  if (dbias_b != nullptr) {  // per-batch bias grad of the preceding Linear (its hb rows)
+    const hipError_t e = hipMemcpyAsync(dbias_b, perb + 2 * (size_t)b * w,
+                                        (size_t)b * w * sizeof(float), hipMemcpyDeviceToDevice, st);
+    if (e != hipSuccess) {
+      set_error("head_film_bwd: hipMemcpyAsync: %s", hipGetErrorString(e));
+      return (int)e;
+    }
+  }
   return check_launch(FILM ? "head_film_bwd" : "head_silu_bwd");
 }
 
@@ -376,22 +397,24 @@ int launch_bwd(const float* dhn, const void* da16, const float* u, const void* h
 
 using namespace pcfm;
 
-extern "C" int pcfm_head_film_fwd(const void* h16, const float* uprev, const void* gprev,
-                                  const float* gamma, const float* beta, const void* sp1,
-                                  const void* shift, int b, int n, int w, float eps, float* u,
-                                  void* a, float* mean, float* rstd, void* stream) {
+extern "C" int pcfm_head_film_fwd(const void* h16, const float* hbias, const float* uprev,
+                                  const void* gprev, const float* gamma, const float* beta,
+                                  const void* sp1, const void* shift, int b, int n, int w,
+                                  float eps, float* u, void* a, float* mean, float* rstd,
+                                  void* stream) {
   PCFM_CHECK_ARG(film_ok(b, n, w), "head_film_fwd: bad shape b=%d n=%d w=%d", b, n, w);
   PCFM_CHECK_ARG(h16 != nullptr || (uprev != nullptr && gprev != nullptr),
                  "head_film_fwd: need h16 or (uprev, gprev)");
-  return launch_fwd<true>(h16, uprev, gprev, gamma, beta, sp1, shift, b, n, w, eps, u, a, mean,
-                          rstd, (hipStream_t)stream);
+  return launch_fwd<true>(h16, uprev, gprev, gamma, beta, sp1, shift,
+                          h16 != nullptr ? hbias : nullptr, b, n, w, eps, u, a, mean, rstd,
+                          (hipStream_t)stream);
 }
 
 extern "C" int pcfm_head_silu_fwd(const float* uprev, const void* gprev, int b, int n, int w,
                                   void* a, void* stream) {
   PCFM_CHECK_ARG(film_ok(b, n, w), "head_silu_fwd: bad shape b=%d n=%d w=%d", b, n, w);
-  return launch_fwd<false>(nullptr, uprev, gprev, nullptr, nullptr, nullptr, nullptr, b, n, w,
-                           0.0f, nullptr, a, nullptr, nullptr, (hipStream_t)stream);
+  return launch_fwd<false>(nullptr, uprev, gprev, nullptr, nullptr, nullptr, nullptr, nullptr, b,
+                           n, w, 0.0f, nullptr, a, nullptr, nullptr, (hipStream_t)stream);
 }
 
 extern "C" size_t pcfm_head_bwd_workspace_bytes(int b, int n, int w) {
@@ -400,21 +423,21 @@ extern "C" size_t pcfm_head_bwd_workspace_bytes(int b, int n, int w) {
 }
 
 extern "C" int pcfm_head_film_bwd(const float* dh_next, const void* da16, const float* u,
-                                  const void* h16, const float* uprev, const void* gprev,
-                                  const float* mean, const float* rstd, const float* gamma,
-                                  const float* beta, const void* sp1, int b, int n, int w,
-                                  float* dh, void* dh16, float* dsp1, float* dshift,
-                                  float* dgamma, float* dbeta, float* dbias, void* ws,
-                                  size_t ws_bytes, void* stream) {
+                                  const void* h16, const float* hbias, const float* uprev,
+                                  const void* gprev, const float* mean, const float* rstd,
+                                  const float* gamma, const float* beta, const void* sp1, int b,
+                                  int n, int w, float* dh, void* dh16, float* dsp1, float* dshift,
+                                  float* dgamma, float* dbeta, float* dbias, float* dbias_b,
+                                  void* ws, size_t ws_bytes, void* stream) {
   PCFM_CHECK_ARG(film_ok(b, n, w), "head_film_bwd: bad shape b=%d n=%d w=%d", b, n, w);
   PCFM_CHECK_ARG(h16 != nullptr || (uprev != nullptr && gprev != nullptr),
                  "head_film_bwd: need h16 or (uprev, gprev)");
   PCFM_CHECK_ARG(ws_bytes >= pcfm_head_bwd_workspace_bytes(b, n, w),
                  "head_film_bwd: workspace %zu < %zu bytes", ws_bytes,
                  pcfm_head_bwd_workspace_bytes(b, n, w));
-  return launch_bwd<true>(dh_next, da16, u, h16, uprev, gprev, mean, rstd, gamma, beta, sp1, b,
-                          n, w, dh, dh16, dsp1, dshift, dgamma, dbeta, dbias, ws,
-                          (hipStream_t)stream);
+  return launch_bwd<true>(dh_next, da16, u, h16, uprev, gprev, mean, rstd, gamma, beta, sp1,
+                          h16 != nullptr ? hbias : nullptr, b, n, w, dh, dh16, dsp1, dshift,
+                          dgamma, dbeta, dbias, dbias_b, ws, (hipStream_t)stream);
 }
 
 extern "C" int pcfm_head_silu_bwd(const void* da16, const float* uprev, const void* gprev, int b,
@@ -425,6 +448,6 @@ extern "C" int pcfm_head_silu_bwd(const void* da16, const float* uprev, const vo
                  "head_silu_bwd: workspace %zu < %zu bytes", ws_bytes,
                  pcfm_head_bwd_workspace_bytes(b, n, w));
   return launch_bwd<false>(nullptr, da16, nullptr, nullptr, uprev, gprev, nullptr, nullptr,
-                           nullptr, nullptr, nullptr, b, n, w, dh, dh16, nullptr, nullptr,
-                           nullptr, nullptr, dbias, ws, (hipStream_t)stream);
+                           nullptr, nullptr, nullptr, nullptr, b, n, w, dh, dh16, nullptr, nullptr,
+                           nullptr, nullptr, dbias, nullptr, ws, (hipStream_t)stream);
 }

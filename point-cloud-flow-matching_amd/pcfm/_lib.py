@@ -73,12 +73,12 @@ SIGNATURES = {
     "pcfm_rows_wgrad_bf16": (_I, [_P, _I, _P, _I, _L, _I, _I, _P, _P, _Z, _P]),
     "pcfm_rows_max_workspace_bytes": (_Z, [_I, _I, _I]),
     "pcfm_rows_max_bf16": (_I, [_P, _I, _I, _I, _P, _P, _P, _Z, _P]),
-    "pcfm_head_film_fwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _F, _P, _P, _P, _P,
-                                _P]),
+    "pcfm_head_film_fwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _F, _P, _P, _P,
+                                   _P, _P]),
     "pcfm_head_silu_fwd": (_I, [_P, _P, _I, _I, _I, _P, _P]),
     "pcfm_head_bwd_workspace_bytes": (_Z, [_I, _I, _I]),
-    "pcfm_head_film_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _P, _P,
-                                _P, _P, _P, _P, _P, _P, _Z, _P]),
+    "pcfm_head_film_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I,
+                                   _P, _P, _P, _P, _P, _P, _P, _P, _P, _Z, _P]),
     "pcfm_head_silu_bwd": (_I, [_P, _P, _P, _I, _I, _I, _P, _P, _P, _P, _Z, _P]),
     "pcfm_bn_workspace_bytes": (_Z, [_I, _I, _I]),
     "pcfm_bn_act_fwd": (_I, [_P, _P, _P, _I, _I, _I, _F, _F, _F, _P, _P, _P, _P, _P, _P, _Z,
@@ -92,7 +92,7 @@ SIGNATURES = {
                                   _P, _P, _Z, _P]),
 }
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 _lock = threading.Lock()
 _lib = None

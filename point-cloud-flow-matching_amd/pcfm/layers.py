@@ -74,16 +74,19 @@ _PER_BLOCK = 6  # ln_weight, ln_bias, sp1, shift, weight16, bias16
 
 class _HeadTrunkBF16(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, n, eps, x16, w_in, b_in, w_out, b_out, *blk):
+    def forward(ctx, n, eps, x16, w_in, hb, w_out, b_out, *blk):
+        # hb (B, W) fp32: the input Linear's bias plus its embedding columns applied
+        # to the per-batch embedding, added to h1 inside the first FiLM kernel
         from pcfm import ops
         nb = len(blk) // _PER_BLOCK
-        h1 = F.linear(x16, w_in, b_in)
+        h1 = F.linear(x16, w_in)
+        hb = hb.contiguous()
         us, gs, as_, stats = [], [], [], []
         u = g = None
         for k in range(nb):
             lw, lb, sp1, sh, wk, bk = blk[_PER_BLOCK * k:_PER_BLOCK * (k + 1)]
             u, a, mean, rstd = ops.head_film_fwd(h1 if k == 0 else None, u, g, lw, lb, sp1, sh,
-                                                 n, eps)
+                                                 n, eps, hbias=hb if k == 0 else None)
             g = F.linear(a, wk, bk)
             us.append(u)
             gs.append(g)
@@ -92,7 +95,7 @@ class _HeadTrunkBF16(torch.autograd.Function):
         a_out = ops.head_silu_fwd(u, g, n)
         out = F.linear(a_out, w_out, b_out)
         ctx.n, ctx.eps, ctx.nb = n, eps, nb
-        ctx.save_for_backward(x16, w_in, h1, w_out, a_out, *us, *gs, *as_, *stats, *blk)
+        ctx.save_for_backward(x16, w_in, h1, hb, w_out, a_out, *us, *gs, *as_, *stats, *blk)
         return out
 
     @staticmethod
@@ -100,10 +103,10 @@ class _HeadTrunkBF16(torch.autograd.Function):
         from pcfm import ops
         n, nb = ctx.n, ctx.nb
         sv = ctx.saved_tensors
-        x16, w_in, h1, w_out, a_out = sv[:5]
-        us, gs, as_ = sv[5:5 + nb], sv[5 + nb:5 + 2 * nb], sv[5 + 2 * nb:5 + 3 * nb]
-        stats = sv[5 + 3 * nb:5 + 5 * nb]
-        blk = sv[5 + 5 * nb:]
+        x16, w_in, h1, hb, w_out, a_out = sv[:6]
+        us, gs, as_ = sv[6:6 + nb], sv[6 + nb:6 + 2 * nb], sv[6 + 2 * nb:6 + 3 * nb]
+        stats = sv[6 + 3 * nb:6 + 5 * nb]
+        blk = sv[6 + 5 * nb:]
         gout = gout.contiguous()
         d_w_out = ops.rows_wgrad_bf16(gout, a_out)
         d_b_out = gout.sum(0)
@@ -117,19 +120,21 @@ class _HeadTrunkBF16(torch.autograd.Function):
             d_blk[_PER_BLOCK * k + 5] = dbias.to(torch.bfloat16)
             da = torch.mm(dh16, wk)
             first = k == 0
-            dh, dh16, dsp1, dshift, dgamma, dbeta, dbias = ops.head_film_bwd(
+            res = ops.head_film_bwd(
                 dh, da, us[k], h1 if first else None, None if first else us[k - 1],
                 None if first else gs[k - 1], stats[2 * k], stats[2 * k + 1], lw, lb, sp1, n,
-                want_dh=not first)
+                want_dh=not first, hbias=hb if first else None)
+            dh, dh16, dsp1, dshift, dgamma, dbeta, dbias = res[:7]
+            if first:
+                d_hb = res[7]
             d_blk[_PER_BLOCK * k] = dgamma
             d_blk[_PER_BLOCK * k + 1] = dbeta
             d_blk[_PER_BLOCK * k + 2] = dsp1.to(torch.bfloat16)
             d_blk[_PER_BLOCK * k + 3] = dshift.to(torch.bfloat16)
-        # dh16 = dL/dh_1 (bf16 output of the input Linear)
+        # dh16 = dL/dh_1 (bf16 output of the input Linear); d hb per batch
         d_w_in = ops.rows_wgrad_bf16(dh16, x16)
-        d_b_in = dbias.to(torch.bfloat16)
         dx = torch.mm(dh16, w_in)
-        return (None, None, dx, d_w_in, d_b_in, d_w_out, d_b_out, *d_blk)
+        return (None, None, dx, d_w_in, d_hb, d_w_out, d_b_out, *d_blk)
 
 
 def fused_trunk_supported(trunk, h: torch.Tensor, emb: torch.Tensor, n: int) -> bool:
@@ -154,7 +159,14 @@ def fused_trunk_supported(trunk, h: torch.Tensor, emb: torch.Tensor, n: int) -> 
 
 
 def fused_trunk(trunk, h: torch.Tensor, emb: torch.Tensor, n: int) -> torch.Tensor:
-    """trunk._run_trunk(h, emb, n) through _HeadTrunkBF16 (same math, autocast casts)."""
+    """trunk._run_trunk(h, emb, n) through _HeadTrunkBF16 (same math, autocast casts).
+
+    h holds the per-point input columns only; the trunk input of the reference is
+    cat([h, emb broadcast over the points]) (models.py:135, 594).  The embedding
+    columns of the input Linear are constant along the points, so they and the
+    bias become one per-batch row hb = W_emb bf16(emb) + b (fp32 accumulation of
+    the same bf16 products), added to h1 in the first FiLM kernel: the input GEMM
+    runs over the point columns only (K = 70 instead of 326)."""
     dt = torch.bfloat16
     blk = []
     for seq, film in zip(trunk.blocks, trunk.films):
@@ -164,10 +176,15 @@ def fused_trunk(trunk, h: torch.Tensor, emb: torch.Tensor, n: int) -> torch.Tens
                 shift.to(dt).contiguous(), seq[1].weight.to(dt), seq[1].bias.to(dt)]
     eps = trunk.films[0].norm.eps if len(trunk.films) else 1e-5
     lin_in, lin_out = trunk.input, trunk.out[1]
-    x16 = h.to(dt).contiguous()
+    k = h.shape[1]
+    kp = (k + 7) // 8 * 8  # 16-B rows for the GEMM operands
+    x16 = F.pad(h.to(dt), (0, kp - k))
+    w_pts = F.pad(lin_in.weight[:, :k].to(dt), (0, kp - k))
     with torch.autocast("cuda", enabled=False):
-        return _HeadTrunkBF16.apply(n, float(eps), x16, lin_in.weight.to(dt), lin_in.bias.to(dt),
-                                    lin_out.weight.to(dt), lin_out.bias.to(dt), *blk)
+        hb = F.linear(emb.to(dt).float(), lin_in.weight[:, k:].to(dt).float(),
+                      lin_in.bias.to(dt).float())
+        return _HeadTrunkBF16.apply(n, float(eps), x16, w_pts, hb, lin_out.weight.to(dt),
+                                    lin_out.bias.to(dt), *blk)
 
 
 class _RowsMax(torch.autograd.Function):

@@ -110,8 +110,13 @@ class _PointTrunk(_TimeCondEmbed):
     fused = True
 
     def _run_trunk(self, h: torch.Tensor, emb: torch.Tensor, n: int) -> torch.Tensor:
+        """The trunk on input cat([h, emb broadcast over the n points]); h is the
+        (B*n, k) per-point part (models.py:135, 594 build the concat)."""
         if self.fused and fused_trunk_supported(self, h, emb, n):
             return fused_trunk(self, h, emb, n)
+        b = emb.shape[0]
+        h = torch.cat([h.reshape(b, n, -1), emb[:, None, :].expand(b, n, -1).to(h.dtype)],
+                      dim=-1).reshape(b * n, -1)
         if self.film_per_point:
             film_emb = emb[:, None, :].expand(emb.shape[0], n, -1).reshape(-1, emb.shape[-1])
         else:
@@ -144,8 +149,7 @@ class VelocityNet(_PointTrunk):
         b, n, d = x.shape
         assert d == self.point_dim, f"VelocityNet expected point_dim={self.point_dim}, got {d}"
         emb = self._embed_t(t, x.dtype) + self._cond_embed(x, cond, cond_drop_mask)
-        h = torch.cat([x, emb[:, None, :].expand(b, n, -1)], dim=-1).reshape(b * n, -1)
-        return self._run_trunk(h, emb, n).reshape(b, n, self.point_dim)
+        return self._run_trunk(x.reshape(b * n, -1), emb, n).reshape(b, n, self.point_dim)
 
     @torch.no_grad()
     def guided_velocity(self, x, t, cond, guidance_scale: float = 0.0):
@@ -473,7 +477,7 @@ class VelocityNetWithContext(_PointTrunk):
         b, n, _ = x.shape
         assert ctx.shape[:2] == (b, n), f"ctx shape mismatch: {tuple(ctx.shape)} vs {(b, n, '*')}"
         emb = self._embed_t(t, x.dtype) + self._cond_embed(x, cond, cond_drop_mask)
-        h = torch.cat([x, ctx, emb[:, None, :].expand(b, n, -1)], dim=-1).reshape(b * n, -1)
+        h = torch.cat([x, ctx.to(x.dtype)], dim=-1).reshape(b * n, -1)
         return self._run_trunk(h, emb, n).reshape(b, n, self.point_dim)
 
 

@@ -696,8 +696,9 @@ def _p(t):
     return t.data_ptr() if t is not None else None
 
 
-def head_film_fwd(h16, uprev, gprev, gamma, beta, sp1, shift, n: int, eps: float):
-    """One FiLM block row pass (include/pcfm.h pcfm_head_film_fwd).
+def head_film_fwd(h16, uprev, gprev, gamma, beta, sp1, shift, n: int, eps: float, hbias=None):
+    """One FiLM block row pass (include/pcfm.h pcfm_head_film_fwd); hbias (B, W) f32
+    is the per-batch input bias added to h16.
     Returns u f32 (R, W), a bf16 (R, W), mean f32 (R,), rstd f32 (R,)."""
     ref = h16 if h16 is not None else uprev
     rows, w = ref.shape
@@ -708,7 +709,8 @@ def head_film_fwd(h16, uprev, gprev, gamma, beta, sp1, shift, n: int, eps: float
     mean = torch.empty((rows,), dtype=torch.float32, device=dev)
     rstd = torch.empty((rows,), dtype=torch.float32, device=dev)
     with _timed("head_film_fwd", rows * w * (2 if h16 is not None else 6) + rows * w * 6, ref):
-        _lib.call("pcfm_head_film_fwd", _p(h16), _p(uprev), _p(gprev), _p(gamma), _p(beta),
+        _lib.call("pcfm_head_film_fwd", _p(h16), _p(hbias), _p(uprev), _p(gprev), _p(gamma),
+                  _p(beta),
                   _p(sp1), _p(shift), b, n, w, float(eps), _p(u), _p(a), _p(mean), _p(rstd),
                   _stream(ref))
     return u, a, mean, rstd
@@ -723,24 +725,28 @@ def head_silu_fwd(uprev, gprev, n: int):
 
 
 def head_film_bwd(dh_next, da16, u, h16, uprev, gprev, mean, rstd, gamma, beta, sp1, n: int,
-                  want_dh: bool):
+                  want_dh: bool, hbias=None):
     """Returns dh f32 (or None), dh16 bf16, dsp1 f32 (B, W), dshift f32 (B, W),
-    dgamma f32 (W,), dbeta f32 (W,), dbias f32 (W,)."""
+    dgamma f32 (W,), dbeta f32 (W,), dbias f32 (W,), and with hbias (h16's per-batch
+    input bias) its gradient dbias_b f32 (B, W) as an 8th value."""
     rows, w = da16.shape
     b = rows // n
     dev = da16.device
     dh = torch.empty((rows, w), dtype=torch.float32, device=dev) if want_dh else None
     dh16 = torch.empty((rows, w), dtype=torch.bfloat16, device=dev)
-    small = torch.empty((2 * b + 3, w), dtype=torch.float32, device=dev)
+    small = torch.empty((3 * b + 3, w), dtype=torch.float32, device=dev)
     dsp1, dshift = small[:b], small[b:2 * b]
     dgamma, dbeta, dbias = small[2 * b], small[2 * b + 1], small[2 * b + 2]
+    dbias_b = small[2 * b + 3:] if hbias is not None else None
     ws = _workspace(_lib.query("pcfm_head_bwd_workspace_bytes", b, n, w), da16)
     with _timed("head_film_bwd", rows * w * (4 + 2 + 4 + (2 if h16 is not None else 6)
                                              + (4 if want_dh else 0) + 2), da16):
-        _lib.call("pcfm_head_film_bwd", _p(dh_next), _p(da16), _p(u), _p(h16), _p(uprev),
-                  _p(gprev), _p(mean), _p(rstd), _p(gamma), _p(beta), _p(sp1), b, n, w, _p(dh),
-                  _p(dh16), _p(dsp1), _p(dshift), _p(dgamma), _p(dbeta), _p(dbias), _p(ws),
-                  ws.numel(), _stream(da16))
+        _lib.call("pcfm_head_film_bwd", _p(dh_next), _p(da16), _p(u), _p(h16), _p(hbias),
+                  _p(uprev), _p(gprev), _p(mean), _p(rstd), _p(gamma), _p(beta), _p(sp1), b, n,
+                  w, _p(dh), _p(dh16), _p(dsp1), _p(dshift), _p(dgamma), _p(dbeta), _p(dbias),
+                  _p(dbias_b), _p(ws), ws.numel(), _stream(da16))
+    if hbias is not None:
+        return dh, dh16, dsp1, dshift, dgamma, dbeta, dbias, dbias_b
     return dh, dh16, dsp1, dshift, dgamma, dbeta, dbias
 
 
