@@ -38,6 +38,8 @@ import torch.distributed as dist  # noqa: E402
 METRIC = "train-step points/sec (B=8, N=20000, xyz+rgb) at 1/2/4/8 MI355X; Chamfer ms"
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 BF16_DENSE_TF = 2500.0          # MI355X dense bf16 MFMA peak (no sparsity)
+VOXEL_OPS = ("avg_voxelize_fwd", "avg_voxelize_bwd", "trilinear_devoxelize_fwd",
+             "trilinear_devoxelize_bwd")  # the PVConv scatter/gather
 BF16X3_PEAK_TF = BF16_DENSE_TF / 3  # fp32-equivalent peak of the 3-product split
 H100_DERIVED_PTS = 1.88e6       # 25 s/epoch at <= 293 steps/epoch (derived)
 # HBM bytes per launch of the voxel ops from rocprofv3 PMC passes (tools/op_traffic.py)
@@ -72,6 +74,8 @@ def parse():
     p.add_argument("--cpu-batch", type=int, default=2, help="CPU baseline sample batch")
     p.add_argument("--no-chamfer", action="store_true")
     p.add_argument("--no-event-timing", action="store_true")
+    p.add_argument("--profile-steps", type=int, default=2,
+                   help="untimed steps with HIP events around every op (per-kernel table)")
     return p.parse_args()
 
 
@@ -162,8 +166,29 @@ def main():
         if rank == 0:
             log(f"warmup step {i + 1}/{args.warmup} done ({time.perf_counter() - t_w:.1f} s)")
 
+    # Per-op HIP-event profile over a few untimed steps: the per-kernel table, and
+    # the choice of the roofline kernels.  Events around every op cost ~1.3 ms of
+    # host time per step, so the timed region below records only those kernels.
+    full, prof_steps = {}, 0
+    roof_ops = set()
+    if not args.no_event_timing:
+        prof_steps = max(1, args.profile_steps)
+        ops.timer.reset()
+        ops.timer.only = None
+        ops.timer.enabled = True
+        for i in range(prof_steps):
+            tr.step(batch, epoch)
+        torch.cuda.synchronize(dev)
+        ops.timer.enabled = False
+        full = ops.timer.summary()
+        if full:
+            roof_ops.add(max(full, key=lambda k: full[k]["ms"]))
+            hbm = [k for k in full if k in VOXEL_OPS]
+            if hbm:
+                roof_ops.add(max(hbm, key=lambda k: full[k]["ms"]))
     ops.timer.reset()
-    ops.timer.enabled = not args.no_event_timing
+    ops.timer.only = roof_ops
+    ops.timer.enabled = bool(roof_ops)
     if ddp:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -188,14 +213,14 @@ def main():
         points = world * cfg.batch_size * cfg.num_points * args.steps
         value = points / elapsed
         ms = elapsed * 1e3 / args.steps
-        summary = ops.timer.summary()
+        summary = ops.timer.summary()  # the roofline kernels, live over the timed region
         rate_key = {"hbm": "GBps", "mfma": "TFLOPs_fp32_equiv", "mfma_bf16": "TFLOPs_bf16"}
-        kernels = {k: {"launches_per_step": v["launches"] / args.steps,
-                       "ms_per_step": v["ms"] / args.steps,
+        kernels = {k: {"launches_per_step": v["launches"] / prof_steps,
+                       "ms_per_step": v["ms"] / prof_steps,
                        rate_key[v["kind"]]:
                        (v["amount"] / (v["ms"] * 1e-3) / (1e9 if v["kind"] == "hbm" else 1e12))
                        if v["ms"] > 0 else None}
-                   for k, v in summary.items()}
+                   for k, v in full.items()}
 
         def roof(op):
             d = summary[op]
@@ -228,9 +253,7 @@ def main():
                     "avg_launch_ms": d["ms"] / d["launches"]}
 
         roofline = roof(max(summary, key=lambda k: summary[k]["ms"])) if summary else None
-        voxel_ops = ("avg_voxelize_fwd", "avg_voxelize_bwd", "trilinear_devoxelize_fwd",
-                     "trilinear_devoxelize_bwd")  # the PVConv scatter/gather
-        hbm_ops = [k for k in summary if k in voxel_ops]
+        hbm_ops = [k for k in summary if k in VOXEL_OPS]
         roofline_scatter = roof(max(hbm_ops, key=lambda k: summary[k]["ms"])) if hbm_ops else None
         log(f"{ms:.2f} ms/step, {value / 1e6:.3f} M points/s; losses {loss_p:.4f} {loss_z:.4f}")
         cham = None

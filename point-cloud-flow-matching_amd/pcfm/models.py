@@ -21,7 +21,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from modules.norm_act import gn_film_residual
+from modules.norm_act import bn_act, gn_film_residual
 from modules.pvconv import PVConv
 from modules.shared_mlp import PointwiseConv1d, SharedMLP
 from pcfm.layers import RowsLinear, fused_trunk, fused_trunk_supported, max_over_points
@@ -315,6 +315,9 @@ class _PVStage(nn.Module):
 
     def forward(self, feat: torch.Tensor, coords: torch.Tensor, emb: torch.Tensor):
         f, c = self.proj((feat, coords))
+        return self.run_blocks(f, c, emb)
+
+    def run_blocks(self, f: torch.Tensor, c: torch.Tensor, emb: torch.Tensor):
         for blk in self.blocks:
             f, c = blk((f, c), emb)
         return f, c
@@ -405,6 +408,24 @@ class ContextNet(_TimeCondEmbed):
         c_in = x.new_zeros((x.shape[0], 1)) if cond is None or cond.numel() == 0 else cond
         return F.silu(self.c_proj(c_in))
 
+    def _stem_proj(self, pts: List[torch.Tensor], emb32: torch.Tensor, coords: torch.Tensor):
+        """Stage 1's 1x1 lift of the stem cat([emb broadcast, xyz, rgb]) (models.py:
+        431-441) without building the stem: the embedding columns of the conv act on
+        a per-cloud constant, so W_emb emb + b is a per-cloud bias and the GEMM runs
+        over the 3 or 6 point channels only; then its BatchNorm + ReLU.  None when
+        the layer is not on the bf16x3 path (the caller builds the stem)."""
+        proj = self.stages[0].proj
+        conv, bn = proj.layers[0], proj.layers[1]
+        if not (pts and isinstance(conv, PointwiseConv1d) and conv.bias is not None
+                and conv.x3_ok(coords) and isinstance(proj.layers[2], nn.ReLU)):
+            return None
+        e = self.emb_dim
+        w = conv.weight[:, :, 0]
+        bias_b = torch.addmm(conv.bias, emb32, w[:, :e].t())
+        pts = torch.cat(pts, dim=1).float() if len(pts) > 1 else pts[0].float().contiguous()
+        pre = _PointwiseParts.apply(w[:, e:], bias_b, pts)
+        return bn_act(pre, bn, 0.0)
+
     def _head_pre(self, scales: List[torch.Tensor], g: Optional[torch.Tensor]) -> torch.Tensor:
         """head_pre(cat(scales | g broadcast over points)) (models.py:460-466).
 
@@ -431,18 +452,24 @@ class ContextNet(_TimeCondEmbed):
         b, n, d = x.shape
         coords = x[..., :3].permute(0, 2, 1).contiguous()
         emb = self._embed_t(t, x.dtype) + self._c_emb(x, cond)
-        stem = [emb[:, :, None].expand(b, self.emb_dim, n)]
+        pts = []
         if self.use_xyz:
-            stem.append(coords)
+            pts.append(coords)
         if self.use_rgb and d == 6:
-            stem.append(x[..., 3:].permute(0, 2, 1).contiguous())
-        stem = torch.cat(stem, dim=1)
+            pts.append(x[..., 3:].permute(0, 2, 1).contiguous())
 
         with torch.amp.autocast("cuda", enabled=False):  # the pyramid runs in fp32
-            f, c = stem.float(), coords.float()
+            c = coords.float()
             emb32 = emb.float()
             scales = []
-            for stage in self.stages:
+            f = self._stem_proj(pts, emb32, c)
+            if f is None:  # stem = cat([emb broadcast over the points, xyz, rgb])
+                stem = torch.cat([emb[:, :, None].expand(b, self.emb_dim, n)] + pts, dim=1)
+                f, c = self.stages[0](stem.float(), c, emb32)
+            else:
+                f, c = self.stages[0].run_blocks(f, c, emb32)
+            scales.append(f)
+            for stage in self.stages[1:]:
                 f, c = stage(f, c, emb32)
                 scales.append(f)
             g = self.global_mlp(f.max(dim=-1).values) if self.with_global else None

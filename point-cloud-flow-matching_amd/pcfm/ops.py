@@ -69,7 +69,11 @@ def _workspace(nbytes: int, like: torch.Tensor) -> torch.Tensor:
 class _OpTimer:
     def __init__(self):
         self.enabled = False
+        self.only = None  # None: every op; else the set of op names to time
         self.records = []  # (op, start_event, end_event, amount, kind)
+
+    def on(self, op):
+        return self.enabled and (self.only is None or op in self.only)
 
     def reset(self):
         self.records = []
@@ -97,12 +101,13 @@ class _timed:
         self.op, self.amount, self.kind, self.dev = op, int(amount), kind, like.device
 
     def __enter__(self):
-        if timer.enabled:
+        self.e0 = None
+        if timer.on(self.op):
             self.e0 = torch.cuda.Event(enable_timing=True)
             self.e0.record(torch.cuda.current_stream(self.dev))
 
     def __exit__(self, *exc):
-        if timer.enabled and exc[0] is None:
+        if self.e0 is not None and exc[0] is None:
             e1 = torch.cuda.Event(enable_timing=True)
             e1.record(torch.cuda.current_stream(self.dev))
             timer.records.append((self.op, self.e0, e1, self.amount, self.kind))

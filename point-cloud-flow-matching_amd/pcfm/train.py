@@ -160,21 +160,29 @@ class EMA:
         self.foreach = bool(foreach)
         self.shadow = {k: v.detach().clone() for k, v in model.state_dict().items()}
         self._keys = None
+        self._lists = None  # (model id, shadow list, live tensor list), built once
 
     @torch.no_grad()
     def update(self, model: nn.Module) -> None:
         d = self.decay
+        if self.foreach:
+            # model.state_dict() per step costs ~1 ms of host time, during which the
+            # GPU drains its queue; the live parameter / buffer tensors do not change
+            # identity across steps (in-place optimizer updates), so list them once
+            if self._lists is None or self._lists[0] != id(model):
+                sd = model.state_dict()
+                keys = [k for k, v in sd.items() if v.dtype.is_floating_point]
+                self._lists = (id(model), [self.shadow[k] for k in keys],
+                               [sd[k].detach() for k in keys])
+            _, shadow, cur = self._lists
+            torch._foreach_mul_(shadow, d)
+            torch._foreach_add_(shadow, cur, alpha=1.0 - d)
+            return
         sd = model.state_dict()
         if self._keys is None:
             self._keys = [k for k, v in sd.items() if v.dtype.is_floating_point]
-        if self.foreach:
-            shadow = [self.shadow[k] for k in self._keys]
-            cur = [sd[k].detach() for k in self._keys]
-            torch._foreach_mul_(shadow, d)
-            torch._foreach_add_(shadow, cur, alpha=1.0 - d)
-        else:
-            for k in self._keys:
-                self.shadow[k].mul_(d).add_(sd[k].detach(), alpha=1.0 - d)
+        for k in self._keys:
+            self.shadow[k].mul_(d).add_(sd[k].detach(), alpha=1.0 - d)
 
     def copy_to(self, model: nn.Module) -> None:
         model.load_state_dict(self.shadow, strict=True)

@@ -112,3 +112,51 @@ def test_context_head_pre_parts_matches_concat(ops):
     assert _rel(y, y64.detach().cpu()) < TOL
     for a, ref in zip(grads, refs):
         assert _rel(a, ref.detach().cpu()) < 2 * TOL
+
+
+def test_context_stem_fold_matches_concat(ops, monkeypatch):
+    """ContextNet's stage-1 lift with the embedding columns folded into a per-cloud
+    bias (ContextNet._stem_proj).  (1) The fold itself against the fp64 conv over
+    the built stem cat([emb broadcast, xyz, rgb]), forward and backward.  (2) The
+    whole (training-mode) ContextNet against its module path, forward.  Network-level
+    parameter gradients are not compared: behind training-mode BatchNorms they are
+    sums that cancel (BN's backward sums to zero over the points), so a 1e-7
+    change in the lift's rounding moves them by up to a few percent in either path;
+    (1) checks the fold's own gradients against fp64.)"""
+    from pcfm.models import ContextNet, _PointwiseParts
+    g = torch.Generator(device="cuda").manual_seed(11)
+    b, n, e = 2, 3000, 64
+    pts = torch.randn(b, 6, n, device="cuda", generator=g).requires_grad_(True)
+    emb = torch.randn(b, e, device="cuda", generator=g).requires_grad_(True)
+    w = (torch.randn(128, e + 6, device="cuda", generator=g) / 8).requires_grad_(True)
+    bias = torch.randn(128, device="cuda", generator=g).requires_grad_(True)
+    gy = torch.randn(b, 128, n, device="cuda", generator=g)
+    pre = _PointwiseParts.apply(w[:, e:], torch.addmm(bias, emb, w[:, :e].t()), pts)
+    got = torch.autograd.grad(pre, [pts, emb, w, bias], gy)
+    d = [t.detach().double().requires_grad_(True) for t in (pts, emb, w, bias)]
+    stem = torch.cat([d[1][:, :, None].expand(b, e, n), d[0]], dim=1)
+    ref = torch.nn.functional.conv1d(stem, d[2][:, :, None], d[3])
+    want = torch.autograd.grad(ref, d, gy.double())
+    assert _rel(pre, ref.detach().cpu()) < TOL
+    for a, r in zip(got, want):
+        assert _rel(a, r.detach().cpu()) < TOL
+
+    torch.manual_seed(5)
+    net = ContextNet(6, 1, emb_dim=64, ctx_dim=16, stage_channels=(128, 128, 128),
+                     stage_blocks=(1, 1, 1), stage_res=(8, 8, 8)).cuda().train()
+    with torch.no_grad():
+        net.head_out.weight.normal_(0.0, 0.1)
+    x = torch.randn(b, n, 6, device="cuda")
+    t = torch.rand(b, device="cuda")
+    cond = torch.rand(b, 1, device="cuda")
+    state = {k: v.clone() for k, v in net.state_dict().items()}
+
+    def run():
+        net.load_state_dict(state)
+        with torch.no_grad():
+            return net(x, t, cond)
+
+    o1 = run()
+    monkeypatch.setattr(ContextNet, "_stem_proj", lambda self, *a: None)
+    o0 = run()
+    assert _rel(o1, o0.double().cpu()) < 1e-4
