@@ -317,6 +317,24 @@ size_t pcfm_rows_max_workspace_bytes(int b, int n, int c);
 int pcfm_rows_max_bf16(const void* h, int b, int n, int c, void* values, int* indices, void* ws,
                        size_t ws_bytes, void* stream);
 
+size_t pcfm_rows_colsum_workspace_bytes(int b, long long rows, int c);
+
+/* out f32 [b][c] = sum over r of x[b][r][c], x bf16 (bf16 = 1) or f32 [b][rows][c],
+ * c even and <= 512; deterministic (fixed partial order).  The per-point
+ * Linears' bias gradients and the gradient of a per-cloud row broadcast over
+ * the points (models.py:594-601 t-gate blend). */
+int pcfm_rows_colsum(const void* x, int bf16, int b, long long rows, int c, float* out, void* ws,
+                     size_t ws_bytes, void* stream);
+
+/* ContextNet's t-gate blend (models.py:533-541) fused with head_out's permute:
+ * out f32 [b][n][c] = alpha[b] * head[b][c][n] + (1 - alpha[b]) * glb[b][c];
+ * backward dhead f32 [b][c][n] = alpha[b] * dout[b][n][c] (glb's gradient is
+ * (1 - alpha[b]) * pcfm_rows_colsum(dout)). */
+int pcfm_tgate_fwd(const float* head, const float* glb, const float* alpha, int b, int c, int n,
+                   float* out, void* stream);
+int pcfm_tgate_bwd(const float* dout, const float* alpha, int b, int c, int n, float* dhead,
+                   void* stream);
+
 /* Trunk rows of VelocityNetWithContext / VelocityNet (models.py:62-79 FiLMBlock,
  * :107-116 residual loop), W = 256 or 512 channels, rows = b*n (batch-major).
  * bf16 tensors are passed as void* (raw 16-bit bf16 bits).

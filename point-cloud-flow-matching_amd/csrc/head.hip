@@ -331,8 +331,156 @@ __global__ void __launch_bounds__(256)
 
 constexpr int kMaxParts = 32;
 
+// ---------------------------------------------------------------------------
+// Column sums over the rows of a (B, rows, C) tensor, bf16 or fp32, into fp32
+// (B, C): the bias gradients of the per-point Linears (dY.sum(0)) and the
+// gradient of a per-cloud row broadcast over the points.  Stage 1: block p of
+// batch b sums rows [p*rows/P, (p+1)*rows/P), threads on (row lane, column
+// pair) so every row is one coalesced stream; stage 2 adds the P partials in
+// order (deterministic).
+// ---------------------------------------------------------------------------
+// stage-1 blocks per batch element: >= 256 rows each, ~2048 blocks in all, <= 256
+inline int colsum_parts(int b, long long rows) {
+  const long long want = std::max(1LL, (2048LL + b - 1) / b);
+  return (int)std::max(1LL, std::min({(rows + 255) / 256, want, 256LL}));
+}
+
+template <bool BF16>
+__global__ void __launch_bounds__(256)
+    colsum_part_kernel(const void* __restrict__ x, long long rows, int C, float* __restrict__ part) {
+  const int b = blockIdx.y, p = blockIdx.x, P = gridDim.x;
+  const int pairs = C / 2;
+  const int rl = threadIdx.x / pairs, cp = threadIdx.x % pairs;
+  const int rstep = 256 / pairs;  // pairs <= 256
+  const long long r0 = rows * p / P, r1 = rows * (p + 1) / P;
+  __shared__ float red[256 * 2];
+  float s0 = 0.0f, s1 = 0.0f;
+  if (rl < rstep) {
+    for (long long r = r0 + rl; r < r1; r += rstep) {
+      const size_t o = ((size_t)b * rows + r) * C + 2 * cp;
+      if constexpr (BF16) {
+        const uint32_t q = *reinterpret_cast<const uint32_t*>(
+            reinterpret_cast<const uint16_t*>(x) + o);
+        s0 += __uint_as_float(q << 16);
+        s1 += __uint_as_float(q & 0xFFFF0000u);
+      } else {
+        const float2 q = *reinterpret_cast<const float2*>(reinterpret_cast<const float*>(x) + o);
+        s0 += q.x;
+        s1 += q.y;
+      }
+    }
+  }
+  red[2 * threadIdx.x] = s0;
+  red[2 * threadIdx.x + 1] = s1;
+  __syncthreads();
+  if (threadIdx.x < pairs) {  // row lanes in a fixed order
+    float a0 = 0.0f, a1 = 0.0f;
+    for (int l = 0; l < rstep; ++l) {
+      a0 += red[2 * (l * pairs + threadIdx.x)];
+      a1 += red[2 * (l * pairs + threadIdx.x) + 1];
+    }
+    float* o = part + ((size_t)b * P + p) * C + 2 * threadIdx.x;
+    o[0] = a0;
+    o[1] = a1;
+  }
+}
+
+// grid (ceil(C / 64), B): 4 thread groups take every 4th partial, combined in order
+__global__ void __launch_bounds__(256)
+    colsum_final_kernel(const float* __restrict__ part, int P, int C, float* __restrict__ out) {
+  __shared__ float red[4][64];
+  const int b = blockIdx.y, cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  float s = 0.0f;
+  if (c < C)
+    for (int p = grp; p < P; p += 4) s += part[((size_t)b * P + p) * C + c];
+  red[grp][cl] = s;
+  __syncthreads();
+  if (grp == 0 && c < C) out[(size_t)b * C + c] = ((red[0][cl] + red[1][cl]) + red[2][cl]) + red[3][cl];
+}
+
+// ContextNet's t-gate blend (models.py:533-541) fused with the (B, C, N) ->
+// (B, N, C) permute of head_out:  out[b][n][c] = a[b] * head[b][c][n] +
+// (1 - a[b]) * glb[b][c];  backward dhead[b][c][n] = a[b] * dout[b][n][c].
+// 64 x 64 tiles through LDS; grid (ceil(N/64), ceil(C/64), B), 256 threads.
+template <bool FWD>
+__global__ void __launch_bounds__(256)
+    tgate_kernel(const float* __restrict__ src, const float* __restrict__ glb,
+                 const float* __restrict__ alpha, int C, int N, float* __restrict__ dst) {
+  __shared__ float tile[64][65];
+  const int b = blockIdx.z, n0 = blockIdx.x * 64, c0 = blockIdx.y * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const float a = alpha[b];
+  if (FWD) {  // read head rows (c, n contiguous), write out rows (n, c contiguous)
+    for (int r = ty; r < 64; r += 4) {
+      const int c = c0 + r, n = n0 + tx;
+      tile[r][tx] = (c < C && n < N) ? src[((size_t)b * C + c) * N + n] : 0.0f;
+    }
+    __syncthreads();
+    for (int r = ty; r < 64; r += 4) {
+      const int n = n0 + r, c = c0 + tx;
+      if (n < N && c < C)
+        dst[((size_t)b * N + n) * C + c] =
+            __builtin_fmaf(a, tile[tx][r], (1.0f - a) * glb[(size_t)b * C + c]);
+    }
+  } else {  // read dout rows (n, c contiguous), write dhead rows (c, n contiguous)
+    for (int r = ty; r < 64; r += 4) {
+      const int n = n0 + r, c = c0 + tx;
+      tile[r][tx] = (n < N && c < C) ? src[((size_t)b * N + n) * C + c] : 0.0f;
+    }
+    __syncthreads();
+    for (int r = ty; r < 64; r += 4) {
+      const int c = c0 + r, n = n0 + tx;
+      if (c < C && n < N) dst[((size_t)b * C + c) * N + n] = a * tile[tx][r];
+    }
+  }
+}
+
 }  // namespace
 }  // namespace pcfm
+
+extern "C" int pcfm_tgate_fwd(const float* head, const float* glb, const float* alpha, int b,
+                              int c, int n, float* out, void* stream) {
+  PCFM_CHECK_ARG(b >= 0 && c > 0 && n >= 0 && b < 65536, "tgate_fwd: bad shape b=%d c=%d n=%d", b,
+                 c, n);
+  if (b == 0 || n == 0) return PCFM_OK;
+  hipLaunchKernelGGL(tgate_kernel<true>, dim3(ceil_div(n, 64), ceil_div(c, 64), b), dim3(256), 0,
+                     (hipStream_t)stream, head, glb, alpha, c, n, out);
+  return check_launch("tgate_fwd");
+}
+
+extern "C" int pcfm_tgate_bwd(const float* dout, const float* alpha, int b, int c, int n,
+                              float* dhead, void* stream) {
+  PCFM_CHECK_ARG(b >= 0 && c > 0 && n >= 0 && b < 65536, "tgate_bwd: bad shape b=%d c=%d n=%d", b,
+                 c, n);
+  if (b == 0 || n == 0) return PCFM_OK;
+  hipLaunchKernelGGL(tgate_kernel<false>, dim3(ceil_div(n, 64), ceil_div(c, 64), b), dim3(256), 0,
+                     (hipStream_t)stream, dout, nullptr, alpha, c, n, dhead);
+  return check_launch("tgate_bwd");
+}
+
+extern "C" size_t pcfm_rows_colsum_workspace_bytes(int b, long long rows, int c) {
+  if (b <= 0 || rows < 0 || c <= 0 || c % 2 != 0 || c > 512) return 0;
+  return (size_t)b * colsum_parts(b, rows) * c * sizeof(float);
+}
+
+extern "C" int pcfm_rows_colsum(const void* x, int bf16, int b, long long rows, int c, float* out,
+                                void* ws, size_t ws_bytes, void* stream) {
+  PCFM_CHECK_ARG(pcfm_rows_colsum_workspace_bytes(b, rows, c) > 0 && b < 65536,
+                 "rows_colsum: bad shape b=%d rows=%lld c=%d (c even, <= 512)", b, rows, c);
+  PCFM_CHECK_ARG(ws_bytes >= pcfm_rows_colsum_workspace_bytes(b, rows, c),
+                 "rows_colsum: workspace too small");
+  hipStream_t st = (hipStream_t)stream;
+  float* part = (float*)ws;
+  const int P = colsum_parts(b, rows);
+  if (bf16)
+    hipLaunchKernelGGL(colsum_part_kernel<true>, dim3(P, b), dim3(256), 0, st, x, rows, c, part);
+  else
+    hipLaunchKernelGGL(colsum_part_kernel<false>, dim3(P, b), dim3(256), 0, st, x, rows, c, part);
+  hipLaunchKernelGGL(colsum_final_kernel, dim3(ceil_div(c, 64), b), dim3(256), 0, st,
+                     (const float*)part, P, c, out);
+  return check_launch("rows_colsum");
+}
 
 extern "C" size_t pcfm_rows_max_workspace_bytes(int b, int n, int c) {
   if (b <= 0 || n <= 0 || c <= 0 || c % 2 != 0) return 0;

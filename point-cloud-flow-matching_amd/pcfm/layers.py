@@ -42,7 +42,7 @@ class _RowsLinearBF16(torch.autograd.Function):
                 x2 = x2.contiguous()
             gw = ops.rows_wgrad_bf16(g2, x2)
         if ctx.has_bias and ctx.needs_input_grad[2]:
-            gb = g2.sum(0)
+            gb = ops.rows_colsum(g2).to(g2.dtype) if ops.colsum_ok(g2) else g2.sum(0)
         return gx, gw, gb
 
 
@@ -109,7 +109,7 @@ class _HeadTrunkBF16(torch.autograd.Function):
         blk = sv[6 + 5 * nb:]
         gout = gout.contiguous()
         d_w_out = ops.rows_wgrad_bf16(gout, a_out)
-        d_b_out = gout.sum(0)
+        d_b_out = ops.rows_colsum(gout).to(gout.dtype) if ops.colsum_ok(gout) else gout.sum(0)
         da = torch.mm(gout, w_out)
         dh, dh16, dbias = ops.head_silu_bwd(da, us[-1], gs[-1], n)
         d_blk = [None] * len(blk)

@@ -344,8 +344,33 @@ class _PointwiseParts(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             gw = ops.pointwise_backward_weight_parts(xs, gy)
         if ctx.needs_input_grad[1]:
-            gb = gy.sum(dim=2)
+            bb, cc, nn_ = gy.shape
+            gb = ops.rows_dot(gy.view(bb * cc, nn_), None, 1.0).view(bb, cc)
         return (gw, gb, *gxs)
+
+
+class _TGate(torch.autograd.Function):
+    """ctx (B, N, C) = a[b] * head (B, C, N)^T + (1 - a[b]) * glb[b] (models.py:533-541);
+    the gate a depends on t only (no gradient)."""
+
+    @staticmethod
+    def forward(ctx, head, glb, alpha):
+        from pcfm import ops
+        alpha = alpha.contiguous()
+        ctx.save_for_backward(alpha)
+        return ops.tgate_forward(head.contiguous(), glb.contiguous(), alpha)
+
+    @staticmethod
+    def backward(ctx, dout):
+        from pcfm import ops
+        (alpha,) = ctx.saved_tensors
+        dout = dout.contiguous()
+        dhead = ops.tgate_backward(dout, alpha) if ctx.needs_input_grad[0] else None
+        dglb = None
+        if ctx.needs_input_grad[1]:
+            s = ops.rows_colsum(dout) if ops.colsum_ok(dout) else dout.sum(dim=1)
+            dglb = (1.0 - alpha)[:, None] * s
+        return dhead, dglb, None
 
 
 class ContextNet(_TimeCondEmbed):
@@ -474,11 +499,18 @@ class ContextNet(_TimeCondEmbed):
                 scales.append(f)
             g = self.global_mlp(f.max(dim=-1).values) if self.with_global else None
             h = self.head_act(self.head_norm(self._head_pre(scales, g)))
-            ctx = self.head_out(h).permute(0, 2, 1)
+            ctx = self.head_out(h)
             if self.use_t_gate:
-                ctx_glb = self.ctx_from_emb(emb32)[:, None, :].expand(b, n, -1)
+                glb = self.ctx_from_emb(emb32)
                 alpha = torch.sigmoid(self.t_gate_k * (t.view(b, 1, 1).float() - self.t_gate_tau))
-                ctx = alpha * ctx + (1.0 - alpha) * ctx_glb
+                if ctx.is_cuda and ctx.dtype == torch.float32 and glb.dtype == torch.float32:
+                    # blend + permute in one pass (csrc/head.hip tgate)
+                    ctx = _TGate.apply(ctx, glb, alpha.reshape(b).detach())
+                else:
+                    ctx = alpha * ctx.permute(0, 2, 1) + (1.0 - alpha) * glb[:, None, :].expand(
+                        b, n, -1)
+            else:
+                ctx = ctx.permute(0, 2, 1)
         return ctx.to(x.dtype)
 
 

@@ -701,6 +701,52 @@ def _p(t):
     return t.data_ptr() if t is not None else None
 
 
+def rows_colsum(x: torch.Tensor) -> torch.Tensor:
+    """x (B, R, C) or (R, C), bf16 or fp32 -> fp32 (B, C) / (C,) sums over R
+    (include/pcfm.h pcfm_rows_colsum)."""
+    squeeze = x.dim() == 2
+    x3 = x.unsqueeze(0) if squeeze else x
+    x3 = x3.contiguous()
+    b, rows, c = x3.shape
+    if x3.dtype not in (torch.bfloat16, torch.float32):
+        raise TypeError("rows_colsum: bf16 or fp32 input")
+    out = torch.empty((b, c), dtype=torch.float32, device=x3.device)
+    ws = _workspace(_lib.query("pcfm_rows_colsum_workspace_bytes", b, rows, c), x3)
+    with _timed("rows_colsum", x3.numel() * x3.element_size(), x3):
+        _lib.call("pcfm_rows_colsum", _ptr(x3), int(x3.dtype == torch.bfloat16), b, rows, c,
+                  _ptr(out), _ptr(ws), ws.numel(), _stream(x3))
+    return out[0] if squeeze else out
+
+
+def colsum_ok(x: torch.Tensor) -> bool:
+    c = x.shape[-1]
+    return (x.is_cuda and x.dim() in (2, 3) and x.dtype in (torch.bfloat16, torch.float32)
+            and c % 2 == 0 and 0 < c <= 512)
+
+
+def tgate_forward(head: torch.Tensor, glb: torch.Tensor, alpha: torch.Tensor) -> torch.Tensor:
+    """head (B, C, N), glb (B, C), alpha (B,) fp32 -> (B, N, C) blend."""
+    for tns, nm in ((head, "head"), (glb, "glb"), (alpha, "alpha")):
+        _check(tns, nm, "f")
+    b, c, n = head.shape
+    out = torch.empty((b, n, c), dtype=torch.float32, device=head.device)
+    with _timed("tgate_fwd", 8 * b * c * n, head):
+        _lib.call("pcfm_tgate_fwd", _ptr(head), _ptr(glb), _ptr(alpha), b, c, n, _ptr(out),
+                  _stream(head))
+    return out
+
+
+def tgate_backward(dout: torch.Tensor, alpha: torch.Tensor) -> torch.Tensor:
+    """dout (B, N, C) -> dhead (B, C, N) = alpha[b] * dout^T."""
+    dout = dout.contiguous()
+    _check(dout, "dout", "f")
+    b, n, c = dout.shape
+    dhead = torch.empty((b, c, n), dtype=torch.float32, device=dout.device)
+    with _timed("tgate_bwd", 8 * b * c * n, dout):
+        _lib.call("pcfm_tgate_bwd", _ptr(dout), _ptr(alpha), b, c, n, _ptr(dhead), _stream(dout))
+    return dhead
+
+
 def head_film_fwd(h16, uprev, gprev, gamma, beta, sp1, shift, n: int, eps: float, hbias=None):
     """One FiLM block row pass (include/pcfm.h pcfm_head_film_fwd); hbias (B, W) f32
     is the per-batch input bias added to h16.

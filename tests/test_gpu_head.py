@@ -153,3 +153,37 @@ def test_rows_max_matches_torch(ops, b, n, c):
     v.backward(gv)
     exp = torch.zeros_like(h).scatter_(1, idx.long().unsqueeze(1), gv.unsqueeze(1))
     assert torch.equal(hh.grad, exp)
+
+
+@pytest.mark.parametrize("shape,dtype", [((160000, 128), torch.bfloat16), ((8, 20000, 64), torch.float32),
+                                         ((3, 777, 6), torch.bfloat16), ((1, 5, 512), torch.float32)])
+def test_rows_colsum_matches_sum(ops, shape, dtype):
+    g = torch.Generator(device="cuda").manual_seed(sum(shape))
+    x = torch.randn(*shape, device="cuda", generator=g).to(dtype)
+    got = ops.rows_colsum(x)
+    want = x.double().sum(dim=-2)
+    scale = x.double().abs().sum(dim=-2).max()
+    assert got.shape == want.shape and got.dtype == torch.float32
+    assert ((got.double() - want).abs().max() / scale).item() < 1e-6
+    assert torch.equal(ops.rows_colsum(x), got)  # deterministic
+
+
+def test_tgate_matches_torch(ops):
+    from pcfm.models import _TGate
+    g = torch.Generator(device="cuda").manual_seed(3)
+    b, c, n = 3, 64, 1000
+    head = torch.randn(b, c, n, device="cuda", generator=g).requires_grad_(True)
+    glb = torch.randn(b, c, device="cuda", generator=g).requires_grad_(True)
+    alpha = torch.rand(b, device="cuda", generator=g)
+    out = _TGate.apply(head, glb, alpha)
+    ref_h = head.detach().double().requires_grad_(True)
+    ref_g = glb.detach().double().requires_grad_(True)
+    a = alpha.double().view(b, 1, 1)
+    ref = a * ref_h.permute(0, 2, 1) + (1.0 - a) * ref_g[:, None, :].expand(b, n, c)
+    assert out.shape == (b, n, c) and out.is_contiguous()
+    assert (out.double() - ref).abs().max().item() < 1e-5
+    gy = torch.randn(b, n, c, device="cuda", generator=g)
+    dh, dg = torch.autograd.grad(out, [head, glb], gy)
+    rh, rg = torch.autograd.grad(ref, [ref_h, ref_g], gy.double())
+    assert (dh.double() - rh).abs().max().item() < 1e-5
+    assert ((dg.double() - rg).abs().max() / rg.abs().max()).item() < 1e-5
