@@ -70,6 +70,13 @@ int pcfm_avg_voxelize_fwd(const float* feat, const int* coords, int b, int c, in
 int pcfm_avg_voxelize_bwd(const float* grad_y, const int* ind, const int* cnt, int b,
                           int c, int n, int s, float* grad_x, void* stream);
 
+/* grad_x = avg_voxelize_bwd(grad_y) + add (add f32 [b][c][n]): PVConv's
+ * feature gradient, voxel branch plus point branch (pvconv.py:35-39), in one
+ * gather. */
+int pcfm_avg_voxelize_bwd_add(const float* grad_y, const int* ind, const int* cnt,
+                              const float* add, int b, int c, int n, int s, float* grad_x,
+                              void* stream);
+
 /* Trilinear devoxelization, forward.
  * Replaces trilinear_devoxelize_forward (src/interpolate/trilinear_devox.cpp:18-55)
  * -> trilinear_devoxelize_kernel (trilinear_devox.cu:21-105).

@@ -122,6 +122,20 @@ extern "C" int pcfm_avg_voxelize_bwd(const float* grad_y, const int* ind, const 
                        (hipStream_t)stream, "avg_voxelize_bwd");
 }
 
+// grad_x = avg_voxelize_bwd(grad_y) + add: the voxelization's input gradient
+// summed with the point branch's (PVConv feeds features to both) in the gather
+extern "C" int pcfm_avg_voxelize_bwd_add(const float* grad_y, const int* ind, const int* cnt,
+                                         const float* add, int b, int c, int n, int s,
+                                         float* grad_x, void* stream) {
+  PCFM_CHECK_ARG(b >= 0 && c >= 0 && n >= 0 && s > 0,
+                 "avg_voxelize_bwd_add: bad size b=%d c=%d n=%d s=%d", b, c, n, s);
+  if (c == 0) return PCFM_OK;
+  GatherEpi epi;
+  epi.add = add;
+  return launch_gather(grad_y, grad_x, b, c, s, n, ProvVoxBwd{ind, cnt, n, s},
+                       (hipStream_t)stream, "avg_voxelize_bwd_add", epi);
+}
+
 extern "C" int pcfm_trilinear_devoxelize_fwd(const float* coords, const float* feat, int b, int c,
                                              int n, int r, int training, float* out, int* inds,
                                              float* wgts, void* stream) {

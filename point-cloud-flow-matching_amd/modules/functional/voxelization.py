@@ -6,7 +6,7 @@ from torch.autograd import Function
 
 from modules.functional import backend as _be
 
-__all__ = ["avg_voxelize"]
+__all__ = ["avg_voxelize", "avg_voxelize_tee"]
 
 
 class AvgVoxelization(Function):
@@ -31,3 +31,33 @@ class AvgVoxelization(Function):
 
 
 avg_voxelize = AvgVoxelization.apply
+
+
+class AvgVoxelizationTee(Function):
+    """(grid, features) from features: the voxelization plus a pass-through of its
+    input for PVConv's point branch (pvconv.py:35-39 feeds `features` to both).
+    The backward sums the two gradients inside the voxelization's gather
+    (pcfm_avg_voxelize_bwd_add) instead of a separate add."""
+
+    @staticmethod
+    def forward(ctx, features, coords, resolution):
+        feats = features.contiguous()
+        vox = coords.int().contiguous()
+        b, c = feats.shape[0], feats.shape[1]
+        r = int(resolution)
+        grid, ind, cnt = _be._backend.avg_voxelize_forward(feats, vox, r)
+        ctx.save_for_backward(ind, cnt)
+        return grid.view(b, c, r, r, r), features.view_as(features)
+
+    @staticmethod
+    def backward(ctx, grad_grid, grad_feat):
+        from pcfm import ops
+        ind, cnt = ctx.saved_tensors
+        b, c = grad_grid.shape[0], grad_grid.shape[1]
+        flat = grad_grid.contiguous().view(b, c, -1)
+        if grad_feat is None:
+            return _be._backend.avg_voxelize_backward(flat, ind, cnt), None, None
+        return ops.avg_voxelize_backward_add(flat, ind, cnt, grad_feat), None, None
+
+
+avg_voxelize_tee = AvgVoxelizationTee.apply

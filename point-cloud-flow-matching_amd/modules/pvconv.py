@@ -102,7 +102,13 @@ class PVConv(nn.Module):
 
     def forward(self, inputs):
         features, coords = inputs
-        grid, grid_coords = self.voxelization(features, coords)
+        if (features.is_cuda and features.dtype == torch.float32 and features.requires_grad
+                and torch.is_grad_enabled()):
+            # the point branch reads the tee'd features: its input gradient is added
+            # to the voxelization's inside the voxelization's backward gather
+            grid, grid_coords, features = self.voxelization.forward_tee(features, coords)
+        else:
+            grid, grid_coords = self.voxelization(features, coords)
         layers = self.voxel_layers  # Conv3d, BN3d, LeakyReLU, Conv3d, BN3d, LeakyReLU[, SE3d]
         grid = conv_bn_act(layers[0], layers[1], grid, layers[2].negative_slope)
         grid = conv_bn_act(layers[3], layers[4], grid, layers[5].negative_slope)

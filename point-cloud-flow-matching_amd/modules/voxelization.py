@@ -35,6 +35,14 @@ class Voxelization(nn.Module):
         vox_coords = torch.round(norm_coords).to(torch.int32)
         return F.avg_voxelize(features, vox_coords, self.r), norm_coords
 
+    def forward_tee(self, features, coords):
+        """forward() plus the features passed through for a second consumer, their
+        two gradients summed inside the voxelization's backward gather."""
+        norm_coords = self._grid_coords(coords.detach())
+        vox_coords = torch.round(norm_coords).to(torch.int32)
+        grid, feats = F.avg_voxelize_tee(features, vox_coords, self.r)
+        return grid, norm_coords, feats
+
     def extra_repr(self):
         tail = f", normalized eps = {self.eps}" if self.normalize else ""
         return f"resolution={self.r}{tail}"

@@ -150,6 +150,26 @@ def avg_voxelize_backward(grad_y: torch.Tensor, indices: torch.Tensor, cnt: torc
     return grad_x
 
 
+def avg_voxelize_backward_add(grad_y: torch.Tensor, indices: torch.Tensor, cnt: torch.Tensor,
+                              add: torch.Tensor):
+    """avg_voxelize_backward(grad_y) + add, add (b,c,n) fp32, in one gather."""
+    _check(grad_y, "grad_y", "f")
+    _check(indices, "indices", "i")
+    _check(cnt, "cnt", "i")
+    add = add.contiguous()
+    _check(add, "add", "f")
+    b, c, s = grad_y.shape
+    n = indices.shape[1]
+    if tuple(add.shape) != (b, c, n):
+        raise ValueError("avg_voxelize_backward_add: add must be (B, C, N)")
+    grad_x = torch.empty((b, c, n), dtype=torch.float32, device=grad_y.device)
+    nbytes = 4 * b * (c * s + n + s + 2 * c * n)
+    with _timed("avg_voxelize_bwd", nbytes, grad_y):
+        _lib.call("pcfm_avg_voxelize_bwd_add", _ptr(grad_y), _ptr(indices), _ptr(cnt), _ptr(add),
+                  b, c, n, s, _ptr(grad_x), _stream(grad_y))
+    return grad_x
+
+
 def trilinear_devoxelize_forward(r: int, is_training: bool, coords: torch.Tensor,
                                  features: torch.Tensor):
     """trilinear_devox.cpp:18-55: -> [outs (b,c,n), inds (b,8,n)|(1,), wgts (b,8,n)|(1,)]"""

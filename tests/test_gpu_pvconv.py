@@ -66,3 +66,36 @@ def test_pvconv_se_devox_fused_matches_modules(ops, monkeypatch, cin, cout, r, n
             assert (a - b).abs().max().item() < 1e-3, name
         else:
             assert _rel(a, b) < 1e-4, name
+
+
+def test_pvconv_voxelize_tee_matches_separate_grads(ops, monkeypatch):
+    """The tee'd voxelization (point-branch gradient added inside the voxelization's
+    backward gather) against the module path where autograd adds the two."""
+    import modules.pvconv as pv
+    from modules.voxelization import Voxelization
+    torch.manual_seed(2)
+    mod = pv.PVConv(128, 128, 3, 16, with_se=True, normalize=True).cuda().train()
+    feats = torch.randn(2, 128, 4000, device="cuda")
+    coords = torch.rand(2, 3, 4000, device="cuda")
+    state = {k: v.clone() for k, v in mod.state_dict().items()}
+    gy = torch.randn(2, 128, 4000, device="cuda")
+
+    def run():
+        mod.load_state_dict(state)
+        f = feats.clone().requires_grad_(True)
+        out, _ = mod((f, coords))
+        out.backward(gy)
+        return out.detach(), f.grad
+
+    o1, g1 = run()
+
+    def plain(self, features, coords):
+        grid, nc = self.forward(features, coords)
+        return grid, nc, features
+
+    monkeypatch.setattr(Voxelization, "forward_tee", plain)
+    o0, g0 = run()
+    # the voxelization's scatter sums are order-nondeterministic at the last bit
+    # (segsum.hpp, like the reference's float atomics): compare at fp32 rounding
+    assert _rel(o1, o0) < 1e-4
+    assert _rel(g1, g0) < 1e-4
