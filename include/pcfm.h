@@ -39,7 +39,8 @@ extern "C" {
  * 5: per-point head kernels; 6: conv3d_igemm workspace,
  * split-operand convolution entry points; fused BatchNorm + activation;
  * 7: channel-segmented pointwise GEMMs, SE3d folded into the devoxelization;
- * 8: per-batch input bias of the head FiLM kernels). */
+ * 8: per-batch input bias of the head FiLM kernels; 9: split-K workspace of
+ * pcfm_conv3d_igemm_cl). */
 int pcfm_abi_version(void);
 /* Thread-local text of the last non-zero return code. */
 const char* pcfm_last_error(void);
@@ -224,7 +225,8 @@ int pcfm_conv3d_supported(int b, int cin, int cout, int r);
 int pcfm_conv3d_igemm(const float* x, const void* wsplit, const float* bias, int b, int cin,
                       int cout, int r, float* y, void* ws, size_t ws_bytes, void* stream);
 
-/* Scratch bytes for pcfm_conv3d_igemm (the channels-last bf16 hi/lo copy of x);
+/* Scratch bytes for pcfm_conv3d_igemm (the channels-last bf16 hi/lo copy of x
+ * plus the split-K partials);
  * 0 = unsupported shape (cin % 64 is needed). */
 size_t pcfm_conv3d_igemm_workspace_bytes(int b, int cin, int cout, int r);
 
@@ -237,9 +239,11 @@ size_t pcfm_conv3d_igemm_workspace_bytes(int b, int cin, int cout, int r);
 size_t pcfm_conv3d_split_bytes(int b, int c, int r);
 int pcfm_conv3d_split(const float* x, int b, int c, int r, void* xs, void* stream);
 
-/* pcfm_conv3d_igemm on an already split input xs (= split(x)). */
+/* pcfm_conv3d_igemm on an already split input xs (= split(x)); ws holds the
+ * split-K partials of small grids (pcfm_conv3d_igemm_cl_workspace_bytes). */
+size_t pcfm_conv3d_igemm_cl_workspace_bytes(int b, int cin, int cout, int r);
 int pcfm_conv3d_igemm_cl(const void* xs, const void* wsplit, const float* bias, int b, int cin,
-                         int cout, int r, float* y, void* stream);
+                         int cout, int r, float* y, void* ws, size_t ws_bytes, void* stream);
 
 /* pcfm_conv3d_wgrad on split operands xs = split(x), gys = split(grad_y);
  * same workspace query (pcfm_conv3d_wgrad_workspace_bytes). */

@@ -140,7 +140,7 @@ __global__ void __launch_bounds__(256)
     conv3_igemm_cl_kernel(const uint16_t* __restrict__ xh, const uint16_t* __restrict__ xl,
                           const uint16_t* __restrict__ wh, const uint16_t* __restrict__ wl,
                           const float* __restrict__ bias, float* __restrict__ y, int K, int M,
-                          int R) {
+                          int R, int S, float* __restrict__ part) {
   using T = TileK<TM, TN, KT>;
   __shared__ __attribute__((aligned(16))) uint16_t lds[T::BUF];
   const int V = R * R * R, R2 = R * R;
@@ -154,6 +154,9 @@ __global__ void __launch_bounds__(256)
     id = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + id / 8;
   }
   const int nmt = M / TM, nvt = V / TN;
+  const int items = (int)gridDim.x / S;  // split-K: S K-ranges per output tile, split outermost
+  const int sp = id / items;
+  id -= sp * items;
   const int m0 = (id % nmt) * TM;
   id /= nmt;
   const int v0 = (id % nvt) * TN, b = id / nvt;
@@ -162,7 +165,8 @@ __global__ void __launch_bounds__(256)
   const int wr = w >> 1, wc = w & 1, r = lane & 31, h = lane >> 5;
   const uint16_t* __restrict__ xbh = xh + (size_t)b * V * K;
   const uint16_t* __restrict__ xbl = xl + (size_t)b * V * K;
-  const int nck = K / KT, nsteps = 27 * nck;
+  const int nck = K / KT, nall = 27 * nck;
+  const int s0 = (int)((long long)nall * sp / S), nsteps = (int)((long long)nall * (sp + 1) / S) - s0;
   // chunk q of this thread: row (t + 256 q) / CPR, 8-channel column (t % CPR) * 8
   const int col = (t % T::CPR) * 8;
   int bv[T::QB], bx[T::QB], by[T::QB], bz[T::QB];
@@ -221,17 +225,22 @@ __global__ void __launch_bounds__(256)
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
 
-  load(0);
+  load(s0);
   store(lds);
   __syncthreads();
   for (int s = 0; s < nsteps; ++s) {
-    if (s + 1 < nsteps) load(s + 1);
+    if (s + 1 < nsteps) load(s0 + s + 1);
     tile_mfma_k<TM, TN, KT>(lds, wr, wc, r, h, acc);
     __syncthreads();
     if (s + 1 < nsteps) store(lds);
     __syncthreads();
   }
-  float* __restrict__ yb = y + (size_t)b * M * V;
+  // S == 1: y (+ bias); else this split's partial, summed in split order by
+  // conv3_ksum_kernel (deterministic)
+  const int nb = items / (nmt * nvt);  // batch elements
+  float* __restrict__ yb =
+      S == 1 ? y + (size_t)b * M * V : part + ((size_t)sp * nb + b) * M * V;
+  const bool add_bias = S == 1 && bias != nullptr;
 #pragma unroll
   for (int i = 0; i < T::SI; ++i)
 #pragma unroll
@@ -240,8 +249,33 @@ __global__ void __launch_bounds__(256)
       for (int e = 0; e < 16; ++e) {
         const int m = m0 + wr * (TM / 2) + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
         const int v = v0 + wc * (TN / 2) + j * 32 + r;
-        yb[(size_t)m * V + v] = acc[i][j][e] + (bias != nullptr ? bias[m] : 0.0f);
+        yb[(size_t)m * V + v] = acc[i][j][e] + (add_bias ? bias[m] : 0.0f);
       }
+}
+
+// y[b][m][v] = bias[m] + sum_sp part[sp][b][m][v], float4 per thread
+__global__ void __launch_bounds__(256)
+    conv3_ksum_kernel(const float* __restrict__ part, const float* __restrict__ bias, int S, int M,
+                      int V, long long total4, float* __restrict__ y) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total4) return;
+  const float4* p4 = reinterpret_cast<const float4*>(part);
+  float4 a = p4[i];
+  for (int sp = 1; sp < S; ++sp) {
+    const float4 q = p4[(size_t)sp * total4 + i];
+    a.x += q.x;
+    a.y += q.y;
+    a.z += q.z;
+    a.w += q.w;
+  }
+  if (bias != nullptr) {
+    const float bb = bias[(int)((i * 4 / V) % M)];  // V % 4 == 0: a float4 is one (b, m) row
+    a.x += bb;
+    a.y += bb;
+    a.z += bb;
+    a.w += bb;
+  }
+  reinterpret_cast<float4*>(y)[i] = a;
 }
 
 // ---------------------------------------------------------------------------
@@ -1079,9 +1113,13 @@ static const uint16_t* zero_row() {
   return rows[dev];
 }
 
+static size_t split_bytes_al(int b, int cin, int r) {
+  return ((size_t)2 * b * r * r * r * cin * sizeof(uint16_t) + 255) / 256 * 256;
+}
+
 extern "C" size_t pcfm_conv3d_igemm_workspace_bytes(int b, int cin, int cout, int r) {
   if (!conv3_shape_ok(b, cin, cout, r) || cin % 64 != 0) return 0;
-  return (size_t)2 * b * r * r * r * cin * sizeof(uint16_t);
+  return split_bytes_al(b, cin, r) + pcfm_conv3d_igemm_cl_workspace_bytes(b, cin, cout, r);
 }
 
 extern "C" int pcfm_conv3d_igemm(const float* x, const void* wsplit, const float* bias, int b,
@@ -1095,7 +1133,10 @@ extern "C" int pcfm_conv3d_igemm(const float* x, const void* wsplit, const float
   const size_t need = pcfm_conv3d_igemm_workspace_bytes(b, cin, cout, r);
   PCFM_CHECK_ARG(ws_bytes >= need, "conv3d_igemm: workspace %zu < %zu bytes", ws_bytes, need);
   const int rc = pcfm_conv3d_split(x, b, cin, r, ws, stream);
-  return rc != PCFM_OK ? rc : pcfm_conv3d_igemm_cl(ws, wsplit, bias, b, cin, cout, r, y, stream);
+  const size_t so = split_bytes_al(b, cin, r);
+  return rc != PCFM_OK ? rc
+                       : pcfm_conv3d_igemm_cl(ws, wsplit, bias, b, cin, cout, r, y,
+                                              (uint8_t*)ws + so, ws_bytes - so, stream);
 }
 
 static size_t wgrad_partial_bytes(int b, int cin, int cout, int r) {
@@ -1142,8 +1183,33 @@ extern "C" int pcfm_conv3d_split(const float* x, int b, int c, int r, void* xs, 
   return check_launch("conv3d_split");
 }
 
+// split-K count of the 64 x 64 tile path (small grids: r = 8): enough blocks
+// to fill the chip, >= 8 K-steps each
+static int igemm_splits(int b, int cin, int cout, int r) {
+  const int V = r * r * r;
+  const long long blocks = (long long)(V / 64) * (cout / 64) * b;
+  const long long nall = 27LL * (cin / PCFM_CONV_KT);
+  long long s = std::max(1LL, (4LL * kCUs + blocks - 1) / blocks);
+  s = std::min(s, std::max(1LL, nall / 8));
+  return (int)std::min(s, 8LL);
+}
+
+static bool igemm_big(int b, int cout, int r) {
+  const int V = r * r * r;
+  const long long big_blocks = (long long)(V / 128) * (cout / 128) * b;
+  return big_blocks >= 2 * kCUs;
+}
+
+extern "C" size_t pcfm_conv3d_igemm_cl_workspace_bytes(int b, int cin, int cout, int r) {
+  if (!conv3_shape_ok(b, cin, cout, r)) return 0;
+  if (b == 0 || igemm_big(b, cout, r)) return 1;
+  const int S = igemm_splits(b, cin, cout, r);
+  return S == 1 ? 1 : (size_t)S * b * cout * r * r * r * sizeof(float);
+}
+
 extern "C" int pcfm_conv3d_igemm_cl(const void* xs, const void* wsplit, const float* bias, int b,
-                                    int cin, int cout, int r, float* y, void* stream) {
+                                    int cin, int cout, int r, float* y, void* ws,
+                                    size_t ws_bytes, void* stream) {
   PCFM_CHECK_ARG(conv3_shape_ok(b, cin, cout, r),
                  "conv3d_igemm_cl: unsupported shape b=%d cin=%d cout=%d r=%d", b, cin, cout, r);
   if (b == 0) return PCFM_OK;
@@ -1177,11 +1243,20 @@ extern "C" int pcfm_conv3d_igemm_cl(const void* xs, const void* wsplit, const fl
   if (big_blocks >= 2 * kCUs) {
     hipLaunchKernelGGL((conv3_igemm_cl_kernel<128, 128, PCFM_CONV_KT>),
                        dim3((V / 128) * (cout / 128) * b), dim3(256), 0, st, xh, xl, wh, wh + total,
-                       bias, y, cin, cout, r);
+                       bias, y, cin, cout, r, 1, nullptr);
   } else {
-    hipLaunchKernelGGL((conv3_igemm_cl_kernel<64, 64, PCFM_CONV_KT>),
-                       dim3((V / 64) * (cout / 64) * b), dim3(256), 0, st, xh, xl, wh, wh + total,
-                       bias, y, cin, cout, r);
+    const int S = igemm_splits(b, cin, cout, r);
+    const size_t need = pcfm_conv3d_igemm_cl_workspace_bytes(b, cin, cout, r);
+    PCFM_CHECK_ARG(S == 1 || (ws != nullptr && ws_bytes >= need),
+                   "conv3d_igemm_cl: workspace %zu < %zu bytes", ws_bytes, need);
+    const int items = (V / 64) * (cout / 64) * b;
+    hipLaunchKernelGGL((conv3_igemm_cl_kernel<64, 64, PCFM_CONV_KT>), dim3(items * S), dim3(256),
+                       0, st, xh, xl, wh, wh + total, bias, y, cin, cout, r, S, (float*)ws);
+    if (S > 1) {
+      const long long total4 = (long long)b * cout * V / 4;
+      hipLaunchKernelGGL(conv3_ksum_kernel, dim3((unsigned)ceil_div(total4, 256)), dim3(256), 0,
+                         st, (const float*)ws, bias, S, cout, V, total4, y);
+    }
   }
   return check_launch("conv3d_igemm_cl");
 }

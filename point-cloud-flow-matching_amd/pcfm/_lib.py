@@ -54,7 +54,8 @@ SIGNATURES = {
     "pcfm_conv3d_igemm_workspace_bytes": (_Z, [_I, _I, _I, _I]),
     "pcfm_conv3d_split_bytes": (_Z, [_I, _I, _I]),
     "pcfm_conv3d_split": (_I, [_P, _I, _I, _I, _P, _P]),
-    "pcfm_conv3d_igemm_cl": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P]),
+    "pcfm_conv3d_igemm_cl_workspace_bytes": (_Z, [_I, _I, _I, _I]),
+    "pcfm_conv3d_igemm_cl": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P, _Z, _P]),
     "pcfm_conv3d_wgrad_cl": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, _Z, _P]),
     "pcfm_conv3d_wgrad_workspace_bytes": (_Z, [_I, _I, _I, _I]),
     "pcfm_conv3d_wgrad": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, _Z, _P]),
@@ -97,7 +98,7 @@ SIGNATURES = {
                                   _P, _P, _Z, _P]),
 }
 
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 _lock = threading.Lock()
 _lib = None

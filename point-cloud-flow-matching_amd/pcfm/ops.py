@@ -547,9 +547,10 @@ def conv3d_igemm_split(xs: torch.Tensor, img: torch.Tensor, bias, b: int, cin: i
     transposed weight image)."""
     y = torch.empty((b, cout, r, r, r), dtype=torch.float32, device=xs.device)
     bias_p = _ptr(bias.contiguous()) if bias is not None else None
+    ws = _workspace(_lib.query("pcfm_conv3d_igemm_cl_workspace_bytes", b, cin, cout, r), xs)
     with _timed(op, 54 * b * r ** 3 * cin * cout, xs, "mfma"):
         _lib.call("pcfm_conv3d_igemm_cl", _ptr(xs), _ptr(img), bias_p, b, cin, cout, r, _ptr(y),
-                  _stream(xs))
+                  _ptr(ws), ws.numel(), _stream(xs))
     return y
 
 
