@@ -997,29 +997,39 @@ __global__ void __launch_bounds__(kW3Threads)
       }
 }
 
-// dw[co][ci][tap] = sum_s part[s][tap][co][ci], in split order
+// dw[co][ci][tap] = sum_s part[s][tap][co][ci], in split order.  A block owns
+// 64 consecutive (co, ci) pairs x 27 taps: partial rows are read coalesced
+// (64 pairs of one tap), the [64][27] result goes out through LDS as one
+// contiguous run of dw.  grid = ceil(cout * cin / 64), 256 threads.
 __global__ void __launch_bounds__(256)
     conv3_wgrad_reduce_kernel(const float* __restrict__ part, int cout, int cin, int S,
                               float* __restrict__ dw) {
-  const size_t total = (size_t)27 * cout * cin;
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;  // dw index
-  if (i >= total) return;
-  const int tap = (int)(i % 27);
-  const size_t cc = i / 27;  // co * cin + ci
-  const float* p = part + (size_t)tap * cout * cin + cc;
-  const size_t ps = total;
-  float sum = 0.0f;
-  int q = 0;
-  for (; q + 4 <= S; q += 4) {
-    const float a0 = p[(size_t)q * ps], a1 = p[(size_t)(q + 1) * ps];
-    const float a2 = p[(size_t)(q + 2) * ps], a3 = p[(size_t)(q + 3) * ps];
-    sum = sum + a0;
-    sum = sum + a1;
-    sum = sum + a2;
-    sum = sum + a3;
+  __shared__ float tile[64 * 27];
+  const size_t pairs = (size_t)cout * cin;
+  const size_t cc0 = (size_t)blockIdx.x * 64;
+  const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const size_t cc = cc0 + cl;
+  const size_t ps = 27 * pairs;  // one split's partial
+  for (int tap = grp; tap < 27; tap += 4) {
+    float sum = 0.0f;
+    if (cc < pairs) {
+      const float* p = part + (size_t)tap * pairs + cc;
+      int q = 0;
+      for (; q + 4 <= S; q += 4) {
+        const float a0 = p[(size_t)q * ps], a1 = p[(size_t)(q + 1) * ps];
+        const float a2 = p[(size_t)(q + 2) * ps], a3 = p[(size_t)(q + 3) * ps];
+        sum = sum + a0;
+        sum = sum + a1;
+        sum = sum + a2;
+        sum = sum + a3;
+      }
+      for (; q < S; ++q) sum = sum + p[(size_t)q * ps];
+    }
+    tile[cl * 27 + tap] = sum;
   }
-  for (; q < S; ++q) sum = sum + p[(size_t)q * ps];
-  dw[i] = sum;
+  __syncthreads();
+  const size_t n = (min(pairs, cc0 + 64) - cc0) * 27;
+  for (size_t e = threadIdx.x; e < n; e += 256) dw[cc0 * 27 + e] = tile[e];
 }
 
 #ifndef PCFM_WGRAD_OCC
@@ -1285,8 +1295,7 @@ extern "C" int pcfm_conv3d_wgrad_cl(const void* xs, const void* gys, int b, int 
                        xh + (size_t)b * V * cin, gh, gh + (size_t)b * V * cout, b, cin, cout, r, S,
                        (float*)ws);
   }
-  const size_t total = (size_t)27 * cout * cin;
-  hipLaunchKernelGGL(conv3_wgrad_reduce_kernel, dim3(ceil_div((long long)total, 256)), dim3(256),
-                     0, st, (const float*)ws, cout, cin, S, grad_w);
+  hipLaunchKernelGGL(conv3_wgrad_reduce_kernel, dim3(ceil_div((long long)cout * cin, 64)),
+                     dim3(256), 0, st, (const float*)ws, cout, cin, S, grad_w);
   return check_launch("conv3d_wgrad_cl");
 }

@@ -180,11 +180,18 @@ __global__ void __launch_bounds__(256)
 __global__ void __launch_bounds__(256)
     rows_wgrad_reduce_kernel(const float* __restrict__ part, size_t total, int S,
                              uint16_t* __restrict__ out) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= total) return;
+  // 64 outputs per block, 4 thread groups over the splits, fixed combine order
+  __shared__ float red[4][64];
+  const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const size_t i = (size_t)blockIdx.x * 64 + cl;
   float sum = 0.0f;
-  for (int q = 0; q < S; ++q) sum = sum + part[(size_t)q * total + i];
-  out[i] = __builtin_bit_cast(uint16_t, (__bf16)sum);
+  if (i < total)
+    for (int q = grp; q < S; q += 4) sum = sum + part[(size_t)q * total + i];
+  red[grp][cl] = sum;
+  __syncthreads();
+  if (grp == 0 && i < total)
+    out[i] = __builtin_bit_cast(
+        uint16_t, (__bf16)(((red[0][cl] + red[1][cl]) + red[2][cl]) + red[3][cl]));
 }
 
 int rows_wgrad_splits(long long R, int M, int N) {
@@ -253,7 +260,7 @@ extern "C" int pcfm_rows_wgrad_bf16(const void* a, int lda, const void* b, int l
   PCFM_ROWS_LAUNCH(0, 1)
   PCFM_ROWS_LAUNCH(0, 0)
 #undef PCFM_ROWS_LAUNCH
-  hipLaunchKernelGGL(rows_wgrad_reduce_kernel, dim3(ceil_div((long long)total, 256)), dim3(256),
+  hipLaunchKernelGGL(rows_wgrad_reduce_kernel, dim3(ceil_div((long long)total, 64)), dim3(256),
                      0, st, (const float*)ws, total, S, (uint16_t*)out);
   return check_launch("rows_wgrad_bf16");
 }

@@ -380,11 +380,17 @@ __global__ void __launch_bounds__(256)
 __global__ void __launch_bounds__(256)
     pw_wgrad_reduce_kernel(const float* __restrict__ part, size_t total, int S,
                            float* __restrict__ dw) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= total) return;
+  // 64 outputs per block; 4 thread groups take every 4th split, combined in
+  // group order (deterministic), so a thread chains S / 4 dependent adds
+  __shared__ float red[4][64];
+  const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const size_t i = (size_t)blockIdx.x * 64 + cl;
   float sum = 0.0f;
-  for (int q = 0; q < S; ++q) sum = sum + part[(size_t)q * total + i];
-  dw[i] = sum;
+  if (i < total)
+    for (int q = grp; q < S; q += 4) sum = sum + part[(size_t)q * total + i];
+  red[grp][cl] = sum;
+  __syncthreads();
+  if (grp == 0 && i < total) dw[i] = ((red[0][cl] + red[1][cl]) + red[2][cl]) + red[3][cl];
 }
 
 int pw_wgrad_splits(int B, int cin, int cout, int N) {
@@ -501,7 +507,7 @@ static int pw_wgrad_launch(const Parts& x, const float* grad_y, int b, int cin, 
   const int tiles = ((cout + 127) / 128) * ((cin + 127) / 128);
   hipLaunchKernelGGL(pw_wgrad_kernel, dim3(tiles, S), dim3(256), 0, st, x, grad_y, b, cin, cout,
                      n, S, (float*)ws);
-  hipLaunchKernelGGL(pw_wgrad_reduce_kernel, dim3(ceil_div((long long)total, 256)), dim3(256), 0,
+  hipLaunchKernelGGL(pw_wgrad_reduce_kernel, dim3(ceil_div((long long)total, 64)), dim3(256), 0,
                      st, (const float*)ws, total, S, grad_w);
   return check_launch("pointwise_wgrad");
 }
