@@ -432,6 +432,16 @@ int pcfm_gn_film_res_bwd(const float* dout, const float* x, const float* w, cons
                          int n, int groups, float* dx, float* dw, float* dbias, float* dgamma,
                          float* dbeta, void* ws, size_t ws_bytes, void* stream);
 
+/* SiLU(GroupNorm(x; w, bias, groups, eps)) over x f32 [b][c][n] (ContextNet's
+ * head_norm + head_act, models.py:460-466); mean/rstd f32 [b][groups]; same
+ * workspace as pcfm_gn_film_res_*.  Backward: dx, dw, dbias from dout. */
+int pcfm_gn_silu_fwd(const float* x, const float* w, const float* bias, int b, int c, int n,
+                     int groups, float eps, float* out, float* mean, float* rstd, void* ws,
+                     size_t ws_bytes, void* stream);
+int pcfm_gn_silu_bwd(const float* dout, const float* x, const float* w, const float* bias,
+                     const float* mean, const float* rstd, int b, int c, int n, int groups,
+                     float* dx, float* dw, float* dbias, void* ws, size_t ws_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -290,24 +290,39 @@ __global__ void __launch_bounds__(256)
 // makes the ds_read_b128 fragment reads conflict-free (64-B rows).  A
 // neighbour outside the grid reads from a zero row (the padding).
 // ---------------------------------------------------------------------------
-constexpr int kGM = 128, kGN = 256, kGK = 32, kGStages = 3;
-constexpr int kGA = kGM * kGK * 2;               // bytes per A image (hi or lo)
-constexpr int kGB = kGN * kGK * 2;               // bytes per B image
-constexpr int kGStage = 2 * kGA + 2 * kGB;       // 48 KiB
+constexpr int kGM = 128, kGN = 256, kGStages = 3;
 
-__device__ __forceinline__ int gswz(int row) { return (row >> 2) & 3; }
+// K-step geometry of the LDS-DMA kernel: KT = 32 (64-B rows, 48 KiB stages,
+// one block per CU) or KT = 16 (32-B rows, 24 KiB stages, two blocks per CU)
+template <int KT>
+struct GK {
+  static constexpr int RB = KT * 2;            // bytes per LDS row (hi or lo)
+  static constexpr int CPR = RB / 16;          // 16-B chunks per row
+  static constexpr int RPP = 1024 / RB;        // rows per 1-KiB LDS-DMA piece
+  static constexpr int A = kGM * RB, B = kGN * RB;  // bytes per image
+  static constexpr int STAGE = 2 * A + 2 * B;
+  static constexpr int APW = 2 * A / 1024 / 8, BPW = 2 * B / 1024 / 8;  // pieces per wave
+  static constexpr int API = A / 1024, BPI = B / 1024;                  // pieces per image
+  // physical chunk p of row r holds logical chunk p ^ swz(r): conflict-free
+  // ds_read_b128 fragment reads
+  static __device__ __forceinline__ int swz(int row) {
+    return KT == 32 ? (row >> 2) & 3 : (row >> 3) & 1;
+  }
+};
 
 __device__ __forceinline__ void glds16(const void* g, uint8_t* l) {
   __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)g,
                                    (void __attribute__((address_space(3)))*)l, 16, 0, 0);
 }
 
+template <int KT>
 __global__ void __launch_bounds__(512)
     conv3_igemm_glds_kernel(const uint16_t* __restrict__ xh, const uint16_t* __restrict__ xl,
                             const uint16_t* __restrict__ wh, const uint16_t* __restrict__ wl,
                             const uint16_t* __restrict__ zrow, const float* __restrict__ bias,
                             float* __restrict__ y, int K, int M, int R) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[kGStages * kGStage];
+  using G = GK<KT>;
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kGStages * G::STAGE];
   const int V = R * R * R, R2 = R * R;
   int id = (int)blockIdx.x;
   {
@@ -321,30 +336,30 @@ __global__ void __launch_bounds__(512)
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   const int wr = w >> 2, wc = w & 3, r = lane & 31, h = lane >> 5;
-  const int nck = K / kGK, nsteps = 27 * nck;
+  const int nck = K / KT, nsteps = 27 * nck;
   const size_t bV = (size_t)b * V;
+  const int prow = lane / G::CPR, pch = lane % G::CPR;  // this lane's place in a piece
 
-  // A pieces: I = 2w + q -> image I >> 3, rows ((I & 7) << 4) + lane / 4.
+  // A pieces: I = APW w + q -> image I / API, rows (I % API) * RPP + lane / CPR.
   // Per-piece element offsets are fixed; a step adds the uniform tap / chunk offset.
-  const uint16_t* abase[2];
+  const uint16_t* abase[G::APW];
 #pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const int I = 2 * w + q;
-    const int row = ((I & 7) << 4) + (lane >> 2);
-    abase[q] = ((I >> 3) ? wl : wh) + (size_t)(m0 + row) * K + (((lane & 3) ^ gswz(row)) << 3);
+  for (int q = 0; q < G::APW; ++q) {
+    const int I = G::APW * w + q;
+    const int row = (I % G::API) * G::RPP + prow;
+    abase[q] = ((I / G::API) ? wl : wh) + (size_t)(m0 + row) * K + ((pch ^ G::swz(row)) << 3);
   }
-  // B pieces: I = 4w + q -> image I >> 4 (waves 0-3: hi, 4-7: lo), rows ((I & 15) << 4) + lane / 4
-  const uint16_t* __restrict__ ximg = (w >= 4) ? xl : xh;
-  const uint16_t* bbase[4];
-  const uint16_t* zbase[4];
-  int bxyz[4];  // x | y << 10 | z << 20 of the piece's voxel
+  // B pieces: I = BPW w + q -> image I / BPI (waves 0-3: hi, 4-7: lo)
+  const uint16_t* bbase[G::BPW];
+  const uint16_t* zbase[G::BPW];
+  int bxyz[G::BPW];  // x | y << 10 | z << 20 of the piece's voxel
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int I = 4 * w + q;
-    const int row = ((I & 15) << 4) + (lane >> 2);
+  for (int q = 0; q < G::BPW; ++q) {
+    const int I = G::BPW * w + q;
+    const int row = (I % G::BPI) * G::RPP + prow;
     const int v = v0 + row;
-    const int cofs = ((lane & 3) ^ gswz(row)) << 3;
-    bbase[q] = ximg + (bV + v) * K + cofs;
+    const int cofs = (pch ^ G::swz(row)) << 3;
+    bbase[q] = ((I / G::BPI) ? xl : xh) + (bV + v) * K + cofs;
     zbase[q] = zrow + cofs;
     bxyz[q] = (v / R2) | (((v / R) % R) << 10) | ((v % R) << 20);
   }
@@ -352,23 +367,24 @@ __global__ void __launch_bounds__(512)
   auto issue = [&](int s, int buf) {
     // channel-chunk-major: the 27 taps of one chunk are consecutive, so the
     // neighbour rows they re-read stay in L2 (tap-major measured slower)
-    const int c0 = (s / 27) * kGK, tap = s - (s / 27) * 27;
-    uint8_t* base = lds + buf * kGStage;
+    const int c0 = (s / 27) * KT, tap = s - (s / 27) * 27;
+    uint8_t* base = lds + buf * G::STAGE;
     const size_t aofs = (size_t)tap * M * K + c0;
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int I = 2 * w + q;
-      glds16(abase[q] + aofs, base + (I >> 3) * kGA + (I & 7) * 1024);
+    for (int q = 0; q < G::APW; ++q) {
+      const int I = G::APW * w + q;
+      glds16(abase[q] + aofs, base + (I / G::API) * G::A + (I % G::API) * 1024);
     }
     const int dx = tap / 9 - 1, dy = (tap / 3) % 3 - 1, dz = tap % 3 - 1;
     const long long bofs = (long long)(dx * R2 + dy * R + dz) * K + c0;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int I = 4 * w + q;
+    for (int q = 0; q < G::BPW; ++q) {
+      const int I = G::BPW * w + q;
       const int x = bxyz[q] & 1023, yy = (bxyz[q] >> 10) & 1023, z = bxyz[q] >> 20;
       const bool inb = (unsigned)(x + dx) < (unsigned)R && (unsigned)(yy + dy) < (unsigned)R &&
                        (unsigned)(z + dz) < (unsigned)R;
-      glds16(inb ? bbase[q] + bofs : zbase[q], base + 2 * kGA + (I >> 4) * kGB + (I & 15) * 1024);
+      glds16(inb ? bbase[q] + bofs : zbase[q],
+             base + 2 * G::A + (I / G::BPI) * G::B + (I % G::BPI) * 1024);
     }
   };
 
@@ -383,32 +399,32 @@ __global__ void __launch_bounds__(512)
   issue(0, 0);
   if (nsteps > 1) issue(1, 1);
   for (int s = 0; s < nsteps; ++s) {
-    // stage s landed (this wave's 6 pieces of it): leave stage s+1's 6 in flight
-    if (s + 1 < nsteps) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    // stage s landed (this wave's pieces of it): leave stage s+1's in flight
+    if (s + 1 < nsteps) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::APW + G::BPW) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // everyone's stage s landed; stage s-1 reads done
 #ifndef PCFM_EXP_NOLOAD
     if (s + 2 < nsteps) issue(s + 2, (s + 2) % kGStages);
 #endif
-    const uint8_t* base = lds + (s % kGStages) * kGStage;
+    const uint8_t* base = lds + (s % kGStages) * G::STAGE;
 #pragma unroll
-    for (int kk = 0; kk < kGK / 16; ++kk) {
+    for (int kk = 0; kk < KT / 16; ++kk) {
       const int kc = 2 * kk + h;
       bf16x8 ah[2], al[2], bh[2], bl[2];
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const int row = wr * 64 + i * 32 + r;
-        const int off = row * 64 + ((kc ^ gswz(row)) << 4);
+        const int off = row * G::RB + ((kc ^ G::swz(row)) << 4);
         ah[i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(base + off));
-        al[i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(base + kGA + off));
+        al[i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(base + G::A + off));
       }
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int row = wc * 64 + j * 32 + r;
-        const int off = 2 * kGA + row * 64 + ((kc ^ gswz(row)) << 4);
+        const int off = 2 * G::A + row * G::RB + ((kc ^ G::swz(row)) << 4);
         bh[j] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(base + off));
-        bl[j] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(base + kGB + off));
+        bl[j] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(base + G::B + off));
       }
 #ifdef PCFM_EXP_NOMFMA
       acc[0][0][kk] += (float)(ah[0][0] + al[0][1] + ah[1][2] + al[1][3] + bh[0][4] + bl[0][5] +
@@ -1245,8 +1261,15 @@ extern "C" int pcfm_conv3d_igemm_cl(const void* xs, const void* wsplit, const fl
       return check_launch("conv3d_igemm_cl");
     }
 #endif
-    hipLaunchKernelGGL(conv3_igemm_glds_kernel, dim3((unsigned)glds_blocks), dim3(512), 0, st, xh,
-                       xl, wh, wh + total, zrow, bias, y, cin, cout, r);
+#ifndef PCFM_CONV_GK
+#define PCFM_CONV_GK 32  // 16: two blocks per CU, measured 1.15-1.18x slower
+#endif
+    if (PCFM_CONV_GK == 16 || cin % 32 != 0)
+      hipLaunchKernelGGL(conv3_igemm_glds_kernel<16>, dim3((unsigned)glds_blocks), dim3(512), 0,
+                         st, xh, xl, wh, wh + total, zrow, bias, y, cin, cout, r);
+    else
+      hipLaunchKernelGGL(conv3_igemm_glds_kernel<32>, dim3((unsigned)glds_blocks), dim3(512), 0,
+                         st, xh, xl, wh, wh + total, zrow, bias, y, cin, cout, r);
     return check_launch("conv3d_igemm_cl");
   }
 #endif

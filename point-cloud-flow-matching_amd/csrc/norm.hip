@@ -294,7 +294,32 @@ __global__ void __launch_bounds__(256)
   const float a = rstd * w[c];
   coef[3 * (size_t)i] = a;
   coef[3 * (size_t)i + 1] = bias[c] - mean * a;
-  coef[3 * (size_t)i + 2] = 1.0f + gamma[i];
+  coef[3 * (size_t)i + 2] = gamma != nullptr ? 1.0f + gamma[i] : 1.0f;
+}
+
+// torch's SiLU x / (1 + exp(-x)) and its derivative s (1 + x (1 - s))
+__device__ __forceinline__ float gn_silu(float x) { return x / (1.0f + expf(-x)); }
+__device__ __forceinline__ float gn_dsilu(float x) {
+  const float sg = 1.0f / (1.0f + expf(-x));
+  return sg * (1.0f + x * (1.0f - sg));
+}
+
+// ContextNet's head: out = SiLU(GN(x)) = SiLU(x * a + s); grid (ceil(N4 / 256), B * C)
+__global__ void __launch_bounds__(256)
+    gn_silu_apply_kernel(const float* __restrict__ x, const float* __restrict__ coef, int N4,
+                         float* __restrict__ out) {
+  const int n4 = blockIdx.x * 256 + threadIdx.x;
+  if (n4 >= N4) return;
+  const int row = blockIdx.y;
+  const float a = coef[3 * (size_t)row], sh = coef[3 * (size_t)row + 1];
+  const size_t i = (size_t)row * N4 + n4;
+  const float4 v = reinterpret_cast<const float4*>(x)[i];
+  float4 o;
+  o.x = gn_silu(__builtin_fmaf(v.x, a, sh));
+  o.y = gn_silu(__builtin_fmaf(v.y, a, sh));
+  o.z = gn_silu(__builtin_fmaf(v.z, a, sh));
+  o.w = gn_silu(__builtin_fmaf(v.w, a, sh));
+  reinterpret_cast<float4*>(out)[i] = o;
 }
 
 // out = x + ((x * a + s) * g1 + beta); grid (ceil(N4 / 256), B * C)
@@ -317,21 +342,32 @@ __global__ void __launch_bounds__(256)
 }
 
 // bwd row sums: grid (kGnParts, B * C); part[row * P + p] = (sum dout, sum dout * xhat)
+// ACT (GN + SiLU): the gradient entering GN is dout * SiLU'(x * a + s), recomputed
+template <bool ACT>
 __global__ void __launch_bounds__(256)
     gn_bwd_stats_kernel(const float* __restrict__ dout, const float* __restrict__ x,
-                        const float* __restrict__ mean, const float* __restrict__ rstd, int C,
+                        const float* __restrict__ mean, const float* __restrict__ rstd,
+                        const float* __restrict__ w, const float* __restrict__ bias, int C,
                         int N, int G, float* __restrict__ part) {
   __shared__ float sh[8];
   const int row = blockIdx.y, p = blockIdx.x;
   const int b = row / C, c = row - b * C, g = c / (C / G);
   const float m = mean[b * G + g], rs = rstd[b * G + g];
+  const float ca = ACT ? rs * w[c] : 0.0f, cs = ACT ? bias[c] - m * ca : 0.0f;
   const int N4 = N / 4, chunk = (N4 + kGnParts - 1) / kGnParts;
   const int f0 = min(N4, p * chunk), f1 = min(N4, f0 + chunk);
   const float4* x4 = reinterpret_cast<const float4*>(x) + (size_t)row * N4;
   const float4* d4 = reinterpret_cast<const float4*>(dout) + (size_t)row * N4;
   float a2 = 0.0f, a3 = 0.0f;
   for (int f = f0 + threadIdx.x; f < f1; f += 256) {
-    const float4 v = x4[f], d = d4[f];
+    const float4 v = x4[f];
+    float4 d = d4[f];
+    if (ACT) {
+      d.x *= gn_dsilu(__builtin_fmaf(v.x, ca, cs));
+      d.y *= gn_dsilu(__builtin_fmaf(v.y, ca, cs));
+      d.z *= gn_dsilu(__builtin_fmaf(v.z, ca, cs));
+      d.w *= gn_dsilu(__builtin_fmaf(v.w, ca, cs));
+    }
     a2 += (d.x + d.y) + (d.z + d.w);
     a3 += (d.x * ((v.x - m) * rs) + d.y * ((v.y - m) * rs)) +
           (d.z * ((v.z - m) * rs) + d.w * ((v.w - m) * rs));
@@ -364,9 +400,9 @@ __global__ void __launch_bounds__(1024)
         a2 += part[(row * kGnParts + p) * 2];
         a3 += part[(row * kGnParts + p) * 2 + 1];
       }
-      g1 = 1.0f + gamma[row];
-      dbeta[row] = a2;
-      dgamma[row] = w[c] * a3 + bias[c] * a2;
+      g1 = gamma != nullptr ? 1.0f + gamma[row] : 1.0f;
+      if (dbeta != nullptr) dbeta[row] = a2;
+      if (dgamma != nullptr) dgamma[row] = w[c] * a3 + bias[c] * a2;
       dws += g1 * a3;
       dbs += g1 * a2;
       t1 = w[c] * g1 * a2;  // sum_n dy w over this channel
@@ -398,25 +434,40 @@ __global__ void __launch_bounds__(1024)
 }
 
 // dx = dout + dout * kc0 - kc1 - xhat * kc2; grid (ceil(N4 / 256), B * C)
+// ACT: dx = dy * kc0 - kc1 - xhat * kc2 with dy = dout * SiLU'(x * a + s) (no residual)
+template <bool ACT>
 __global__ void __launch_bounds__(256)
     gn_film_bwd_apply_kernel(const float* __restrict__ dout, const float* __restrict__ x,
                              const float* __restrict__ mean, const float* __restrict__ rstd,
-                             const float* __restrict__ kc, int C, int G, int N4,
+                             const float* __restrict__ kc, const float* __restrict__ w,
+                             const float* __restrict__ bias, int C, int G, int N4,
                              float* __restrict__ dx) {
   const int n4 = blockIdx.x * 256 + threadIdx.x;
   if (n4 >= N4) return;
   const int row = blockIdx.y;
-  const int b = row / C, g = (row - b * C) / (C / G);
+  const int b = row / C, c = row - b * C, g = c / (C / G);
   const float m = mean[b * G + g], rs = rstd[b * G + g];
   const float k0 = kc[3 * (size_t)row], k1 = kc[3 * (size_t)row + 1], k2 = kc[3 * (size_t)row + 2];
   const size_t i = (size_t)row * N4 + n4;
   const float4 v = reinterpret_cast<const float4*>(x)[i];
   const float4 d = reinterpret_cast<const float4*>(dout)[i];
   float4 o;
-  o.x = d.x + ((d.x * k0 - k1) - ((v.x - m) * rs) * k2);
-  o.y = d.y + ((d.y * k0 - k1) - ((v.y - m) * rs) * k2);
-  o.z = d.z + ((d.z * k0 - k1) - ((v.z - m) * rs) * k2);
-  o.w = d.w + ((d.w * k0 - k1) - ((v.w - m) * rs) * k2);
+  if (ACT) {
+    const float ca = rs * w[c], cs = bias[c] - m * ca;
+    const float dy0 = d.x * gn_dsilu(__builtin_fmaf(v.x, ca, cs));
+    const float dy1 = d.y * gn_dsilu(__builtin_fmaf(v.y, ca, cs));
+    const float dy2 = d.z * gn_dsilu(__builtin_fmaf(v.z, ca, cs));
+    const float dy3 = d.w * gn_dsilu(__builtin_fmaf(v.w, ca, cs));
+    o.x = (dy0 * k0 - k1) - ((v.x - m) * rs) * k2;
+    o.y = (dy1 * k0 - k1) - ((v.y - m) * rs) * k2;
+    o.z = (dy2 * k0 - k1) - ((v.z - m) * rs) * k2;
+    o.w = (dy3 * k0 - k1) - ((v.w - m) * rs) * k2;
+  } else {
+    o.x = d.x + ((d.x * k0 - k1) - ((v.x - m) * rs) * k2);
+    o.y = d.y + ((d.y * k0 - k1) - ((v.y - m) * rs) * k2);
+    o.z = d.z + ((d.z * k0 - k1) - ((v.z - m) * rs) * k2);
+    o.w = d.w + ((d.w * k0 - k1) - ((v.w - m) * rs) * k2);
+  }
   reinterpret_cast<float4*>(dx)[i] = o;
 }
 
@@ -525,11 +576,52 @@ extern "C" int pcfm_gn_film_res_bwd(const float* dout, const float* x, const flo
   hipStream_t st = (hipStream_t)stream;
   float* part = (float*)ws;
   float* kc = part + (size_t)b * c * kGnParts * 2;
-  hipLaunchKernelGGL(gn_bwd_stats_kernel, dim3(kGnParts, b * c), dim3(256), 0, st, dout, x, mean,
-                     rstd, c, n, groups, part);
+  hipLaunchKernelGGL(gn_bwd_stats_kernel<false>, dim3(kGnParts, b * c), dim3(256), 0, st, dout, x,
+                     mean, rstd, w, bias, c, n, groups, part);
   hipLaunchKernelGGL(gn_bwd_finalize_kernel, dim3(1), dim3(1024), 0, st, (const float*)part, w,
                      bias, gamma, rstd, b, c, n, groups, kc, dgamma, dbeta, dw, dbias);
-  hipLaunchKernelGGL(gn_film_bwd_apply_kernel, dim3(ceil_div(n / 4, 256), b * c), dim3(256), 0,
-                     st, dout, x, mean, rstd, (const float*)kc, c, groups, n / 4, dx);
+  hipLaunchKernelGGL(gn_film_bwd_apply_kernel<false>, dim3(ceil_div(n / 4, 256), b * c), dim3(256),
+                     0, st, dout, x, mean, rstd, (const float*)kc, w, bias, c, groups, n / 4, dx);
   return check_launch("gn_film_res_bwd");
+}
+
+// ContextNet head: SiLU(GroupNorm(x)) (models.py:460-466 head_norm + head_act)
+extern "C" int pcfm_gn_silu_fwd(const float* x, const float* w, const float* bias, int b, int c,
+                                int n, int groups, float eps, float* out, float* mean, float* rstd,
+                                void* ws, size_t ws_bytes, void* stream) {
+  PCFM_CHECK_ARG(gn_ok(b, c, n, groups), "gn_silu_fwd: bad shape b=%d c=%d n=%d groups=%d", b, c,
+                 n, groups);
+  PCFM_CHECK_ARG(ws_bytes >= pcfm_gn_film_workspace_bytes(b, c, n, groups),
+                 "gn_silu_fwd: workspace too small");
+  hipStream_t st = (hipStream_t)stream;
+  float* part = (float*)ws;
+  float* coef = part + (size_t)b * groups * kGnParts * 2;
+  hipLaunchKernelGGL(gn_stats_kernel, dim3(groups * kGnParts, b), dim3(256), 0, st, x, c, n,
+                     groups, part);
+  hipLaunchKernelGGL(gn_finalize_kernel, dim3(ceil_div((long long)b * c, 256)), dim3(256), 0, st,
+                     (const float*)part, x, w, bias, nullptr, b, c, n, groups, eps, mean, rstd,
+                     coef);
+  hipLaunchKernelGGL(gn_silu_apply_kernel, dim3(ceil_div(n / 4, 256), b * c), dim3(256), 0, st, x,
+                     (const float*)coef, n / 4, out);
+  return check_launch("gn_silu_fwd");
+}
+
+extern "C" int pcfm_gn_silu_bwd(const float* dout, const float* x, const float* w,
+                                const float* bias, const float* mean, const float* rstd, int b,
+                                int c, int n, int groups, float* dx, float* dw, float* dbias,
+                                void* ws, size_t ws_bytes, void* stream) {
+  PCFM_CHECK_ARG(gn_ok(b, c, n, groups), "gn_silu_bwd: bad shape b=%d c=%d n=%d groups=%d", b, c,
+                 n, groups);
+  PCFM_CHECK_ARG(ws_bytes >= pcfm_gn_film_workspace_bytes(b, c, n, groups),
+                 "gn_silu_bwd: workspace too small");
+  hipStream_t st = (hipStream_t)stream;
+  float* part = (float*)ws;
+  float* kc = part + (size_t)b * c * kGnParts * 2;
+  hipLaunchKernelGGL(gn_bwd_stats_kernel<true>, dim3(kGnParts, b * c), dim3(256), 0, st, dout, x,
+                     mean, rstd, w, bias, c, n, groups, part);
+  hipLaunchKernelGGL(gn_bwd_finalize_kernel, dim3(1), dim3(1024), 0, st, (const float*)part, w,
+                     bias, nullptr, rstd, b, c, n, groups, kc, nullptr, nullptr, dw, dbias);
+  hipLaunchKernelGGL(gn_film_bwd_apply_kernel<true>, dim3(ceil_div(n / 4, 256), b * c), dim3(256),
+                     0, st, dout, x, mean, rstd, (const float*)kc, w, bias, c, groups, n / 4, dx);
+  return check_launch("gn_silu_bwd");
 }

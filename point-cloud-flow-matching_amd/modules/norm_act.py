@@ -148,6 +148,36 @@ class _GNFiLMRes(torch.autograd.Function):
         return dx, dw, db, dg, dbt, None, None
 
 
+class _GNSiLU(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, groups, eps):
+        from pcfm import ops
+        out, mean, rstd = ops.gn_silu_forward(x, weight, bias, groups, eps)
+        ctx.save_for_backward(x, weight, bias, mean, rstd)
+        ctx.groups = groups
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        from pcfm import ops
+        x, weight, bias, mean, rstd = ctx.saved_tensors
+        dx, dw, db = ops.gn_silu_backward(dout, x, weight, bias, mean, rstd, ctx.groups)
+        return dx, dw, db, None, None
+
+
+def gn_silu(x: torch.Tensor, norm) -> torch.Tensor:
+    """SiLU(norm(x)) for a GroupNorm `norm` (ContextNet's head_norm + head_act,
+    reference models.py:460-466); fused on a HIP device in fp32."""
+    fused = (x.is_cuda and x.dtype == torch.float32 and x.dim() == 3
+             and isinstance(norm, torch.nn.GroupNorm) and norm.affine
+             and x.shape[2] % 4 == 0 and x.shape[1] <= 1024 and x.shape[0] * x.shape[1] < 65536
+             and not torch.is_autocast_enabled("cuda"))
+    if fused:
+        return _GNSiLU.apply(x.contiguous(), norm.weight, norm.bias, int(norm.num_groups),
+                             float(norm.eps))
+    return torch.nn.functional.silu(norm(x))
+
+
 def gn_film_residual(x: torch.Tensor, norm, gamma: torch.Tensor, beta: torch.Tensor):
     """x + (norm(x) * (1 + gamma[:, :, None]) + beta[:, :, None]) for a GroupNorm
     `norm` (reference models.py:322-368); fused on a HIP device in fp32."""

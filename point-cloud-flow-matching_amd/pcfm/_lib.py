@@ -71,6 +71,8 @@ SIGNATURES = {
     "pcfm_rows_colsum_workspace_bytes": (_Z, [_I, _L, _I]),
     "pcfm_rows_colsum": (_I, [_P, _I, _I, _L, _I, _P, _P, _Z, _P]),
     "pcfm_avg_voxelize_bwd_add": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _P, _P]),
+    "pcfm_gn_silu_fwd": (_I, [_P, _P, _P, _I, _I, _I, _I, _F, _P, _P, _P, _P, _Z, _P]),
+    "pcfm_gn_silu_bwd": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P, _Z, _P]),
     "pcfm_tgate_fwd": (_I, [_P, _P, _P, _I, _I, _I, _P, _P]),
     "pcfm_tgate_bwd": (_I, [_P, _P, _I, _I, _I, _P, _P]),
     "pcfm_pointwise_gemm_parts": (_I, [_I, _P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P]),

@@ -21,7 +21,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from modules.norm_act import bn_act, gn_film_residual
+from modules.norm_act import bn_act, gn_film_residual, gn_silu
 from modules.pvconv import PVConv
 from modules.shared_mlp import PointwiseConv1d, SharedMLP
 from pcfm.layers import RowsLinear, fused_trunk, fused_trunk_supported, max_over_points
@@ -498,7 +498,11 @@ class ContextNet(_TimeCondEmbed):
                 f, c = stage(f, c, emb32)
                 scales.append(f)
             g = self.global_mlp(f.max(dim=-1).values) if self.with_global else None
-            h = self.head_act(self.head_norm(self._head_pre(scales, g)))
+            pre = self._head_pre(scales, g)
+            if isinstance(self.head_norm, nn.GroupNorm) and isinstance(self.head_act, nn.SiLU):
+                h = gn_silu(pre, self.head_norm)  # one fused pass pair on the GPU
+            else:
+                h = self.head_act(self.head_norm(pre))
             ctx = self.head_out(h)
             if self.use_t_gate:
                 glb = self.ctx_from_emb(emb32)

@@ -904,6 +904,35 @@ def gn_film_res_forward(x, weight, bias, gamma, beta, groups: int, eps: float):
     return out, stats[0], stats[1]
 
 
+def gn_silu_forward(x, weight, bias, groups: int, eps: float):
+    """out = SiLU(GroupNorm(x)) -> (out, mean, rstd)"""
+    _check(x, "input", "f")
+    b, c, n = x.shape
+    out = torch.empty_like(x)
+    stats = torch.empty((2, b, groups), dtype=torch.float32, device=x.device)
+    ws = _workspace(_lib.query("pcfm_gn_film_workspace_bytes", b, c, n, groups), x)
+    with _timed("gn_silu_fwd", 4 * 3 * x.numel(), x):
+        _lib.call("pcfm_gn_silu_fwd", _ptr(x), _ptr(weight), _ptr(bias), b, c, n, groups,
+                  float(eps), _ptr(out), _ptr(stats[0]), _ptr(stats[1]), _ptr(ws), ws.numel(),
+                  _stream(x))
+    return out, stats[0], stats[1]
+
+
+def gn_silu_backward(dout, x, weight, bias, mean, rstd, groups: int):
+    """-> (dx, dweight, dbias)"""
+    dout = dout.contiguous()
+    b, c, n = x.shape
+    dx = torch.empty_like(x)
+    small = torch.empty((2 * c,), dtype=torch.float32, device=x.device)
+    dw, dbias = small[:c], small[c:]
+    ws = _workspace(_lib.query("pcfm_gn_film_workspace_bytes", b, c, n, groups), x)
+    with _timed("gn_silu_bwd", 4 * 5 * x.numel(), x):
+        _lib.call("pcfm_gn_silu_bwd", _ptr(dout), _ptr(x), _ptr(weight), _ptr(bias), _ptr(mean),
+                  _ptr(rstd), b, c, n, groups, _ptr(dx), _ptr(dw), _ptr(dbias), _ptr(ws),
+                  ws.numel(), _stream(x))
+    return dx, dw, dbias
+
+
 def gn_film_res_backward(dout, x, weight, bias, gamma, mean, rstd, groups: int):
     """-> (dx, dweight, dbias, dgamma (B, C), dbeta (B, C))"""
     dout = dout.contiguous()

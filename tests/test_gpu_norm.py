@@ -136,3 +136,28 @@ def test_conv_bn_act_fused_matches_modules(ops, kind):
     assert rel(bn2.bias.grad, bn.bias.grad) < 1e-3
     torch.testing.assert_close(bn2.running_mean, bn.running_mean, rtol=1e-4, atol=1e-5)
     torch.testing.assert_close(bn2.running_var, bn.running_var, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("b,c,n,groups", [(8, 256, 20000, 32), (2, 128, 1000, 32), (3, 64, 36, 8)])
+def test_gn_silu_matches_torch(ops, b, c, n, groups):
+    """SiLU(GroupNorm(x)) (ContextNet head_norm + head_act) fused vs torch."""
+    from modules.norm_act import gn_silu
+    torch.manual_seed(2)
+    norm = torch.nn.GroupNorm(groups, c).cuda()
+    with torch.no_grad():
+        norm.weight.uniform_(0.5, 1.5)
+        norm.bias.uniform_(-0.5, 0.5)
+    x = torch.randn(b, c, n, device="cuda") * 1.5 + 2.0
+    xa, xb = x.clone().requires_grad_(True), x.clone().requires_grad_(True)
+    ref = torch.nn.functional.silu(norm(xa))
+    gy = torch.randn_like(ref)
+    ref.backward(gy)
+    grads_ref = [xa.grad, norm.weight.grad.clone(), norm.bias.grad.clone()]
+    norm.zero_grad()
+    out = gn_silu(xb, norm)
+    torch.testing.assert_close(out, ref, rtol=1e-4, atol=1e-4)
+    out.backward(gy)
+    got = [xb.grad, norm.weight.grad, norm.bias.grad]
+    for a, r in zip(got, grads_ref):
+        scale = r.abs().max().item()
+        torch.testing.assert_close(a, r, rtol=1e-4, atol=1e-4 * max(1.0, scale))
