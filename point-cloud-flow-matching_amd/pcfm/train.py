@@ -14,6 +14,8 @@ Deliberate, result-preserving differences (all switchable in TrainConfig):
     device instead of the host round trip of GradScaler.step; same update rule.
   * `device_rng`: t ~ Beta(a, 1) is sampled on the device (the reference
     samples on the CPU and copies, train.py:604-605, :639-640); same law.
+  * `tunableop`: the autocast Linears use library GEMM algorithms measured on
+    MI355X for this step (PyTorch TunableOp, pcfm/data/tunableop_gfx950.csv);
   * `miopen_find`: torch.backends.cudnn.benchmark = True, i.e. MIOpen picks
     each convolution's solver by timing the candidates once per shape.
 """
@@ -47,6 +49,8 @@ class TrainConfig:
     enc_depth: int = 4
     pf_width: int = 512
     pf_depth: int = 6
+    # runtime: MI355X-measured library GEMM choices (pcfm/data/tunableop_gfx950.csv)
+    tunableop: bool = True
     pf_emb_dim: int = 256
     cfg_drop_p: float = 0.1
     lf_width: int = 512
@@ -236,6 +240,27 @@ def synthetic_batch(cfg: TrainConfig, device, generator: Optional[torch.Generato
     return batch
 
 
+TUNABLEOP_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data",
+                              "tunableop_gfx950.csv")
+
+
+def enable_tunableop(path: str = TUNABLEOP_FILE, tune: bool = False) -> bool:
+    """Library GEMM choice for the autocast Linears (hipBLASLt / rocBLAS) from
+    PyTorch TunableOp results measured on MI355X for this train step
+    (tools/tune_gemms.sh writes them; tune=True measures unseen shapes).  Shapes
+    not in the file, or a file from another library version, keep the default
+    algorithm.  Returns False if the file is absent."""
+    from torch.cuda import tunable
+    if not tune and not os.path.exists(path):
+        return False
+    tunable.enable(True)
+    tunable.tuning_enable(bool(tune))
+    tunable.set_filename(path, insert_device_ordinal=False)
+    if os.path.exists(path):
+        tunable.read_file(path)
+    return True
+
+
 class Trainer:
     """Models + optimizer + one FM training iteration (train.py:553-673)."""
 
@@ -245,6 +270,9 @@ class Trainer:
         self.device = torch.device(device)
         if self.device.type == "cuda" and cfg.miopen_find:
             torch.backends.cudnn.benchmark = True
+        if self.device.type == "cuda" and cfg.tunableop:
+            out = os.environ.get("PCFM_TUNE_GEMMS")  # tools/tune_gemms.sh: measure, write here
+            enable_tunableop(out, tune=True) if out else enable_tunableop()
         self.rank, self.world_size = rank, world_size
         seed_all(cfg.seed + rank)
         self.enc, self.pf, self.lf = build_models(cfg, self.device)
