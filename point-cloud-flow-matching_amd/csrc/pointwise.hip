@@ -377,6 +377,131 @@ __global__ void __launch_bounds__(256)
       }
 }
 
+// Wide form for cout, cin multiples of 256 (one 256 x 256 tile): 512 threads,
+// 8 waves of 64 (co) x 128 (ci), so dY and x rows are each read once per
+// K-range instead of cin/128 resp. cout/128 times; 80 KiB LDS, one block per CU.
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2)))
+    pw_wgrad256_kernel(const Parts x, const float* __restrict__ dy, int B, int cin, int cout,
+                       int N, int S, float* __restrict__ part) {
+  constexpr int TM = 256, TN = 256;
+  constexpr int A_ELEMS = TM * kLDR, B_ELEMS = TN * kLDR;
+  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * A_ELEMS + 2 * B_ELEMS];
+  const int nco = cout / TM;
+  const int co0 = (blockIdx.x % nco) * TM, ci0 = (blockIdx.x / nco) * TN;
+  const int sp = blockIdx.y;
+  const int steps_per_b = (N + kKT - 1) / kKT;
+  const long long nsteps = (long long)B * steps_per_b;
+  const long long k0 = nsteps * sp / S, k1 = nsteps * (sp + 1) / S;
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wr = w >> 1, wc = w & 1, r = lane & 31, h = lane >> 5;  // wr 0..3 (co), wc 0..1 (ci)
+  const int srow = t >> 1, shalf = (t & 1) * 16;                     // row 0..255, 16-point half
+  const int co = co0 + srow, ci = ci0 + srow;
+  const bool vec = (N & 3) == 0;
+  const float* __restrict__ xrow = x.row(0, ci, N);
+  const size_t xbstride = (size_t)(x.row(1, ci, N) - xrow);
+
+  float ra[16], rb[16];
+  uint32_t pmask = 0u;
+  auto load = [&](long long ks) {
+    const int b = (int)(ks / steps_per_b);
+    const int p0 = (int)(ks - (long long)b * steps_per_b) * kKT + shalf;
+    const float* as = dy + ((size_t)b * cout + co) * N;
+    const float* bs = xrow + (size_t)b * xbstride;
+    pmask = 0u;
+    if (vec && p0 + 16 <= N) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float4 fa = *reinterpret_cast<const float4*>(as + p0 + 4 * q);
+        const float4 fb = *reinterpret_cast<const float4*>(bs + p0 + 4 * q);
+        ra[4 * q] = fa.x;
+        ra[4 * q + 1] = fa.y;
+        ra[4 * q + 2] = fa.z;
+        ra[4 * q + 3] = fa.w;
+        rb[4 * q] = fb.x;
+        rb[4 * q + 1] = fb.y;
+        rb[4 * q + 2] = fb.z;
+        rb[4 * q + 3] = fb.w;
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int p = p0 + q;
+        const int pc = p < N ? p : N - 1;
+        ra[q] = as[pc];
+        rb[q] = bs[pc];
+        pmask |= p < N ? 0u : (1u << q);
+      }
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      ra[q] = (pmask >> q) & 1u ? 0.0f : ra[q];
+      rb[q] = (pmask >> q) & 1u ? 0.0f : rb[q];
+    }
+    uint16_t* ah = lds + srow * kLDR + shalf;
+    store_split<16>(ra, ah, ah + A_ELEMS);
+    uint16_t* bh = lds + 2 * A_ELEMS + srow * kLDR + shalf;
+    store_split<16>(rb, bh, bh + B_ELEMS);
+  };
+
+  f32x16 acc[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
+
+  if (k0 < k1) {
+    load(k0);
+    store();
+  }
+  __syncthreads();
+  for (long long ks = k0; ks < k1; ++ks) {
+    if (ks + 1 < k1) load(ks + 1);
+#pragma unroll
+    for (int kk = 0; kk < kKT / 16; ++kk) {
+      bf16x8 ah[2], al[2], bh[4], bl[4];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int o = (wr * 64 + i * 32 + r) * kLDR + kk * 16 + 8 * h;
+        ah[i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(lds + o));
+        al[i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(lds + A_ELEMS + o));
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int o = 2 * A_ELEMS + (wc * 128 + j * 32 + r) * kLDR + kk * 16 + 8 * h;
+        bh[j] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(lds + o));
+        bl[j] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(lds + B_ELEMS + o));
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
+        }
+    }
+    __syncthreads();
+    if (ks + 1 < k1) store();
+    __syncthreads();
+  }
+  float* pb = part + (size_t)sp * cout * cin;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int o = co0 + wr * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+        const int c = ci0 + wc * 128 + j * 32 + r;
+        pb[(size_t)o * cin + c] = acc[i][j][e];
+      }
+}
+
 __global__ void __launch_bounds__(256)
     pw_wgrad_reduce_kernel(const float* __restrict__ part, size_t total, int S,
                            float* __restrict__ dw) {
@@ -393,7 +518,22 @@ __global__ void __launch_bounds__(256)
   if (grp == 0 && i < total) dw[i] = ((red[0][cl] + red[1][cl]) + red[2][cl]) + red[3][cl];
 }
 
+bool pw_wgrad_wide(int cin, int cout) {
+#ifdef PCFM_PW_NO256
+  return false;
+#else
+  return cin % 256 == 0 && cout % 256 == 0;
+#endif
+}
+
 int pw_wgrad_splits(int B, int cin, int cout, int N) {
+  if (pw_wgrad_wide(cin, cout)) {  // one 512-thread block per CU
+    const long long tiles = (long long)(cout / 256) * (cin / 256);
+    const long long steps = (long long)B * ((N + kKT - 1) / kKT);
+    long long s = std::max(1LL, ((long long)kCUs + tiles - 1) / tiles);
+    s = std::min(s, std::max(1LL, steps / 16));
+    return (int)std::min(s, 256LL);
+  }
   const long long tiles = (long long)((cout + 127) / 128) * ((cin + 127) / 128);
   const long long steps = (long long)B * ((N + kKT - 1) / kKT);
   long long s = std::max(1LL, (2LL * kCUs + tiles - 1) / tiles);
@@ -504,9 +644,14 @@ static int pw_wgrad_launch(const Parts& x, const float* grad_y, int b, int cin, 
                            float* grad_w, void* ws, hipStream_t st) {
   const size_t total = (size_t)cout * cin;
   const int S = pw_wgrad_splits(b, cin, cout, n);
-  const int tiles = ((cout + 127) / 128) * ((cin + 127) / 128);
-  hipLaunchKernelGGL(pw_wgrad_kernel, dim3(tiles, S), dim3(256), 0, st, x, grad_y, b, cin, cout,
-                     n, S, (float*)ws);
+  if (pw_wgrad_wide(cin, cout)) {
+    hipLaunchKernelGGL(pw_wgrad256_kernel, dim3((cout / 256) * (cin / 256), S), dim3(512), 0, st,
+                       x, grad_y, b, cin, cout, n, S, (float*)ws);
+  } else {
+    const int tiles = ((cout + 127) / 128) * ((cin + 127) / 128);
+    hipLaunchKernelGGL(pw_wgrad_kernel, dim3(tiles, S), dim3(256), 0, st, x, grad_y, b, cin,
+                       cout, n, S, (float*)ws);
+  }
   hipLaunchKernelGGL(pw_wgrad_reduce_kernel, dim3(ceil_div((long long)total, 64)), dim3(256), 0,
                      st, (const float*)ws, total, S, grad_w);
   return check_launch("pointwise_wgrad");
