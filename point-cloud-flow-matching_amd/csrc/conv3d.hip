@@ -240,7 +240,10 @@ __global__ void __launch_bounds__(256)
   const int nb = items / (nmt * nvt);  // batch elements
   float* __restrict__ yb =
       S == 1 ? y + (size_t)b * M * V : part + ((size_t)sp * nb + b) * M * V;
-  const bool add_bias = S == 1 && bias != nullptr;
+  float biasv[T::SI][16];
+#pragma unroll
+  for (int i = 0; i < T::SI; ++i)
+    load_bias16(S == 1 ? bias : nullptr, m0 + wr * (TM / 2) + i * 32, h, M, biasv[i]);
 #pragma unroll
   for (int i = 0; i < T::SI; ++i)
 #pragma unroll
@@ -249,7 +252,7 @@ __global__ void __launch_bounds__(256)
       for (int e = 0; e < 16; ++e) {
         const int m = m0 + wr * (TM / 2) + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
         const int v = v0 + wc * (TN / 2) + j * 32 + r;
-        yb[(size_t)m * V + v] = acc[i][j][e] + (add_bias ? bias[m] : 0.0f);
+        yb[(size_t)m * V + v] = acc[i][j][e] + biasv[i][e];
       }
 }
 
@@ -449,6 +452,9 @@ __global__ void __launch_bounds__(512)
     }
   }
   float* __restrict__ yb = y + (size_t)b * M * V;
+  float biasv[2][16];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) load_bias16(bias, m0 + wr * 64 + i * 32, h, M, biasv[i]);
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -457,7 +463,7 @@ __global__ void __launch_bounds__(512)
       for (int e = 0; e < 16; ++e) {
         const int m = m0 + wr * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
         const int v = v0 + wc * 64 + j * 32 + r;
-        yb[(size_t)m * V + v] = acc[i][j][e] + (bias != nullptr ? bias[m] : 0.0f);
+        yb[(size_t)m * V + v] = acc[i][j][e] + biasv[i][e];
       }
 }
 
@@ -659,6 +665,9 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
     }
   }
   float* __restrict__ yb = y + (size_t)b * M * V;
+  float biasv[2][16];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) load_bias16(bias, m0 + wr * 64 + i * 32, h, M, biasv[i]);
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -667,7 +676,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
       for (int e = 0; e < 16; ++e) {
         const int m = m0 + wr * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
         const int v = v0 + wc * 64 + j * 32 + r;
-        yb[(size_t)m * V + v] = acc[i][j][e] + (bias != nullptr ? bias[m] : 0.0f);
+        yb[(size_t)m * V + v] = acc[i][j][e] + biasv[i][e];
       }
 }
 

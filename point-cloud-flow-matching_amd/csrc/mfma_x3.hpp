@@ -155,5 +155,19 @@ __device__ __forceinline__ bf16x8 tr_operand(const uint8_t* img, int kk, int col
   return __builtin_bit_cast(bf16x8, __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7));
 }
 
+// ---------------------------------------------------------------------------
+// Epilogue bias of one 32x32 accumulator: element e of lane half h is row
+// mg + (e & 3) + 8 (e >> 2) + 4 h.  All 16 values are loaded before the
+// tile's first store: vmcnt counts stores too, so a bias load placed after
+// a store waits for that store's acknowledgement -- 16-64 serialised round
+// trips per wave in the fused-add form.  Rows >= M read row M - 1 (unused).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void load_bias16(const float* __restrict__ bias, int mg, int h, int M,
+                                            float (&bv)[16]) {
+#pragma unroll
+  for (int e = 0; e < 16; ++e)
+    bv[e] = bias != nullptr ? bias[min(mg + (e & 3) + 8 * (e >> 2) + 4 * h, M - 1)] : 0.0f;
+}
+
 }  // namespace
 }  // namespace pcfm

@@ -144,6 +144,8 @@ __global__ void __launch_bounds__(256)
     // a 32-row group lies inside one output part (parts are 128-aligned)
     const int mg = m0 + wr * (TM / 2) + i * 32;
     float* __restrict__ yr = y.row(b, min(mg, M - 1), N);
+    float bv[16];
+    load_bias16(bias != nullptr ? bias + bo : nullptr, mg, h, M, bv);
 #pragma unroll
     for (int j = 0; j < T::SJ; ++j)
 #pragma unroll
@@ -151,7 +153,7 @@ __global__ void __launch_bounds__(256)
         const int dm = (e & 3) + 8 * (e >> 2) + 4 * h;
         const int m = mg + dm;
         const int p = p0 + wc * (TN / 2) + j * 32 + r;
-        if (m < M && p < N) yr[(size_t)dm * N + p] = acc[i][j][e] + (bias != nullptr ? bias[bo + m] : 0.0f);
+        if (m < M && p < N) yr[(size_t)dm * N + p] = acc[i][j][e] + bv[e];
       }
   }
 }
@@ -259,6 +261,8 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))
   for (int i = 0; i < 2; ++i) {
     const int mg = m0 + wr * 64 + i * 32;
     float* __restrict__ yr = y.row(b, min(mg, M - 1), N);
+    float bv[16];
+    load_bias16(bias != nullptr ? bias + bo : nullptr, mg, h, M, bv);
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -266,7 +270,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))
         const int dm = (e & 3) + 8 * (e >> 2) + 4 * h;
         const int m = mg + dm;
         const int p = p0 + wc * 64 + j * 32 + r;
-        if (m < M && p < N) yr[(size_t)dm * N + p] = acc[i][j][e] + (bias != nullptr ? bias[bo + m] : 0.0f);
+        if (m < M && p < N) yr[(size_t)dm * N + p] = acc[i][j][e] + bv[e];
       }
   }
 }
