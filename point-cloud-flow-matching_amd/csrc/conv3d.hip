@@ -318,6 +318,55 @@ __device__ __forceinline__ void glds16(const void* g, uint8_t* l) {
                                    (void __attribute__((address_space(3)))*)l, 16, 0, 0);
 }
 
+// One step's MFMA operands of a wave (64 x 64 of the 128 x 256 tile):
+// F[kk] = {A hi 0, A hi 1, A lo 0, A lo 1, B hi 0, B hi 1, B lo 0, B lo 1}
+template <int KT>
+__device__ __forceinline__ void glds_frags(const uint8_t* lds, int buf, int wr, int wc, int r,
+                                           int h, bf16x8 (&F)[KT / 16][8]) {
+  using G = GK<KT>;
+  const uint8_t* base = lds + buf * G::STAGE;
+#pragma unroll
+  for (int kk = 0; kk < KT / 16; ++kk) {
+    const int kc = 2 * kk + h;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int row = wr * 64 + i * 32 + r;
+      const int off = row * G::RB + ((kc ^ G::swz(row)) << 4);
+      F[kk][i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(base + off));
+      F[kk][2 + i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(base + G::A + off));
+    }
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int row = wc * 64 + j * 32 + r;
+      const int off = 2 * G::A + row * G::RB + ((kc ^ G::swz(row)) << 4);
+      F[kk][4 + j] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(base + off));
+      F[kk][6 + j] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(base + G::B + off));
+    }
+  }
+}
+
+template <int KT>
+__device__ __forceinline__ void glds_mfma(const bf16x8 (&F)[KT / 16][8], f32x16 (&acc)[2][2]) {
+#pragma unroll
+  for (int kk = 0; kk < KT / 16; ++kk) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F[kk][i], F[kk][4 + j], acc[i][j], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F[kk][i], F[kk][6 + j], acc[i][j], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F[kk][2 + i], F[kk][4 + j], acc[i][j], 0, 0, 0);
+  }
+}
+
 template <int KT>
 __global__ void __launch_bounds__(512)
     conv3_igemm_glds_kernel(const uint16_t* __restrict__ xh, const uint16_t* __restrict__ xl,
@@ -399,6 +448,54 @@ __global__ void __launch_bounds__(512)
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
 
+#ifndef PCFM_CONV_GLDS_NOPF
+  // Fragment registers double-buffered across steps: after the barrier of
+  // step s the waves read step s+1's fragments while step s's 24 MFMAs run,
+  // so the LDS read latency of a step hides behind the previous step's
+  // matrix work (the single-buffered form exposed it at every step: 2 waves
+  // per SIMD cannot cover it).  Stage s's LDS buffer is refilled (stage s+3)
+  // once every wave holds its fragments: lgkmcnt(0) + barrier.
+  bf16x8 F0[KT / 16][8], F1[KT / 16][8];
+  issue(0, 0);
+  if (nsteps > 1) issue(1, 1);
+  if (nsteps > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::APW + G::BPW) : "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  if (nsteps > 2) issue(2, 2);
+  glds_frags<KT>(lds, 0, wr, wc, r, h, F0);
+  // step s with the prefetch of step s+1 (s + 1 < nsteps)
+  auto step = [&](int s, bf16x8 (&Fc)[KT / 16][8], bf16x8 (&Fn)[KT / 16][8]) {
+    // stage s+1 landed (own pieces; stage s+2's stay in flight)
+    if (s + 2 < nsteps) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::APW + G::BPW) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's stage-s reads done
+    __builtin_amdgcn_s_barrier();
+#ifndef PCFM_EXP_NOLOAD
+    if (s + 3 < nsteps) issue(s + 3, s % kGStages);
+#endif
+    glds_frags<KT>(lds, (s + 1) % kGStages, wr, wc, r, h, Fn);
+    glds_mfma<KT>(Fc, acc);
+    // reads of step s+1 interleaved with the first MFMAs of step s (two
+    // ds_read_b128 per MFMA gap are free, microarch guide "LDS")
+#pragma unroll
+    for (int g = 0; g < 4 * (KT / 16); ++g) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 12 * (KT / 16) - 4 * (KT / 16), 0);
+  };
+  int s = 0;
+  for (; s + 2 < nsteps; s += 2) {
+    step(s, F0, F1);
+    step(s + 1, F1, F0);
+  }
+  if (s + 1 < nsteps) {
+    step(s, F0, F1);
+    glds_mfma<KT>(F1, acc);
+  } else {
+    glds_mfma<KT>(F0, acc);
+  }
+#else
   issue(0, 0);
   if (nsteps > 1) issue(1, 1);
   for (int s = 0; s < nsteps; ++s) {
@@ -451,6 +548,7 @@ __global__ void __launch_bounds__(512)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
     }
   }
+#endif
   float* __restrict__ yb = y + (size_t)b * M * V;
   float biasv[2][16];
 #pragma unroll
