@@ -260,7 +260,8 @@ def main():
         if not args.no_chamfer:
             cham = {"published_shape_32x2000x1000": chamfer_ms(dev, 32, 2000, 1000),
                     "published_fwd_bwd_ms": 1.4,
-                    "c2_shape_8x20000x20000": chamfer_ms(dev, 8, 20000, 20000, iters=5)}
+                    "c2_shape_8x20000x20000": chamfer_ms(dev, 8, 20000, 20000, iters=5),
+                    "c5_shape_4x100000x100000": chamfer_ms(dev, 4, 100000, 100000, iters=2)}
             log(f"chamfer: {cham}")
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
