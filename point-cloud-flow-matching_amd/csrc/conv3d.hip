@@ -372,7 +372,8 @@ __global__ void __launch_bounds__(512)
     conv3_igemm_glds_kernel(const uint16_t* __restrict__ xh, const uint16_t* __restrict__ xl,
                             const uint16_t* __restrict__ wh, const uint16_t* __restrict__ wl,
                             const uint16_t* __restrict__ zrow, const float* __restrict__ bias,
-                            float* __restrict__ y, int K, int M, int R) {
+                            float* __restrict__ y, int K, int M, int R, int S,
+                            float* __restrict__ part) {
   using G = GK<KT>;
   __shared__ __attribute__((aligned(16))) uint8_t lds[kGStages * G::STAGE];
   const int V = R * R * R, R2 = R * R;
@@ -382,13 +383,19 @@ __global__ void __launch_bounds__(512)
     id = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + id / 8;
   }
   const int nmt = M / kGM, nvt = V / kGN;
+  const int nb = (int)gridDim.x / (S * nmt * nvt);  // batch elements
   const int m0 = (id % nmt) * kGM;
   id /= nmt;
-  const int v0 = (id % nvt) * kGN, b = id / nvt;
+  const int v0 = (id % nvt) * kGN;
+  id /= nvt;
+  const int b = id % nb, sp = id / nb;
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   const int wr = w >> 2, wc = w & 3, r = lane & 31, h = lane >> 5;
-  const int nck = K / KT, nsteps = 27 * nck;
+  // split-K (small grids, r = 8): this block's K-steps [k0, k1) of 27 * K / KT
+  const int nall = 27 * (K / KT);
+  const int k0 = (int)((long long)nall * sp / S), k1 = (int)((long long)nall * (sp + 1) / S);
+  const int nsteps = k1 - k0;
   const size_t bV = (size_t)b * V;
   const int prow = lane / G::CPR, pch = lane % G::CPR;  // this lane's place in a piece
 
@@ -416,9 +423,10 @@ __global__ void __launch_bounds__(512)
     bxyz[q] = (v / R2) | (((v / R) % R) << 10) | ((v % R) << 20);
   }
 
-  auto issue = [&](int s, int buf) {
+  auto issue = [&](int sl, int buf) {
     // channel-chunk-major: the 27 taps of one chunk are consecutive, so the
     // neighbour rows they re-read stay in L2 (tap-major measured slower)
+    const int s = k0 + sl;
     const int c0 = (s / 27) * KT, tap = s - (s / 27) * 27;
     uint8_t* base = lds + buf * G::STAGE;
     const size_t aofs = (size_t)tap * M * K + c0;
@@ -549,10 +557,10 @@ __global__ void __launch_bounds__(512)
     }
   }
 #endif
-  float* __restrict__ yb = y + (size_t)b * M * V;
+  float* __restrict__ yb = S == 1 ? y + (size_t)b * M * V : part + ((size_t)sp * nb + b) * M * V;
   float biasv[2][16];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) load_bias16(bias, m0 + wr * 64 + i * 32, h, M, biasv[i]);
+  for (int i = 0; i < 2; ++i) load_bias16(S == 1 ? bias : nullptr, m0 + wr * 64 + i * 32, h, M, biasv[i]);
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -1064,6 +1072,51 @@ __global__ void __launch_bounds__(kW3Threads)
     const uint8_t* iAl = cur + kW3AImg;
     const uint8_t* iBh = cur + 2 * kW3AImg;
     const uint8_t* iBl = iBh + kW3BImg;
+#ifdef PCFM_WG3_KKPF
+    // operands of K-slice kk+1 read while kk's MFMAs run (two register sets)
+    bf16x8 F[2][8];
+    auto frags = [&](int kk, bf16x8 (&f)[8]) {
+      const int vk = v0 + kk * 16 + 8 * h;
+      const int xq = vk >> (2 * lgR), yq = (vk >> lgR) & (R - 1), z0 = vk & (R - 1);
+      const bool xyok = (unsigned)(xq + dx) < (unsigned)R && (unsigned)(yq + dy_) < (unsigned)R;
+      const uint32_t mall = xyok ? 0xFFFFFFFFu : 0u;
+      const uint32_t m0 = (dz < 0 && z0 == 0) ? (mall & 0xFFFF0000u) : mall;
+      const uint32_t m3 = (dz > 0 && z0 + 8 == R) ? (mall & 0x0000FFFFu) : mall;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        f[i] = tr_operand_rows(iAh, kk * 16, wr * 64 + i * 32, lane);
+        f[2 + i] = tr_operand_rows(iAl, kk * 16, wr * 64 + i * 32, lane);
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        f[4 + j] = mask_k8(tr_operand_rows(iBh, kk * 16 + 1 + dz, wc * 64 + j * 32, lane), m0,
+                           mall, m3);
+        f[6 + j] = mask_k8(tr_operand_rows(iBl, kk * 16 + 1 + dz, wc * 64 + j * 32, lane), m0,
+                           mall, m3);
+      }
+    };
+    frags(0, F[0]);
+#pragma unroll
+    for (int kk = 0; kk < kWV / 16; ++kk) {
+      if (kk + 1 < kWV / 16) frags(kk + 1, F[(kk + 1) & 1]);
+      const bf16x8(&f)[8] = F[kk & 1];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f[i], f[4 + j], acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f[i], f[6 + j], acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f[2 + i], f[4 + j], acc[i][j], 0, 0, 0);
+    }
+#else
 #pragma unroll
     for (int kk = 0; kk < kWV / 16; ++kk) {
       // validity of this lane's 8 voxels for tap (dx, dy, dz)
@@ -1102,6 +1155,7 @@ __global__ void __launch_bounds__(kW3Threads)
         for (int j = 0; j < 2; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
     }
+#endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // step ks+1 landed (this wave's pieces)
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
@@ -1333,9 +1387,35 @@ static bool igemm_big(int b, int cout, int r) {
   return big_blocks >= 2 * kCUs;
 }
 
+#ifndef PCFM_CONV_GLDS_MINV
+#define PCFM_CONV_GLDS_MINV 512  // 4096: r = 8 on the 64x64-tile kernel instead
+#endif
+// LDS-DMA kernel applies (128 x 256 tiles); small grids (r = 8) split K so
+// that about one block per CU runs, >= 8 K-steps per split, ordered reduce.
+static bool glds_ok(int cout, int r) {
+  const int V = r * r * r;
+  return V % kGN == 0 && V >= PCFM_CONV_GLDS_MINV && cout % kGM == 0;
+}
+
+static int glds_splits(int b, int cin, int cout, int r) {
+  const int V = r * r * r;
+  const long long items = (long long)(V / kGN) * (cout / kGM) * b;
+  const long long nall = 27LL * (cin / 16);  // K-steps at KT = 16 (the shorter bound)
+  long long s = std::max(1LL, (long long)kCUs / std::max(1LL, items));
+  s = std::min(s, std::max(1LL, nall / 16));
+  return (int)std::min(s, 8LL);
+}
+
 extern "C" size_t pcfm_conv3d_igemm_cl_workspace_bytes(int b, int cin, int cout, int r) {
   if (!conv3_shape_ok(b, cin, cout, r)) return 0;
-  if (b == 0 || igemm_big(b, cout, r)) return 1;
+  if (b == 0) return 1;
+#ifndef PCFM_CONV_NOGLDS
+  if (glds_ok(cout, r)) {
+    const int S = glds_splits(b, cin, cout, r);
+    return S == 1 ? 1 : (size_t)S * b * cout * r * r * r * sizeof(float);
+  }
+#endif
+  if (igemm_big(b, cout, r)) return 1;
   const int S = igemm_splits(b, cin, cout, r);
   return S == 1 ? 1 : (size_t)S * b * cout * r * r * r * sizeof(float);
 }
@@ -1354,15 +1434,20 @@ extern "C" int pcfm_conv3d_igemm_cl(const void* xs, const void* wsplit, const fl
   hipStream_t st = (hipStream_t)stream;
   const long long big_blocks = (long long)(V / 128) * (cout / 128) * b;
 #ifndef PCFM_CONV_NOGLDS
-  const long long glds_blocks = (long long)(V / kGN) * (cout / kGM) * b;
-  if (V % kGN == 0 && V >= 4096 && cout % kGM == 0) {  // r >= 16 (r = 8: 64x64 tiles)
+  if (glds_ok(cout, r)) {
+    const int S = glds_splits(b, cin, cout, r);
+    const long long glds_blocks = (long long)(V / kGN) * (cout / kGM) * b * S;
+    const size_t need = pcfm_conv3d_igemm_cl_workspace_bytes(b, cin, cout, r);
+    PCFM_CHECK_ARG(S == 1 || (ws != nullptr && ws_bytes >= need),
+                   "conv3d_igemm_cl: workspace %zu < %zu bytes", ws_bytes, need);
+    float* part = S == 1 ? nullptr : (float*)ws;
     const uint16_t* zrow = zero_row();  // 64 B of zeros: the padding row
     if (zrow == nullptr) {
       set_error("conv3d_igemm_cl: zero-row allocation failed");
       return (int)hipErrorOutOfMemory;
     }
 #ifdef PCFM_CONV_GLDS3  // three-tap variant: 3x less X traffic, measured equal speed
-    if (cin % kHK == 0) {
+    if (S == 1 && cin % kHK == 0) {
       hipLaunchKernelGGL(conv3_igemm_glds3_kernel, dim3((unsigned)glds_blocks), dim3(512), 0, st,
                          xh, xl, wh, wh + total, bias, y, cin, cout, r);
       return check_launch("conv3d_igemm_cl");
@@ -1373,10 +1458,15 @@ extern "C" int pcfm_conv3d_igemm_cl(const void* xs, const void* wsplit, const fl
 #endif
     if (PCFM_CONV_GK == 16 || cin % 32 != 0)
       hipLaunchKernelGGL(conv3_igemm_glds_kernel<16>, dim3((unsigned)glds_blocks), dim3(512), 0,
-                         st, xh, xl, wh, wh + total, zrow, bias, y, cin, cout, r);
+                         st, xh, xl, wh, wh + total, zrow, bias, y, cin, cout, r, S, part);
     else
       hipLaunchKernelGGL(conv3_igemm_glds_kernel<32>, dim3((unsigned)glds_blocks), dim3(512), 0,
-                         st, xh, xl, wh, wh + total, zrow, bias, y, cin, cout, r);
+                         st, xh, xl, wh, wh + total, zrow, bias, y, cin, cout, r, S, part);
+    if (S > 1) {
+      const long long total4 = (long long)b * cout * V / 4;
+      hipLaunchKernelGGL(conv3_ksum_kernel, dim3((unsigned)ceil_div(total4, 256)), dim3(256), 0,
+                         st, (const float*)part, bias, S, cout, V, total4, y);
+    }
     return check_launch("conv3d_igemm_cl");
   }
 #endif

@@ -27,7 +27,7 @@ def ops():
 
 @pytest.mark.parametrize("b,cin,cout,r", [(2, 128, 128, 8), (1, 128, 256, 8), (1, 256, 128, 8),
                                           (2, 128, 128, 16), (1, 256, 256, 8), (1, 128, 128, 32),
-                                          (1, 128, 128, 24)])
+                                          (1, 128, 128, 24), (8, 256, 256, 8)])
 def test_conv3d_fwd_bwd_vs_fp64(ops, b, cin, cout, r):
     g = torch.Generator(device="cuda").manual_seed(b * 1000 + cin + r)
     x = torch.randn(b, cin, r, r, r, device="cuda", generator=g)
