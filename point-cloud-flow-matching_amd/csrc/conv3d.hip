@@ -1072,51 +1072,6 @@ __global__ void __launch_bounds__(kW3Threads)
     const uint8_t* iAl = cur + kW3AImg;
     const uint8_t* iBh = cur + 2 * kW3AImg;
     const uint8_t* iBl = iBh + kW3BImg;
-#ifdef PCFM_WG3_KKPF
-    // operands of K-slice kk+1 read while kk's MFMAs run (two register sets)
-    bf16x8 F[2][8];
-    auto frags = [&](int kk, bf16x8 (&f)[8]) {
-      const int vk = v0 + kk * 16 + 8 * h;
-      const int xq = vk >> (2 * lgR), yq = (vk >> lgR) & (R - 1), z0 = vk & (R - 1);
-      const bool xyok = (unsigned)(xq + dx) < (unsigned)R && (unsigned)(yq + dy_) < (unsigned)R;
-      const uint32_t mall = xyok ? 0xFFFFFFFFu : 0u;
-      const uint32_t m0 = (dz < 0 && z0 == 0) ? (mall & 0xFFFF0000u) : mall;
-      const uint32_t m3 = (dz > 0 && z0 + 8 == R) ? (mall & 0x0000FFFFu) : mall;
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        f[i] = tr_operand_rows(iAh, kk * 16, wr * 64 + i * 32, lane);
-        f[2 + i] = tr_operand_rows(iAl, kk * 16, wr * 64 + i * 32, lane);
-      }
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        f[4 + j] = mask_k8(tr_operand_rows(iBh, kk * 16 + 1 + dz, wc * 64 + j * 32, lane), m0,
-                           mall, m3);
-        f[6 + j] = mask_k8(tr_operand_rows(iBl, kk * 16 + 1 + dz, wc * 64 + j * 32, lane), m0,
-                           mall, m3);
-      }
-    };
-    frags(0, F[0]);
-#pragma unroll
-    for (int kk = 0; kk < kWV / 16; ++kk) {
-      if (kk + 1 < kWV / 16) frags(kk + 1, F[(kk + 1) & 1]);
-      const bf16x8(&f)[8] = F[kk & 1];
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f[i], f[4 + j], acc[i][j], 0, 0, 0);
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f[i], f[6 + j], acc[i][j], 0, 0, 0);
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f[2 + i], f[4 + j], acc[i][j], 0, 0, 0);
-    }
-#else
 #pragma unroll
     for (int kk = 0; kk < kWV / 16; ++kk) {
       // validity of this lane's 8 voxels for tap (dx, dy, dz)
@@ -1155,7 +1110,6 @@ __global__ void __launch_bounds__(kW3Threads)
         for (int j = 0; j < 2; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
     }
-#endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // step ks+1 landed (this wave's pieces)
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
