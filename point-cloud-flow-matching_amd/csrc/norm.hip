@@ -19,6 +19,7 @@ namespace pcfm {
 namespace {
 
 constexpr int kBnParts = 16;  // target blocks per channel in the stats passes
+constexpr int kBnUnroll = 4;  // float4 loads per thread issued together in the stats passes
 inline int bn_parts(int b) { return b * ((kBnParts + b - 1) / b); }
 
 __device__ __forceinline__ float act(float v, float slope) {
@@ -64,12 +65,21 @@ __global__ void __launch_bounds__(256)
   part_range(S4, p - b * PS, PS, s0, s1);
   const float4* __restrict__ x4 = reinterpret_cast<const float4*>(x) + ((size_t)b * C + c) * S4;
   float s = 0.0f, q = 0.0f;
-  for (int s4 = s0 + threadIdx.x; s4 < s1; s4 += 256) {
-    const float4 v = x4[s4];
+  auto add = [&](const float4 v) {
     const float d0 = v.x - K, d1 = v.y - K, d2 = v.z - K, d3 = v.w - K;
     s += (d0 + d1) + (d2 + d3);
     q += (d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3);
+  };
+  int s4 = s0 + threadIdx.x;
+  // kBnUnroll float4 loads in flight per thread before the first use
+  for (; s4 + (kBnUnroll - 1) * 256 < s1; s4 += kBnUnroll * 256) {
+    float4 v[kBnUnroll];
+#pragma unroll
+    for (int u = 0; u < kBnUnroll; ++u) v[u] = x4[s4 + u * 256];
+#pragma unroll
+    for (int u = 0; u < kBnUnroll; ++u) add(v[u]);
   }
+  for (; s4 < s1; s4 += 256) add(x4[s4]);
   block_sum2(s, q, sh);
   if (threadIdx.x == 0) {
     part[((size_t)c * P + p) * 2] = s;
@@ -142,8 +152,7 @@ __global__ void __launch_bounds__(256)
   const float4* __restrict__ x4 = reinterpret_cast<const float4*>(x) + row;
   const float4* __restrict__ d4 = reinterpret_cast<const float4*>(dz) + row;
   float sg = 0.0f, sgx = 0.0f;
-  for (int s4 = s0 + threadIdx.x; s4 < s1; s4 += 256) {
-    const float4 v = x4[s4], d = d4[s4];
+  auto add = [&](const float4 v, const float4 d) {
     const float xv[4] = {v.x, v.y, v.z, v.w}, dv[4] = {d.x, d.y, d.z, d.w};
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -152,7 +161,20 @@ __global__ void __launch_bounds__(256)
       sg += g;
       sgx += g * xh;
     }
+  };
+  int s4 = s0 + threadIdx.x;
+  // same per-thread summation order as one-at-a-time; only the loads move up
+  for (; s4 + (kBnUnroll - 1) * 256 < s1; s4 += kBnUnroll * 256) {
+    float4 v[kBnUnroll], d[kBnUnroll];
+#pragma unroll
+    for (int u = 0; u < kBnUnroll; ++u) {
+      v[u] = x4[s4 + u * 256];
+      d[u] = d4[s4 + u * 256];
+    }
+#pragma unroll
+    for (int u = 0; u < kBnUnroll; ++u) add(v[u], d[u]);
   }
+  for (; s4 < s1; s4 += 256) add(x4[s4], d4[s4]);
   block_sum2(sg, sgx, sh);
   if (threadIdx.x == 0) {
     part[((size_t)c * P + p) * 2] = sg;

@@ -36,10 +36,13 @@ namespace pcfm {
 namespace {  // kernels get internal linkage: this header is included by several .hip files
 
 // --------------------------------------------------------------------------
-// 1: counting sort by key, one block (1024 threads) per batch element.
-// The key histogram lives in LDS (kSortKeys ints = 128 KiB; larger key spaces
-// take several passes over the keys), so counting and ranking use LDS atomics
-// only.
+// 1: counting sort by key.  Block (p, b) owns the key range [p, p+1) * span of
+// batch element b (grid = (P, B), 1024 threads): every block reads all n keys
+// of its batch element (L2-resident, 80 KB at N = 20000), counts the keys
+// BELOW its range itself -- its base in the sorted order, so the P blocks never
+// wait for each other -- and histograms / ranks its own keys in LDS
+// (kSortKeys ints = 128 KiB; a wider range takes several passes).  One block
+// per batch element left 248 of 256 CUs idle for the ~23 us of the sort.
 //   start[b, 0..V]  exclusive prefix of the counts (start[b, V] = total)
 //   cnt_out[b, v]   the counts (optional: the voxelization's `cnt` output)
 //   vinv[b, v]      (float)(1.0 / (double)cnt) (optional, vox.cu:66)
@@ -47,34 +50,55 @@ namespace {  // kernels get internal linkage: this header is included by several
 //                   key is outside [0, V) (the item contributes nothing)
 // --------------------------------------------------------------------------
 constexpr int kSortKeys = 32768;
-constexpr int kSortBatch = 8;  // keys per thread in flight
+constexpr int kSortBatch = 8;     // keys per thread in flight
+constexpr int kSortMinSpan = 256;  // keys per block at least
+constexpr int kSortMaxParts = 16;  // blocks per batch element at most
+
+inline int seg_sort_parts(int V) {
+  return std::max(1, std::min(kSortMaxParts, V / kSortMinSpan));
+}
+inline int seg_sort_span(int V) { return (V + seg_sort_parts(V) - 1) / seg_sort_parts(V); }
 
 __global__ void __launch_bounds__(1024)
-    seg_sort_kernel(const int* __restrict__ key, long long key_bstride, int n, int V,
+    seg_sort_kernel(const int* __restrict__ key, long long key_bstride, int n, int V, int span,
                     int* __restrict__ start, int* __restrict__ cnt_out, float* __restrict__ vinv,
                     int* __restrict__ rank) {
-  extern __shared__ int hist[];  // [min(V, kSortKeys)]
+  extern __shared__ int hist[];  // [min(span, kSortKeys)]
   __shared__ int wsum[16];
-  const int b = blockIdx.x;
+  const int p = blockIdx.x, b = blockIdx.y;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int* __restrict__ kb = key + (size_t)b * key_bstride;
   int* __restrict__ sb = start + (size_t)b * (V + 1);
   int* __restrict__ rb = rank + (size_t)b * n;
+  const int pk0 = min(V, p * span), pk1 = min(V, pk0 + span);
   int carry = 0;
-  for (int k0 = 0; k0 < V; k0 += kSortKeys) {
-    const int len = min(kSortKeys, V - k0);
+  for (int k0 = pk0; k0 < pk1; k0 += kSortKeys) {
+    const int len = min(kSortKeys, pk1 - k0);
     for (int e = t; e < len; e += 1024) hist[e] = 0;
     __syncthreads();
+    int below = 0;  // first chunk: keys in [0, pk0) -> this block's base
     for (int i0 = 0; i0 < n; i0 += 1024 * kSortBatch) {
       int kk[kSortBatch];  // keys first (independent loads), then the LDS atomics
 #pragma unroll
       for (int q = 0; q < kSortBatch; ++q) {
         const int i = i0 + q * 1024 + t;
-        kk[q] = i < n ? kb[i] - k0 : -1;
+        kk[q] = i < n ? kb[i] : -1;
       }
 #pragma unroll
-      for (int q = 0; q < kSortBatch; ++q)
-        if ((unsigned)kk[q] < (unsigned)len) atomicAdd(hist + kk[q], 1);
+      for (int q = 0; q < kSortBatch; ++q) {
+        if ((unsigned)(kk[q] - k0) < (unsigned)len) atomicAdd(hist + (kk[q] - k0), 1);
+        below += (k0 == pk0 && (unsigned)kk[q] < (unsigned)pk0) ? 1 : 0;
+      }
+    }
+    if (k0 == pk0) {
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) below += __shfl_xor(below, o, 64);
+      if (lane == 0) wsum[w] = below;
+    }
+    __syncthreads();
+    if (k0 == pk0) {
+#pragma unroll
+      for (int g = 0; g < 16; ++g) carry += wsum[g];
     }
     __syncthreads();
     // exclusive scan: wave w owns the 64-aligned segment [lo, hi)
@@ -117,19 +141,19 @@ __global__ void __launch_bounds__(1024)
 #pragma unroll
       for (int q = 0; q < kSortBatch; ++q) {
         const int i = i0 + q * 1024 + t;
-        kk[q] = i < n ? kb[i] - k0 : -1;
+        kk[q] = i < n ? kb[i] : -1;
       }
 #pragma unroll
       for (int q = 0; q < kSortBatch; ++q) {
         const int i = i0 + q * 1024 + t;
-        if ((unsigned)kk[q] < (unsigned)len) rb[i] = atomicAdd(hist + kk[q], 1);
-        else if (k0 == 0 && i < n && (unsigned)(kk[q] + k0) >= (unsigned)V) rb[i] = -1;
+        if ((unsigned)(kk[q] - k0) < (unsigned)len) rb[i] = atomicAdd(hist + (kk[q] - k0), 1);
+        else if (p == 0 && k0 == pk0 && i < n && (unsigned)kk[q] >= (unsigned)V) rb[i] = -1;
       }
     }
     carry += total;
     __syncthreads();
   }
-  if (t == 0) sb[V] = carry;
+  if (t == 0 && pk1 == V && (pk0 < V || p == 0)) sb[V] = carry;
 }
 
 // --------------------------------------------------------------------------
@@ -568,11 +592,12 @@ inline int seg_scatter(const float* in, const int* key, long long key_bstride, b
                        float* out, void* ws, hipStream_t st, const char* what) {
   if (B == 0 || V == 0) return PCFM_OK;
   SegWs w = seg_ws_carve(ws, B, C, n, V, TAPS);
-  const size_t sort_lds = (size_t)std::min(V, kSortKeys) * sizeof(int);
+  const int span = seg_sort_span(V);
+  const size_t sort_lds = (size_t)std::min(span, kSortKeys) * sizeof(int);
   int e = allow_big_lds((const void*)seg_sort_kernel);
   if (e) return e;
-  hipLaunchKernelGGL(seg_sort_kernel, dim3(B), dim3(1024), sort_lds, st, key, key_bstride, n, V,
-                     w.start, cnt_out, avg ? w.vinv : nullptr, w.rank);
+  hipLaunchKernelGGL(seg_sort_kernel, dim3(seg_sort_parts(V), B), dim3(1024), sort_lds, st, key,
+                     key_bstride, n, V, span, w.start, cnt_out, avg ? w.vinv : nullptr, w.rank);
   if (C == 0) return check_launch(what);
   const int tiles = seg_tiles(V), umax = seg_umax(n, V, TAPS), slots = umax - tiles;
   hipLaunchKernelGGL(seg_units_kernel<TAPS>, dim3(B), dim3(1024), 0, st, w.start, V, r, tiles,

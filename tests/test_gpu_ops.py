@@ -48,6 +48,7 @@ VOX_CASES = [
     (2, 64, 5000, 16, "clustered"),
     (2, 128, 20000, 32, "clustered"),
     (1, 3, 4000, 64, "uniform"),     # r^3 > LDS row: chunked path
+    (2, 2, 3000, 100, "uniform"),    # sort blocks each span > LDS: multi-pass per block
     (2, 5, 300, 4, "one_voxel"),     # every point in one voxel
     (1, 7, 0, 4, "uniform"),         # empty cloud
     (2, 3, 17, 1, "uniform"),        # r = 1
@@ -82,7 +83,7 @@ def test_avg_voxelize(b, c, n, r, layout):
 # ---------------------------------------------------------------- devoxelize
 DEVOX_CASES = [
     (2, 4, 100, 2), (3, 16, 1000, 8), (2, 256, 20000, 8), (2, 256, 20000, 16),
-    (2, 128, 20000, 32), (1, 3, 3000, 64), (1, 5, 0, 4), (2, 3, 50, 1),
+    (2, 128, 20000, 32), (1, 3, 3000, 64), (1, 5, 0, 4), (2, 3, 50, 1), (1, 2, 2000, 100),
 ]
 
 
