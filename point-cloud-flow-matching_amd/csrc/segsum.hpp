@@ -167,6 +167,11 @@ __global__ void __launch_bounds__(1024)
 #define PCFM_ROWS_ITEMS 64
 #endif
 constexpr int kRowsItems = PCFM_ROWS_ITEMS;  // items per block (64 or 128)
+#ifndef PCFM_ROWS_ALLC
+#define PCFM_ROWS_ALLC 1
+#endif
+// 64-item blocks loop over all channel groups (grid.y = 1)
+constexpr bool kRowsAllC = PCFM_ROWS_ALLC && kRowsItems == 64;
 
 __global__ void __launch_bounds__(256)
     seg_rows_kernel(const float* __restrict__ in, const int* __restrict__ rank,
@@ -213,6 +218,32 @@ __global__ void __launch_bounds__(256)
       tile[cc][2 * lane] = v.x;
       tile[cc][2 * lane + 1] = v.y;
     }
+  } else if (kRowsAllC) {
+    // every channel group of the block's items in turn: an item's whole row
+    // (C floats) is written by one wave within a few hundred cycles, instead of
+    // in C/64 pieces by blocks dispatched far apart
+    const int j = j0 + lane;
+    __syncthreads();
+    for (int g0 = 0; g0 < C; g0 += 64) {
+      float v[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int c = g0 + w + 4 * q;
+        v[q] = (c < C && j < n) ? in[((size_t)b * C + c) * n + j] : 0.0f;
+      }
+#pragma unroll
+      for (int q = 0; q < 16; ++q) tile[w + 4 * q][lane] = v[q];
+      __syncthreads();
+      const int c = g0 + lane;
+      if (c < C) {
+        for (int jr = w; jr < kRowsItems; jr += 4) {
+          const int r = rk[jr];
+          if (r >= 0) xs[((size_t)b * n + r) * C + c] = tile[lane][jr];
+        }
+      }
+      __syncthreads();
+    }
+    return;
   } else {
     const int j = j0 + lane;
     for (int cc = w; cc < 64; cc += 4) {
@@ -603,7 +634,8 @@ inline int seg_scatter(const float* in, const int* key, long long key_bstride, b
   hipLaunchKernelGGL(seg_units_kernel<TAPS>, dim3(B), dim3(1024), 0, st, w.start, V, r, tiles,
                      umax, w.units, w.tinfo, w.nunits);
   if (n > 0)
-    hipLaunchKernelGGL(seg_rows_kernel, dim3(ceil_div(n, kRowsItems), ceil_div(C, 64), B),
+    hipLaunchKernelGGL(seg_rows_kernel,
+                       dim3(ceil_div(n, kRowsItems), kRowsAllC ? 1 : ceil_div(C, 64), B),
                        dim3(256), 0,
                        st, in, w.rank, key, key_bstride, TAPS == 8 ? tapw : nullptr, C, n, w.xs,
                        w.skey, w.ws8);
