@@ -416,6 +416,18 @@ int pcfm_bn_act_bwd(const float* dz, const float* x, const float* gamma, const f
                     float* dx, float* dgamma, float* dbeta, float* dbias_in, void* ws,
                     size_t ws_bytes, void* stream);
 
+/* pcfm_bn_act_bwd for a voxel convolution's output x [b][c][s] (c, s multiples
+ * of 64) whose dx only feeds that convolution's backward: dx is written
+ * directly as the channels-last bf16 hi/lo split of pcfm_conv3d_split
+ * (dxs: pcfm_conv3d_split_bytes(b, c, r) bytes, r^3 = s), not as fp32.
+ * dgamma / dbeta / dbias_in as pcfm_bn_act_bwd (dbias_in summed per 64-voxel
+ * tile, then over tiles in a fixed order). */
+size_t pcfm_bn_act_bwd_split_workspace_bytes(int b, int c, int s);
+int pcfm_bn_act_bwd_split(const float* dz, const float* x, const float* gamma, const float* beta,
+                          const float* mean, const float* invstd, int b, int c, int s,
+                          float slope, void* dxs, float* dgamma, float* dbeta, float* dbias_in,
+                          void* ws, size_t ws_bytes, void* stream);
+
 /* GroupNorm + FiLM + residual of the hybrid backbone's PV blocks
  * (models.py:322-346 _FiLM1d(norm="group"), :349-368 _PVBlock):
  *   out = x + (GroupNorm(x; groups, w, bias, eps) * (1 + gamma[b]) + beta[b])

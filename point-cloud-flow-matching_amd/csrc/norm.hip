@@ -250,6 +250,86 @@ __global__ void __launch_bounds__(256)
   if (lane == 0) dbias[c] = s;
 }
 
+// dbias[c] = sum over (b, k) of rowpart[(b * C + c) * nch + k] for long rows:
+// one block per channel, thread-strided in a fixed order, then a fixed tree.
+__global__ void __launch_bounds__(256)
+    bn_bias_finalize_block_kernel(const float* __restrict__ rowpart, int B, int C, int nch,
+                                  float* __restrict__ dbias) {
+  __shared__ float sh[8];
+  const int c = blockIdx.x;
+  float s = 0.0f;
+  for (int bb = 0; bb < B; ++bb) {
+    const float* __restrict__ rp = rowpart + ((size_t)bb * C + c) * nch;
+    for (int k = threadIdx.x; k < nch; k += 256) s += rp[k];
+  }
+  float z = 0.0f;
+  block_sum2(s, z, sh);
+  if (threadIdx.x == 0) dbias[c] = s;
+}
+
+// BN backward apply for a voxel convolution's output, fused with the
+// channels-last bf16 hi/lo split the convolution's backward reads
+// (conv3_split_cl_kernel): dx is never written as fp32 [B][C][V].
+// grid = (S / 64, C / 64, B), 256 threads; a 64 x 64 LDS tile.
+// rowpart[(b * C + c) * (S / 64) + vb] = sum of dx over the tile's 64 voxels
+// (fixed order: 16 sequential per thread, then a 4-lane xor tree).
+typedef __bf16 bn_bf16x2 __attribute__((ext_vector_type(2)));
+__global__ void __launch_bounds__(256)
+    bn_bwd_apply_split_kernel(const float* __restrict__ dz, const float* __restrict__ x,
+                              const float* __restrict__ mean, const float* __restrict__ invstd,
+                              const float* __restrict__ gamma, const float* __restrict__ beta,
+                              const float* __restrict__ dgamma, const float* __restrict__ dbeta,
+                              int C, int S, float inv_n, float slope, uint16_t* __restrict__ dxh,
+                              uint16_t* __restrict__ dxl, float* __restrict__ rowpart) {
+  __shared__ float tile[64][65];
+  const int v0 = blockIdx.x * 64, c0 = blockIdx.y * 64, b = blockIdx.z;
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+  const size_t rbase = ((size_t)b * C + c0) * S + v0;
+  float xv[16], dv[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const size_t o = rbase + (size_t)(4 * i + w) * S + lane;
+    xv[i] = x[o];
+    dv[i] = dz[o];
+  }
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int c = c0 + 4 * i + w;
+    const float m = mean[c], is = invstd[c], gm = gamma[c], bt = beta[c];
+    const float mg = dbeta[c] * inv_n, mgx = dgamma[c] * inv_n, k = gm * is;
+    const float xh = (xv[i] - m) * is;
+    const float g = __builtin_fmaf(xh, gm, bt) > 0.0f ? dv[i] : dv[i] * slope;
+    tile[4 * i + w][lane] = k * ((g - mg) - xh * mgx);
+  }
+  __syncthreads();
+  {
+    const int v = t >> 2, cg = (t & 3) * 16;
+    const size_t o = ((size_t)b * S + v0 + v) * C + c0 + cg;
+    uint32_t* h32 = reinterpret_cast<uint32_t*>(dxh + o);
+    uint32_t* l32 = reinterpret_cast<uint32_t*>(dxl + o);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const float f0 = tile[cg + 2 * q][v], f1 = tile[cg + 2 * q + 1][v];
+      bn_bf16x2 hi, lo;
+      hi.x = (__bf16)f0;
+      hi.y = (__bf16)f1;
+      lo.x = (__bf16)(f0 - (float)hi.x);
+      lo.y = (__bf16)(f1 - (float)hi.y);
+      h32[q] = __builtin_bit_cast(uint32_t, hi);
+      l32[q] = __builtin_bit_cast(uint32_t, lo);
+    }
+  }
+  if (rowpart != nullptr) {
+    const int c = t >> 2, vq = (t & 3) * 16;
+    float sum = 0.0f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) sum += tile[c][vq + q];
+    sum += __shfl_xor(sum, 1, 64);
+    sum += __shfl_xor(sum, 2, 64);
+    if ((t & 3) == 0) rowpart[((size_t)b * C + c0 + c) * (S / 64) + blockIdx.x] = sum;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // GroupNorm + FiLM + residual of the hybrid backbone's PV blocks
 // (reference models.py:322-346 _FiLM1d with GroupNorm, :349-368 _PVBlock):
@@ -556,6 +636,37 @@ extern "C" int pcfm_bn_act_bwd(const float* dz, const float* x, const float* gam
     hipLaunchKernelGGL(bn_bias_finalize_kernel, dim3(ceil_div(c, 4)), dim3(256), 0, st,
                        (const float*)rowpart, b, c, nch, dbias_in);
   return check_launch("bn_act_bwd");
+}
+
+extern "C" size_t pcfm_bn_act_bwd_split_workspace_bytes(int b, int c, int s) {
+  if (!bn_ok(b, c, s) || c % 64 != 0 || s % 64 != 0) return 0;
+  return ((size_t)c * bn_parts(b) * 2 + (size_t)b * c * (s / 64)) * sizeof(float);
+}
+
+extern "C" int pcfm_bn_act_bwd_split(const float* dz, const float* x, const float* gamma,
+                                     const float* beta, const float* mean, const float* invstd,
+                                     int b, int c, int s, float slope, void* dxs, float* dgamma,
+                                     float* dbeta, float* dbias_in, void* ws, size_t ws_bytes,
+                                     void* stream) {
+  PCFM_CHECK_ARG(bn_ok(b, c, s) && c % 64 == 0 && s % 64 == 0 && (long long)b < 65536,
+                 "bn_act_bwd_split: bad shape b=%d c=%d s=%d (c, s multiples of 64)", b, c, s);
+  PCFM_CHECK_ARG(ws_bytes >= pcfm_bn_act_bwd_split_workspace_bytes(b, c, s),
+                 "bn_act_bwd_split: workspace too small");
+  hipStream_t st = (hipStream_t)stream;
+  float* part = (float*)ws;
+  hipLaunchKernelGGL(bn_bwd_stats_kernel, dim3(c, bn_parts(b)), dim3(256), 0, st, dz, x, mean,
+                     invstd, gamma, beta, b, c, s, slope, part);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(ceil_div(c, 256)), dim3(256), 0, st,
+                     (const float*)part, c, bn_parts(b), dgamma, dbeta);
+  float* rowpart = dbias_in != nullptr ? part + (size_t)c * bn_parts(b) * 2 : nullptr;
+  uint16_t* dxh = (uint16_t*)dxs;
+  hipLaunchKernelGGL(bn_bwd_apply_split_kernel, dim3(s / 64, c / 64, b), dim3(256), 0, st, dz, x,
+                     mean, invstd, gamma, beta, (const float*)dgamma, (const float*)dbeta, c, s,
+                     (float)(1.0 / ((double)b * s)), slope, dxh, dxh + (size_t)b * s * c, rowpart);
+  if (dbias_in != nullptr)
+    hipLaunchKernelGGL(bn_bias_finalize_block_kernel, dim3(c), dim3(256), 0, st,
+                       (const float*)rowpart, b, c, s / 64, dbias_in);
+  return check_launch("bn_act_bwd_split");
 }
 
 extern "C" size_t pcfm_gn_film_workspace_bytes(int b, int c, int n, int groups) {

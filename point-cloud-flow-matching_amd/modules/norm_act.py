@@ -98,9 +98,10 @@ class _Conv3dBnAct(torch.autograd.Function):
         from pcfm import ops
         xs, w, y, gamma, beta, mean, invstd = ctx.saved_tensors
         bsz, cin, cout, r = ctx.dims
-        dy, dgamma, dbeta, db = ops.bn_act_backward(dz, y, gamma, beta, mean, invstd, ctx.slope,
-                                                    want_dbias_in=ctx.has_bias)
-        gys = ops.conv3d_split(dy)
+        # BN backward writes d(conv output) straight into the split layout the
+        # conv's backward GEMMs read (no fp32 dy pass)
+        gys, dgamma, dbeta, db = ops.bn_act_backward_split(dz, y, gamma, beta, mean, invstd,
+                                                           ctx.slope, want_dbias_in=ctx.has_bias)
         dx = dw = None
         if ctx.needs_input_grad[0]:
             dx = ops.conv3d_igemm_split(gys, ops.conv3d_prep_weight(w, True), None, bsz, cout, cin,

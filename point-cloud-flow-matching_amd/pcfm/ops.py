@@ -872,6 +872,29 @@ def bn_act_backward(dz: torch.Tensor, x: torch.Tensor, weight, bias, mean, invst
     return dx, dgb[0], dgb[1], (dgb[2] if want_dbias_in else None)
 
 
+def bn_act_backward_split(dz: torch.Tensor, x: torch.Tensor, weight, bias, mean, invstd,
+                          slope: float, want_dbias_in: bool = False):
+    """bn_act_backward for a voxel conv output x (B, C, R, R, R) whose dx only feeds
+    that conv's backward: -> (split(dx) as conv3d_split lays it out, dgamma, dbeta,
+    dbias_in or None); dx is never materialised in fp32."""
+    dz = dz.contiguous()
+    b, c, r = x.shape[0], x.shape[1], x.shape[2]
+    s = x.numel() // max(1, b * c)
+    n = _lib.query("pcfm_conv3d_split_bytes", b, c, r)
+    wsb = _lib.query("pcfm_bn_act_bwd_split_workspace_bytes", b, c, s)
+    if n == 0 or wsb == 0:
+        raise RuntimeError(f"bn_act_backward_split: unsupported shape {tuple(x.shape)}")
+    dxs = torch.empty(n, dtype=torch.uint8, device=x.device)
+    dgb = torch.empty((3, c), dtype=torch.float32, device=x.device)
+    ws = _workspace(wsb, x)
+    with _timed("bn_act_bwd", 4 * 5 * x.numel(), x):
+        _lib.call("pcfm_bn_act_bwd_split", _ptr(dz), _ptr(x), _ptr(weight), _ptr(bias),
+                  _ptr(mean), _ptr(invstd), b, c, s, float(slope), _ptr(dxs), _ptr(dgb[0]),
+                  _ptr(dgb[1]), _ptr(dgb[2]) if want_dbias_in else None, _ptr(ws), ws.numel(),
+                  _stream(x))
+    return dxs, dgb[0], dgb[1], (dgb[2] if want_dbias_in else None)
+
+
 def rows_max_bf16(h: torch.Tensor):
     """(values bf16 (B, C), indices int32 (B, C)) = max over dim 1 of h (B, N, C) bf16."""
     _check_cuda(h, "h")

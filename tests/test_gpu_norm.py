@@ -161,3 +161,30 @@ def test_gn_silu_matches_torch(ops, b, c, n, groups):
     for a, r in zip(got, grads_ref):
         scale = r.abs().max().item()
         torch.testing.assert_close(a, r, rtol=1e-4, atol=1e-4 * max(1.0, scale))
+
+
+@pytest.mark.parametrize("b,c,r,slope", [(2, 128, 16, 0.1), (8, 256, 8, 0.1), (1, 64, 4, 0.0)])
+def test_bn_act_backward_split_matches_unfused(ops, b, c, r, slope):
+    """pcfm_bn_act_bwd_split == pcfm_bn_act_bwd followed by pcfm_conv3d_split:
+    the split images bit for bit (same per-element formula), dgamma / dbeta bit
+    for bit (same stats pass), the conv bias gradient to fp32 summation order."""
+    g = torch.Generator(device="cuda").manual_seed(3)
+    x = torch.randn(b, c, r, r, r, device="cuda", generator=g) * 2.0 + 1.0
+    dz = torch.randn(b, c, r, r, r, device="cuda", generator=g)
+    gamma = torch.rand(c, device="cuda", generator=g) + 0.5
+    beta = torch.rand(c, device="cuda", generator=g) - 0.5
+    mean = x.mean(dim=(0, 2, 3, 4))
+    invstd = torch.rsqrt(x.var(dim=(0, 2, 3, 4), unbiased=False) + 1e-5)
+    dx, dg, dbt, db = ops.bn_act_backward(dz, x, gamma, beta, mean, invstd, slope,
+                                          want_dbias_in=True)
+    ref = ops.conv3d_split(dx)
+    got, dg2, dbt2, db2 = ops.bn_act_backward_split(dz, x, gamma, beta, mean, invstd, slope,
+                                                    want_dbias_in=True)
+    assert torch.equal(got, ref)
+    assert torch.equal(dg2, dg) and torch.equal(dbt2, dbt)
+    # sum_{b,s} dx is analytically ~0 (sum xhat = 0): compare at the rounding
+    # scale of the summed terms, not relative to the near-zero result
+    scale = float(dx.abs().sum(dim=(0, 2, 3, 4)).max())
+    torch.testing.assert_close(db2, db, rtol=0, atol=1e-5 * scale)
+    _, _, _, none = ops.bn_act_backward_split(dz, x, gamma, beta, mean, invstd, slope)
+    assert none is None
