@@ -416,6 +416,15 @@ int pcfm_bn_act_bwd(const float* dz, const float* x, const float* gamma, const f
                     float* dx, float* dgamma, float* dbeta, float* dbias_in, void* ws,
                     size_t ws_bytes, void* stream);
 
+/* pcfm_bn_act_fwd whose output only feeds a voxel convolution: y is written
+ * directly as the channels-last bf16 hi/lo split of pcfm_conv3d_split (ys:
+ * pcfm_conv3d_split_bytes(b, c, r) bytes, r^3 = s; c, s multiples of 64), not
+ * as fp32.  Workspace: pcfm_bn_workspace_bytes(b, c, s). */
+int pcfm_bn_act_fwd_split(const float* x, const float* gamma, const float* beta, int b, int c,
+                          int s, float eps, float slope, float momentum, float* running_mean,
+                          float* running_var, void* ys, float* mean, float* invstd, void* ws,
+                          size_t ws_bytes, void* stream);
+
 /* pcfm_bn_act_bwd for a voxel convolution's output x [b][c][s] (c, s multiples
  * of 64) whose dx only feeds that convolution's backward: dx is written
  * directly as the channels-last bf16 hi/lo split of pcfm_conv3d_split

@@ -274,6 +274,53 @@ __global__ void __launch_bounds__(256)
 // rowpart[(b * C + c) * (S / 64) + vb] = sum of dx over the tile's 64 voxels
 // (fixed order: 16 sequential per thread, then a 4-lane xor tree).
 typedef __bf16 bn_bf16x2 __attribute__((ext_vector_type(2)));
+
+// A 64 (channel) x 64 (voxel) fp32 LDS tile -> channels-last bf16 hi / lo
+// rows [b][v][c] (conv3_split_cl_kernel's layout and rounding), 256 threads:
+// thread t writes 16 channels of voxel t / 4.
+__device__ __forceinline__ void tile_store_split(const float (&tile)[64][65], int b, int C, int S,
+                                                 int v0, int c0, int t, uint16_t* __restrict__ h,
+                                                 uint16_t* __restrict__ l) {
+  const int v = t >> 2, cg = (t & 3) * 16;
+  const size_t o = ((size_t)b * S + v0 + v) * C + c0 + cg;
+  uint32_t* h32 = reinterpret_cast<uint32_t*>(h + o);
+  uint32_t* l32 = reinterpret_cast<uint32_t*>(l + o);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const float f0 = tile[cg + 2 * q][v], f1 = tile[cg + 2 * q + 1][v];
+    bn_bf16x2 hi, lo;
+    hi.x = (__bf16)f0;
+    hi.y = (__bf16)f1;
+    lo.x = (__bf16)(f0 - (float)hi.x);
+    lo.y = (__bf16)(f1 - (float)hi.y);
+    h32[q] = __builtin_bit_cast(uint32_t, hi);
+    l32[q] = __builtin_bit_cast(uint32_t, lo);
+  }
+}
+
+// act(bn(x)) written directly as the next convolution's split input (the
+// fp32 activation is never materialised); grid = (S / 64, C / 64, B).
+__global__ void __launch_bounds__(256)
+    bn_act_apply_split_kernel(const float* __restrict__ x, const float* __restrict__ mean,
+                              const float* __restrict__ invstd, const float* __restrict__ gamma,
+                              const float* __restrict__ beta, int C, int S, float slope,
+                              uint16_t* __restrict__ yh, uint16_t* __restrict__ yl) {
+  __shared__ float tile[64][65];
+  const int v0 = blockIdx.x * 64, c0 = blockIdx.y * 64, b = blockIdx.z;
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+  const size_t rbase = ((size_t)b * C + c0) * S + v0;
+  float xv[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) xv[i] = x[rbase + (size_t)(4 * i + w) * S + lane];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int c = c0 + 4 * i + w;
+    tile[4 * i + w][lane] = act(__builtin_fmaf((xv[i] - mean[c]) * invstd[c], gamma[c], beta[c]),
+                                slope);
+  }
+  __syncthreads();
+  tile_store_split(tile, b, C, S, v0, c0, t, yh, yl);
+}
 __global__ void __launch_bounds__(256)
     bn_bwd_apply_split_kernel(const float* __restrict__ dz, const float* __restrict__ x,
                               const float* __restrict__ mean, const float* __restrict__ invstd,
@@ -302,23 +349,7 @@ __global__ void __launch_bounds__(256)
     tile[4 * i + w][lane] = k * ((g - mg) - xh * mgx);
   }
   __syncthreads();
-  {
-    const int v = t >> 2, cg = (t & 3) * 16;
-    const size_t o = ((size_t)b * S + v0 + v) * C + c0 + cg;
-    uint32_t* h32 = reinterpret_cast<uint32_t*>(dxh + o);
-    uint32_t* l32 = reinterpret_cast<uint32_t*>(dxl + o);
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const float f0 = tile[cg + 2 * q][v], f1 = tile[cg + 2 * q + 1][v];
-      bn_bf16x2 hi, lo;
-      hi.x = (__bf16)f0;
-      hi.y = (__bf16)f1;
-      lo.x = (__bf16)(f0 - (float)hi.x);
-      lo.y = (__bf16)(f1 - (float)hi.y);
-      h32[q] = __builtin_bit_cast(uint32_t, hi);
-      l32[q] = __builtin_bit_cast(uint32_t, lo);
-    }
-  }
+  tile_store_split(tile, b, C, S, v0, c0, t, dxh, dxl);
   if (rowpart != nullptr) {
     const int c = t >> 2, vq = (t & 3) * 16;
     float sum = 0.0f;
@@ -636,6 +667,29 @@ extern "C" int pcfm_bn_act_bwd(const float* dz, const float* x, const float* gam
     hipLaunchKernelGGL(bn_bias_finalize_kernel, dim3(ceil_div(c, 4)), dim3(256), 0, st,
                        (const float*)rowpart, b, c, nch, dbias_in);
   return check_launch("bn_act_bwd");
+}
+
+extern "C" int pcfm_bn_act_fwd_split(const float* x, const float* gamma, const float* beta, int b,
+                                     int c, int s, float eps, float slope, float momentum,
+                                     float* running_mean, float* running_var, void* ys,
+                                     float* mean, float* invstd, void* ws, size_t ws_bytes,
+                                     void* stream) {
+  PCFM_CHECK_ARG(bn_ok(b, c, s) && c % 64 == 0 && s % 64 == 0 && (long long)b < 65536,
+                 "bn_act_fwd_split: bad shape b=%d c=%d s=%d (c, s multiples of 64)", b, c, s);
+  PCFM_CHECK_ARG(ws_bytes >= pcfm_bn_workspace_bytes(b, c, s), "bn_act_fwd_split: workspace too small");
+  PCFM_CHECK_ARG((running_mean == nullptr) == (running_var == nullptr),
+                 "bn_act_fwd_split: running_mean and running_var must both be given or both NULL");
+  hipStream_t st = (hipStream_t)stream;
+  float* part = (float*)ws;
+  hipLaunchKernelGGL(bn_stats_kernel, dim3(c, bn_parts(b)), dim3(256), 0, st, x, b, c, s, part);
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(ceil_div(c, 256)), dim3(256), 0, st,
+                     (const float*)part, x, b, c, s, bn_parts(b), eps, momentum, running_mean,
+                     running_var, mean, invstd);
+  uint16_t* yh = (uint16_t*)ys;
+  hipLaunchKernelGGL(bn_act_apply_split_kernel, dim3(s / 64, c / 64, b), dim3(256), 0, st, x,
+                     (const float*)mean, (const float*)invstd, gamma, beta, c, s, slope, yh,
+                     yh + (size_t)b * s * c);
+  return check_launch("bn_act_fwd_split");
 }
 
 extern "C" size_t pcfm_bn_act_bwd_split_workspace_bytes(int b, int c, int s) {

@@ -111,6 +111,84 @@ class _Conv3dBnAct(torch.autograd.Function):
         return dx, dw, db, dgamma, dbeta, None, None, None, None, None
 
 
+class _Conv3dBnActPair(torch.autograd.Function):
+    """PVConv's two voxel layers act2(BN2(Conv2(act1(BN1(Conv1(x)))))) in one
+    autograd node, so the inner activation lives only as Conv2's channels-last
+    split input (bn_act_forward_split) and its gradient only as Conv1's split
+    grad (bn_act_backward_split): no fp32 pass over either."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, g1, bt1, rm1, rv1, w2, b2, g2, bt2, rm2, rv2, eps1, mom1,
+                slope1, eps2, mom2, slope2):
+        from pcfm import ops
+        bsz, cin, r = x.shape[0], x.shape[1], x.shape[2]
+        cmid, cout = w1.shape[0], w2.shape[0]
+        xs = ops.conv3d_split(x)
+        y1 = ops.conv3d_igemm_split(xs, ops.conv3d_prep_weight(w1, False), b1, bsz, cin, cmid,
+                                    r, "conv3d_fwd")
+        z1s, m1, is1 = ops.bn_act_forward_split(y1, g1, bt1, eps1, slope1, mom1, rm1, rv1)
+        y2 = ops.conv3d_igemm_split(z1s, ops.conv3d_prep_weight(w2, False), b2, bsz, cmid, cout,
+                                    r, "conv3d_fwd")
+        z2, m2, is2 = ops.bn_act_forward(y2, g2, bt2, eps2, slope2, mom2, rm2, rv2)
+        ctx.save_for_backward(xs, w1, y1, g1, bt1, m1, is1, z1s, w2, y2, g2, bt2, m2, is2)
+        ctx.slopes = (slope1, slope2)
+        ctx.has_bias = (b1 is not None, b2 is not None)
+        ctx.dims = (bsz, cin, cmid, cout, r)
+        return z2
+
+    @staticmethod
+    def backward(ctx, dz2):
+        from pcfm import ops
+        xs, w1, y1, g1, bt1, m1, is1, z1s, w2, y2, g2, bt2, m2, is2 = ctx.saved_tensors
+        bsz, cin, cmid, cout, r = ctx.dims
+        gys2, dg2, dbt2, db2 = ops.bn_act_backward_split(dz2, y2, g2, bt2, m2, is2,
+                                                         ctx.slopes[1],
+                                                         want_dbias_in=ctx.has_bias[1])
+        dz1 = ops.conv3d_igemm_split(gys2, ops.conv3d_prep_weight(w2, True), None, bsz, cout,
+                                     cmid, r, "conv3d_bwd_data")
+        dw2 = ops.conv3d_wgrad_split(z1s, gys2, bsz, cmid, cout, r)
+        del gys2
+        gys1, dg1, dbt1, db1 = ops.bn_act_backward_split(dz1, y1, g1, bt1, m1, is1,
+                                                         ctx.slopes[0],
+                                                         want_dbias_in=ctx.has_bias[0])
+        del dz1
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = ops.conv3d_igemm_split(gys1, ops.conv3d_prep_weight(w1, True), None, bsz, cmid,
+                                        cin, r, "conv3d_bwd_data")
+        dw1 = ops.conv3d_wgrad_split(xs, gys1, bsz, cin, cmid, r)
+        return (dx, dw1, db1, dg1, dbt1, None, None, dw2, db2, dg2, dbt2, None, None,
+                None, None, None, None, None, None)
+
+
+def conv_bn_act_pair(conv1, bn1, slope1: float, conv2, bn2, slope2: float,
+                     x: torch.Tensor) -> torch.Tensor:
+    """act2(bn2(conv2(act1(bn1(conv1(x)))))) for two VoxelConv3d layers: one
+    autograd node on the GPU path when both layers qualify, else two
+    conv_bn_act calls."""
+    from modules.shared_mlp import PointwiseConv1d
+    ok = (not isinstance(conv1, PointwiseConv1d) and not isinstance(conv2, PointwiseConv1d)
+          and _fusable_pre(bn1) and _fusable_pre(bn2) and hasattr(conv1, "x3_ok")
+          and hasattr(conv2, "x3_ok") and conv1.x3_ok(x) and conv1.bias is not None
+          and conv2.bias is not None and conv1.out_channels % 64 == 0
+          and x[0, 0].numel() % 64 == 0 and x.shape[0] * conv2.out_channels < 65536)
+    if ok:
+        from pcfm import ops
+        # shape / dtype / device stand-in for conv1's output (no allocation)
+        probe = x.new_empty(()).expand((x.shape[0], conv1.out_channels) + tuple(x.shape[2:]))
+        ok = conv2.x3_ok(probe) and ops.conv3d_split_supported(probe)
+    if not ok:
+        x = conv_bn_act(conv1, bn1, x, slope1)
+        return conv_bn_act(conv2, bn2, x, slope2)
+    bn1.num_batches_tracked.add_(1)
+    bn2.num_batches_tracked.add_(1)
+    return _Conv3dBnActPair.apply(
+        x.contiguous(), conv1.weight, conv1.bias, bn1.weight, bn1.bias, bn1.running_mean,
+        bn1.running_var, conv2.weight, conv2.bias, bn2.weight, bn2.bias, bn2.running_mean,
+        bn2.running_var, float(bn1.eps), float(bn1.momentum), float(slope1), float(bn2.eps),
+        float(bn2.momentum), float(slope2))
+
+
 def conv_bn_act(conv, bn, x: torch.Tensor, slope: float) -> torch.Tensor:
     """act(bn(conv(x))) for a PointwiseConv1d / VoxelConv3d `conv`: one fused
     autograd node on the GPU path, the modules' own forwards otherwise."""

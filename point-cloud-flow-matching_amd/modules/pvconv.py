@@ -13,7 +13,7 @@ import torch.nn as nn
 import torch.nn.functional as TF
 
 import modules.functional as F
-from modules.norm_act import conv_bn_act
+from modules.norm_act import conv_bn_act_pair
 from modules.se import SE3d
 from modules.shared_mlp import SharedMLP
 from modules.voxel_conv import VoxelConv3d
@@ -110,8 +110,8 @@ class PVConv(nn.Module):
         else:
             grid, grid_coords = self.voxelization(features, coords)
         layers = self.voxel_layers  # Conv3d, BN3d, LeakyReLU, Conv3d, BN3d, LeakyReLU[, SE3d]
-        grid = conv_bn_act(layers[0], layers[1], grid, layers[2].negative_slope)
-        grid = conv_bn_act(layers[3], layers[4], grid, layers[5].negative_slope)
+        grid = conv_bn_act_pair(layers[0], layers[1], layers[2].negative_slope,
+                                layers[3], layers[4], layers[5].negative_slope, grid)
         pf = self.point_features(features)
         if (len(layers) > 6 and _se_devox_ok(layers[6], grid, pf)
                 and (self.training or not torch.is_grad_enabled())):

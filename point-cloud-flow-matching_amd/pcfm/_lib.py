@@ -93,6 +93,8 @@ SIGNATURES = {
                              _P]),
     "pcfm_bn_act_bwd": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _F, _P, _P, _P, _P, _P, _Z,
                              _P]),
+    "pcfm_bn_act_fwd_split": (_I, [_P, _P, _P, _I, _I, _I, _F, _F, _F, _P, _P, _P, _P, _P, _P,
+                                   _Z, _P]),
     "pcfm_bn_act_bwd_split_workspace_bytes": (_Z, [_I, _I, _I]),
     "pcfm_bn_act_bwd_split": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _F, _P, _P, _P, _P, _P,
                                    _Z, _P]),

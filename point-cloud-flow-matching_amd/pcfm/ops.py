@@ -855,6 +855,27 @@ def bn_act_forward(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, ep
     return y, stats[0], stats[1]
 
 
+def bn_act_forward_split(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, eps: float,
+                         slope: float, momentum: float, running_mean, running_var):
+    """bn_act_forward for a voxel conv output x (B, C, R, R, R) whose activation only
+    feeds the next voxel conv: -> (split(act(bn(x))) as conv3d_split lays it out,
+    mean, invstd); running stats updated in place."""
+    _check(x, "input", "f")
+    b, c, r = x.shape[0], x.shape[1], x.shape[2]
+    s = x.numel() // max(1, b * c)
+    n = _lib.query("pcfm_conv3d_split_bytes", b, c, r)
+    if n == 0 or c % 64 != 0:
+        raise RuntimeError(f"bn_act_forward_split: unsupported shape {tuple(x.shape)}")
+    ys = torch.empty(n, dtype=torch.uint8, device=x.device)
+    stats = torch.empty((2, c), dtype=torch.float32, device=x.device)
+    ws = _workspace(_lib.query("pcfm_bn_workspace_bytes", b, c, s), x)
+    with _timed("bn_act_fwd", 4 * 3 * x.numel(), x):
+        _lib.call("pcfm_bn_act_fwd_split", _ptr(x), _ptr(weight), _ptr(bias), b, c, s,
+                  float(eps), float(slope), float(momentum), _p(running_mean), _p(running_var),
+                  _ptr(ys), _ptr(stats[0]), _ptr(stats[1]), _ptr(ws), ws.numel(), _stream(x))
+    return ys, stats[0], stats[1]
+
+
 def bn_act_backward(dz: torch.Tensor, x: torch.Tensor, weight, bias, mean, invstd, slope: float,
                     want_dbias_in: bool = False):
     """-> (dx, dgamma, dbeta, dbias_in) with dbias_in = sum of dx over (b, s) per

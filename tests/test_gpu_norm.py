@@ -188,3 +188,32 @@ def test_bn_act_backward_split_matches_unfused(ops, b, c, r, slope):
     torch.testing.assert_close(db2, db, rtol=0, atol=1e-5 * scale)
     _, _, _, none = ops.bn_act_backward_split(dz, x, gamma, beta, mean, invstd, slope)
     assert none is None
+
+
+@pytest.mark.parametrize("b,c,r", [(2, 128, 16), (2, 256, 8), (1, 128, 32)])
+def test_conv_bn_act_pair_matches_two_nodes(ops, b, c, r):
+    """PVConv's fused pair node (inner activation only as Conv2's split input)
+    equals two single-layer nodes bit for bit: the split of act(bn(y1)) is the
+    same bf16 pair either way, so every output, gradient and running stat must
+    agree exactly."""
+    from modules.norm_act import _Conv3dBnActPair, conv_bn_act, conv_bn_act_pair
+    from modules.voxel_conv import VoxelConv3d
+    torch.manual_seed(5)
+    mods = [VoxelConv3d(c, c, 3, padding=1).cuda(), torch.nn.BatchNorm3d(c, eps=1e-4).cuda(),
+            VoxelConv3d(c, c, 3, padding=1).cuda(), torch.nn.BatchNorm3d(c, eps=1e-4).cuda()]
+    ref = copy.deepcopy(mods)
+    x = torch.randn(b, c, r, r, r, device="cuda")
+    xa, xb = x.clone().requires_grad_(True), x.clone().requires_grad_(True)
+    za = conv_bn_act(ref[2], ref[3], conv_bn_act(ref[0], ref[1], xa, 0.1), 0.1)
+    zb = conv_bn_act_pair(mods[0], mods[1], 0.1, mods[2], mods[3], 0.1, xb)
+    assert isinstance(zb.grad_fn, _Conv3dBnActPair._backward_cls)
+    assert torch.equal(za, zb)
+    gz = torch.randn_like(za)
+    za.backward(gz)
+    zb.backward(gz)
+    assert torch.equal(xa.grad, xb.grad)
+    for m_ref, m in zip(ref, mods):
+        for (name, p_ref), p in zip(m_ref.named_parameters(), m.parameters()):
+            assert torch.equal(p_ref.grad, p.grad), name
+        for (name, b_ref), bb in zip(m_ref.named_buffers(), m.buffers()):
+            assert torch.equal(b_ref, bb), name
