@@ -278,7 +278,8 @@ def main():
                      "the reference's default cuDNN TF32 2^-11) + bf16 autocast MLP head "
                      "(reference AMP config)",
             "data": "synthetic (randn xyz, U[0,1] rgb, U[0,1] cond; no dataset on the box)",
-            "config": {"workload": "hybrid flow-matching train step, B=8/GPU, N=20000 xyz+rgb, "
+            "config": {"workload": f"{cfg.pf_backbone} flow-matching train step, "
+                                   f"B={cfg.batch_size}/GPU, N={cfg.num_points} xyz+rgb, "
                                    "latent 128, 1 joint, stages (128,256,256)@(32,16,8)",
                        "global_batch": world * cfg.batch_size, "points_per_cloud": cfg.num_points,
                        "backbone": cfg.pf_backbone, "parallelism": f"dp{world}"},
