@@ -1,6 +1,6 @@
 """Attribute the bench train step's device time to aten ops / autograd nodes
 (torch.profiler, shapes recorded), to find which model-level op each kernel
-belongs to.  Dev tool: `python tools/aten_profile.py [steps] > out.txt`."""
+belongs to.  Dev tool: `python tools/aten_profile.py [steps] [key filter] > out.txt`."""
 import os
 import sys
 
@@ -34,8 +34,9 @@ def main():
     rows = sorted(ka, key=lambda e: -e.self_device_time_total)
     tot = sum(e.self_device_time_total for e in ka)
     print(f"total self device time {tot / 1e3 / steps:.2f} ms/step")
-    for e in rows[:120]:
-        if e.self_device_time_total <= 0:
+    pat = sys.argv[2].lower() if len(sys.argv) > 2 else None  # optional key filter
+    for e in (rows if pat else rows[:120]):
+        if e.self_device_time_total <= 0 or (pat and pat not in e.key.lower()):
             continue
         print(f"{e.self_device_time_total / 1e3 / steps:8.3f} ms {e.count // steps:4d}x  "
               f"{e.key[:60]:60s} {str(e.input_shapes)[:150]}")
