@@ -1141,23 +1141,36 @@ __global__ void __launch_bounds__(256)
   const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
   const size_t cc = cc0 + cl;
   const size_t ps = 27 * pairs;  // one split's partial
-  for (int tap = grp; tap < 27; tap += 4) {
-    float sum = 0.0f;
-    if (cc < pairs) {
-      const float* p = part + (size_t)tap * pairs + cc;
-      int q = 0;
-      for (; q + 4 <= S; q += 4) {
-        const float a0 = p[(size_t)q * ps], a1 = p[(size_t)(q + 1) * ps];
-        const float a2 = p[(size_t)(q + 2) * ps], a3 = p[(size_t)(q + 3) * ps];
-        sum = sum + a0;
-        sum = sum + a1;
-        sum = sum + a2;
-        sum = sum + a3;
-      }
-      for (; q < S; ++q) sum = sum + p[(size_t)q * ps];
+  // this thread's taps grp, grp + 4, ... (7 at most) accumulate side by side:
+  // per split q all their partials are loaded before any is added, two splits
+  // per round (each tap's sum keeps the split order)
+  constexpr int kT = 7;
+  float sum[kT];
+#pragma unroll
+  for (int k = 0; k < kT; ++k) sum[k] = 0.0f;
+  if (cc < pairs) {
+    const float* p = part + cc;
+    auto tap_of = [&](int k) { return min(grp + 4 * k, 26); };
+    int q = 0;
+    for (; q + 2 <= S; q += 2) {
+      float a[2][kT];
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int k = 0; k < kT; ++k)
+          a[u][k] = p[(size_t)(q + u) * ps + (size_t)tap_of(k) * pairs];
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int k = 0; k < kT; ++k) sum[k] = sum[k] + a[u][k];
     }
-    tile[cl * 27 + tap] = sum;
+    for (; q < S; ++q)
+#pragma unroll
+      for (int k = 0; k < kT; ++k) sum[k] = sum[k] + p[(size_t)q * ps + (size_t)tap_of(k) * pairs];
   }
+#pragma unroll
+  for (int k = 0; k < kT; ++k)
+    if (grp + 4 * k < 27) tile[cl * 27 + grp + 4 * k] = sum[k];
   __syncthreads();
   const size_t n = (min(pairs, cc0 + 64) - cc0) * 27;
   for (size_t e = threadIdx.x; e < n; e += 256) dw[cc0 * 27 + e] = tile[e];
