@@ -185,8 +185,18 @@ __global__ void __launch_bounds__(256)
   const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
   const size_t i = (size_t)blockIdx.x * 64 + cl;
   float sum = 0.0f;
-  if (i < total)
-    for (int q = grp; q < S; q += 4) sum = sum + part[(size_t)q * total + i];
+  if (i < total) {
+    int q = grp;
+    // 4 of the group's partials loaded before they are added (same order)
+    for (; q + 12 < S; q += 16) {
+      float v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = part[(size_t)(q + 4 * u) * total + i];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) sum = sum + v[u];
+    }
+    for (; q < S; q += 4) sum = sum + part[(size_t)q * total + i];
+  }
   red[grp][cl] = sum;
   __syncthreads();
   if (grp == 0 && i < total)
