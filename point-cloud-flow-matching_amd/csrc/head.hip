@@ -409,8 +409,18 @@ __global__ void __launch_bounds__(256)
   const int b = blockIdx.y, cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
   float s = 0.0f;
-  if (c < C)
-    for (int p = grp; p < P; p += 4) s += part[((size_t)b * P + p) * C + c];
+  if (c < C) {
+    int p = grp;
+    // 4 of the group's partials loaded before they are added (same order)
+    for (; p + 12 < P; p += 16) {
+      float v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = part[((size_t)b * P + p + 4 * u) * C + c];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) s += v[u];
+    }
+    for (; p < P; p += 4) s += part[((size_t)b * P + p) * C + c];
+  }
   red[grp][cl] = s;
   __syncthreads();
   if (grp == 0 && c < C) out[(size_t)b * C + c] = ((red[0][cl] + red[1][cl]) + red[2][cl]) + red[3][cl];
