@@ -301,7 +301,16 @@ __global__ void __launch_bounds__(256)
   float s = 0.0f;
   if (c < W) {
     const float* p = part + ((size_t)b * chunks * kSums + k) * W + c;
-    for (int q = grp; q < chunks; q += 4) s += p[(size_t)q * kSums * W];
+    int q = grp;
+    // 4 of the group's partials loaded before they are added (same order)
+    for (; q + 12 < chunks; q += 16) {
+      float v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = p[(size_t)(q + 4 * u) * kSums * W];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) s += v[u];
+    }
+    for (; q < chunks; q += 4) s += p[(size_t)q * kSums * W];
   }
   red[grp][cl] = s;
   __syncthreads();
