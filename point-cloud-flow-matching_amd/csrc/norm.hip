@@ -114,18 +114,67 @@ __global__ void __launch_bounds__(256)
   }
 }
 
+// bn_finalize / bn_bwd_finalize folded into the apply passes (one launch
+// less each): every apply block re-derives its channel's statistics from the
+// P partials with exactly the finalize arithmetic, and one designated block
+// per channel writes mean / invstd (+ running stats) or dgamma / dbeta.
+struct BnFwdFin {
+  const float* part;
+  int B, S, P;
+  float eps, momentum;
+  float* rmean;
+  float* rvar;
+  __device__ __forceinline__ void get(const float* x, int c, float& m, float& is, float& var,
+                                      double& n) const {
+    float s = 0.0f, q = 0.0f;
+    for (int p = 0; p < P; ++p) {
+      s += part[((size_t)c * P + p) * 2];
+      q += part[((size_t)c * P + p) * 2 + 1];
+    }
+    n = (double)B * S;
+    const float K = x[(size_t)c * S];
+    const float md = (float)(s / n);
+    var = fmaxf((float)(q / n) - md * md, 0.0f);
+    m = K + md;
+    is = rsqrtf(var + eps);
+  }
+  __device__ __forceinline__ void publish(int c, float m, float is, float var, double n,
+                                          float* mean, float* invstd) const {
+    mean[c] = m;
+    invstd[c] = is;
+    if (rmean != nullptr) {
+      rmean[c] = (1.0f - momentum) * rmean[c] + momentum * m;
+      rvar[c] = (1.0f - momentum) * rvar[c] + momentum * (float)(var * n / (n - 1.0));
+    }
+  }
+};
+__device__ __forceinline__ void bn_bwd_fin(const float* part, int P, int c, float& sg,
+                                           float& sgx) {
+  sg = 0.0f;
+  sgx = 0.0f;
+  for (int p = 0; p < P; ++p) {
+    sg += part[((size_t)c * P + p) * 2];
+    sgx += part[((size_t)c * P + p) * 2 + 1];
+  }
+}
+
 // y = act((x - mean) * invstd * gamma + beta), float4 per thread;
 // grid = (ceil(S4 / 256), B * C).
 __global__ void __launch_bounds__(256)
-    bn_act_apply_kernel(const float* __restrict__ x, const float* __restrict__ mean,
-                        const float* __restrict__ invstd, const float* __restrict__ gamma,
+    bn_act_apply_kernel(const float* __restrict__ x, BnFwdFin fin, float* __restrict__ mean,
+                        float* __restrict__ invstd, const float* __restrict__ gamma,
                         const float* __restrict__ beta, int C, int S4, float slope,
                         float* __restrict__ y) {
+  const int c = (int)(blockIdx.y % C);
+  float m, is, var;
+  double n;
+  fin.get(x, c, m, is, var, n);
+  if (blockIdx.x == 0 && blockIdx.y < (unsigned)C && threadIdx.x == 0)
+    fin.publish(c, m, is, var, n, mean, invstd);
   const int s4 = blockIdx.x * 256 + threadIdx.x;
   if (s4 >= S4) return;
-  const int c = (int)(blockIdx.y % C);
   const size_t i = (size_t)blockIdx.y * S4 + s4;
-  const float m = mean[c], is = invstd[c], g = gamma[c], bt = beta[c];
+  const float g = gamma[c], bt = beta[c];
   const float4 v = reinterpret_cast<const float4*>(x)[i];
   float4 o;
   o.x = act(__builtin_fmaf((v.x - m) * is, g, bt), slope);
@@ -202,7 +251,8 @@ __global__ void __launch_bounds__(256)
     bn_bwd_apply_kernel(const float* __restrict__ dz, const float* __restrict__ x,
                         const float* __restrict__ mean, const float* __restrict__ invstd,
                         const float* __restrict__ gamma, const float* __restrict__ beta,
-                        const float* __restrict__ dgamma, const float* __restrict__ dbeta, int C,
+                        const float* __restrict__ part, int P, float* __restrict__ dgamma,
+                        float* __restrict__ dbeta, int C,
                         int S4, float inv_n, float slope, float* __restrict__ dx,
                         float* __restrict__ rowpart) {
   __shared__ float sh[8];
@@ -210,8 +260,14 @@ __global__ void __launch_bounds__(256)
   const bool ok = s4 < S4;
   const int c = (int)(blockIdx.y % C);
   const size_t i = (size_t)blockIdx.y * S4 + (ok ? s4 : 0);
+  float sg, sgx;
+  bn_bwd_fin(part, P, c, sg, sgx);
+  if (blockIdx.x == 0 && blockIdx.y < (unsigned)C && threadIdx.x == 0) {
+    dbeta[c] = sg;
+    dgamma[c] = sgx;
+  }
   const float m = mean[c], is = invstd[c], gm = gamma[c], bt = beta[c];
-  const float mg = dbeta[c] * inv_n, mgx = dgamma[c] * inv_n, k = gm * is;
+  const float mg = sg * inv_n, mgx = sgx * inv_n, k = gm * is;
   float o[4] = {0.0f, 0.0f, 0.0f, 0.0f};
   if (ok) {
     const float4 v = reinterpret_cast<const float4*>(x)[i];
@@ -301,13 +357,24 @@ __device__ __forceinline__ void tile_store_split(const float (&tile)[64][65], in
 // act(bn(x)) written directly as the next convolution's split input (the
 // fp32 activation is never materialised); grid = (S / 64, C / 64, B).
 __global__ void __launch_bounds__(256)
-    bn_act_apply_split_kernel(const float* __restrict__ x, const float* __restrict__ mean,
-                              const float* __restrict__ invstd, const float* __restrict__ gamma,
+    bn_act_apply_split_kernel(const float* __restrict__ x, BnFwdFin fin,
+                              float* __restrict__ mean, float* __restrict__ invstd,
+                              const float* __restrict__ gamma,
                               const float* __restrict__ beta, int C, int S, float slope,
                               uint16_t* __restrict__ yh, uint16_t* __restrict__ yl) {
   __shared__ float tile[64][65];
+  __shared__ float st_m[64], st_is[64];
   const int v0 = blockIdx.x * 64, c0 = blockIdx.y * 64, b = blockIdx.z;
   const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+  if (t < 64) {
+    float m, is, var;
+    double n;
+    fin.get(x, c0 + t, m, is, var, n);
+    st_m[t] = m;
+    st_is[t] = is;
+    if (blockIdx.x == 0 && b == 0) fin.publish(c0 + t, m, is, var, n, mean, invstd);
+  }
+  __syncthreads();
   const size_t rbase = ((size_t)b * C + c0) * S + v0;
   float xv[16];
 #pragma unroll
@@ -315,8 +382,8 @@ __global__ void __launch_bounds__(256)
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     const int c = c0 + 4 * i + w;
-    tile[4 * i + w][lane] = act(__builtin_fmaf((xv[i] - mean[c]) * invstd[c], gamma[c], beta[c]),
-                                slope);
+    tile[4 * i + w][lane] =
+        act(__builtin_fmaf((xv[i] - st_m[c - c0]) * st_is[c - c0], gamma[c], beta[c]), slope);
   }
   __syncthreads();
   tile_store_split(tile, b, C, S, v0, c0, t, yh, yl);
@@ -325,12 +392,25 @@ __global__ void __launch_bounds__(256)
     bn_bwd_apply_split_kernel(const float* __restrict__ dz, const float* __restrict__ x,
                               const float* __restrict__ mean, const float* __restrict__ invstd,
                               const float* __restrict__ gamma, const float* __restrict__ beta,
-                              const float* __restrict__ dgamma, const float* __restrict__ dbeta,
+                              const float* __restrict__ part, int P, float* __restrict__ dgamma,
+                              float* __restrict__ dbeta,
                               int C, int S, float inv_n, float slope, uint16_t* __restrict__ dxh,
                               uint16_t* __restrict__ dxl, float* __restrict__ rowpart) {
   __shared__ float tile[64][65];
+  __shared__ float st_g[64], st_gx[64];
   const int v0 = blockIdx.x * 64, c0 = blockIdx.y * 64, b = blockIdx.z;
   const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+  if (t < 64) {
+    float sg, sgx;
+    bn_bwd_fin(part, P, c0 + t, sg, sgx);
+    st_g[t] = sg;
+    st_gx[t] = sgx;
+    if (blockIdx.x == 0 && b == 0) {
+      dbeta[c0 + t] = sg;
+      dgamma[c0 + t] = sgx;
+    }
+  }
+  __syncthreads();
   const size_t rbase = ((size_t)b * C + c0) * S + v0;
   float xv[16], dv[16];
 #pragma unroll
@@ -343,7 +423,7 @@ __global__ void __launch_bounds__(256)
   for (int i = 0; i < 16; ++i) {
     const int c = c0 + 4 * i + w;
     const float m = mean[c], is = invstd[c], gm = gamma[c], bt = beta[c];
-    const float mg = dbeta[c] * inv_n, mgx = dgamma[c] * inv_n, k = gm * is;
+    const float mg = st_g[c - c0] * inv_n, mgx = st_gx[c - c0] * inv_n, k = gm * is;
     const float xh = (xv[i] - m) * is;
     const float g = __builtin_fmaf(xh, gm, bt) > 0.0f ? dv[i] : dv[i] * slope;
     tile[4 * i + w][lane] = k * ((g - mg) - xh * mgx);
@@ -637,11 +717,9 @@ extern "C" int pcfm_bn_act_fwd(const float* x, const float* gamma, const float* 
   hipStream_t st = (hipStream_t)stream;
   float* part = (float*)ws;
   hipLaunchKernelGGL(bn_stats_kernel, dim3(c, bn_parts(b)), dim3(256), 0, st, x, b, c, s, part);
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3(ceil_div(c, 256)), dim3(256), 0, st,
-                     (const float*)part, x, b, c, s, bn_parts(b), eps, momentum, running_mean,
-                     running_var, mean, invstd);
+  const BnFwdFin fin{part, b, s, bn_parts(b), eps, momentum, running_mean, running_var};
   hipLaunchKernelGGL(bn_act_apply_kernel, dim3(ceil_div(s / 4, 256), b * c), dim3(256), 0, st, x,
-                     (const float*)mean, (const float*)invstd, gamma, beta, c, s / 4, slope, y);
+                     fin, mean, invstd, gamma, beta, c, s / 4, slope, y);
   return check_launch("bn_act_fwd");
 }
 
@@ -656,12 +734,10 @@ extern "C" int pcfm_bn_act_bwd(const float* dz, const float* x, const float* gam
   float* part = (float*)ws;
   hipLaunchKernelGGL(bn_bwd_stats_kernel, dim3(c, bn_parts(b)), dim3(256), 0, st, dz, x, mean,
                      invstd, gamma, beta, b, c, s, slope, part);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(ceil_div(c, 256)), dim3(256), 0, st,
-                     (const float*)part, c, bn_parts(b), dgamma, dbeta);
   const int nch = ceil_div(s / 4, 256);
   float* rowpart = dbias_in != nullptr ? part + (size_t)c * bn_parts(b) * 2 : nullptr;
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(nch, b * c), dim3(256), 0, st, dz, x, mean, invstd,
-                     gamma, beta, (const float*)dgamma, (const float*)dbeta, c, s / 4,
+                     gamma, beta, (const float*)part, bn_parts(b), dgamma, dbeta, c, s / 4,
                      (float)(1.0 / ((double)b * s)), slope, dx, rowpart);
   if (dbias_in != nullptr)
     hipLaunchKernelGGL(bn_bias_finalize_kernel, dim3(ceil_div(c, 4)), dim3(256), 0, st,
@@ -682,12 +758,10 @@ extern "C" int pcfm_bn_act_fwd_split(const float* x, const float* gamma, const f
   hipStream_t st = (hipStream_t)stream;
   float* part = (float*)ws;
   hipLaunchKernelGGL(bn_stats_kernel, dim3(c, bn_parts(b)), dim3(256), 0, st, x, b, c, s, part);
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3(ceil_div(c, 256)), dim3(256), 0, st,
-                     (const float*)part, x, b, c, s, bn_parts(b), eps, momentum, running_mean,
-                     running_var, mean, invstd);
+  const BnFwdFin fin{part, b, s, bn_parts(b), eps, momentum, running_mean, running_var};
   uint16_t* yh = (uint16_t*)ys;
   hipLaunchKernelGGL(bn_act_apply_split_kernel, dim3(s / 64, c / 64, b), dim3(256), 0, st, x,
-                     (const float*)mean, (const float*)invstd, gamma, beta, c, s, slope, yh,
+                     fin, mean, invstd, gamma, beta, c, s, slope, yh,
                      yh + (size_t)b * s * c);
   return check_launch("bn_act_fwd_split");
 }
@@ -710,12 +784,10 @@ extern "C" int pcfm_bn_act_bwd_split(const float* dz, const float* x, const floa
   float* part = (float*)ws;
   hipLaunchKernelGGL(bn_bwd_stats_kernel, dim3(c, bn_parts(b)), dim3(256), 0, st, dz, x, mean,
                      invstd, gamma, beta, b, c, s, slope, part);
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(ceil_div(c, 256)), dim3(256), 0, st,
-                     (const float*)part, c, bn_parts(b), dgamma, dbeta);
   float* rowpart = dbias_in != nullptr ? part + (size_t)c * bn_parts(b) * 2 : nullptr;
   uint16_t* dxh = (uint16_t*)dxs;
   hipLaunchKernelGGL(bn_bwd_apply_split_kernel, dim3(s / 64, c / 64, b), dim3(256), 0, st, dz, x,
-                     mean, invstd, gamma, beta, (const float*)dgamma, (const float*)dbeta, c, s,
+                     mean, invstd, gamma, beta, (const float*)part, bn_parts(b), dgamma, dbeta, c, s,
                      (float)(1.0 / ((double)b * s)), slope, dxh, dxh + (size_t)b * s * c, rowpart);
   if (dbias_in != nullptr)
     hipLaunchKernelGGL(bn_bias_finalize_block_kernel, dim3(c), dim3(256), 0, st,
