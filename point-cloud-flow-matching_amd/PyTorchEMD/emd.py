@@ -3,7 +3,9 @@
 `emd_cuda` is the native module (approxmatch_forward / matchcost_forward /
 matchcost_backward, PyTorchEMD/cuda/emd.cpp:8-27) on the gfx950 library; float
 and double inputs are both supported, like the reference's
-AT_DISPATCH_FLOATING_TYPES.
+AT_DISPATCH_FLOATING_TYPES.  CPU tensors run the pure-PyTorch backend
+(pcfm.cpu_ops) where the reference asserts "Only support cuda currently."
+(emd.py:13).
 """
 import torch
 
@@ -18,7 +20,6 @@ class EarthMoverDistanceFunction(torch.autograd.Function):
     def forward(ctx, xyz1, xyz2):
         xyz1 = xyz1.contiguous()
         xyz2 = xyz2.contiguous()
-        assert xyz1.is_cuda and xyz2.is_cuda, "Only support cuda currently."
         match = emd_cuda.approxmatch_forward(xyz1, xyz2)
         cost = emd_cuda.matchcost_forward(xyz1, xyz2, match)
         ctx.save_for_backward(xyz1, xyz2, match)

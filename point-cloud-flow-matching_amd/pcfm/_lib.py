@@ -1,10 +1,9 @@
 """ctypes binding of the C ABI in include/pcfm.h (libpcfm_hip.so, gfx950).
 
 The library is built in-tree by ``__graft_entry__.build()`` (``make -C
-point-cloud-flow-matching_amd/csrc``).  There is no CPU implementation behind
-this module: if the library is missing, or a tensor is not on a HIP device,
-every op raises -- exactly like the reference backend, which only accepts CUDA
-tensors (third_party/pvcnn/modules/functional/src/utils.hpp:7-18).
+point-cloud-flow-matching_amd/csrc``).  Nothing here falls back: if the
+library is missing, every op on a HIP tensor raises.  (CPU tensors never reach
+this module -- pcfm.ops sends them to the pure-PyTorch pcfm.cpu_ops.)
 """
 from __future__ import annotations
 
@@ -126,7 +125,7 @@ def load() -> ctypes.CDLL:
                 raise RuntimeError(
                     f"pcfm: HIP library {LIB_PATH} is not built; run "
                     "`python -c 'import __graft_entry__ as g; g.build()'` "
-                    "(there is no CPU fallback)")
+                    "(HIP tensors have no fallback)")
             lib = ctypes.CDLL(LIB_PATH)
             for name, (res, args) in SIGNATURES.items():
                 fn = getattr(lib, name)

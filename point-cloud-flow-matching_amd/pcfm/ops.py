@@ -9,7 +9,9 @@ names, argument order and meaning, return values, and the same argument checks
 
 Every op runs on the current HIP stream of the tensors' device through the C ABI
 (include/pcfm.h); outputs are allocated with torch.empty (the kernels write
-every element, so the reference's torch::zeros pre-fill is not needed).
+every element, so the reference's torch::zeros pre-fill is not needed).  The
+reference-named entry points also accept CPU tensors, which run the pure-PyTorch
+backend in pcfm.cpu_ops (BASELINE configs[0]); HIP tensors never fall back.
 """
 from __future__ import annotations
 
@@ -18,7 +20,7 @@ import types
 
 import torch
 
-from . import _lib
+from . import _lib, cpu_ops
 
 
 # --------------------------------------------------------------------------
@@ -46,6 +48,23 @@ def _check_int(x: torch.Tensor, name: str) -> None:
 
 def _check(x, name, kind):
     _check_cuda(x, name)
+    _check_contig(x, name)
+    (_check_float if kind == "f" else _check_int)(x, name)
+
+
+def _host(*ts) -> bool:
+    """True when every tensor is a CPU tensor: the call then runs the pure-PyTorch
+    backend (pcfm.cpu_ops, BASELINE configs[0]); a mix of CPU and HIP tensors is an
+    error, as in the reference (utils.hpp:7-18)."""
+    cpu = [not t.is_cuda for t in ts if isinstance(t, torch.Tensor)]
+    if all(cpu):
+        return True
+    if any(cpu):
+        raise RuntimeError("all tensors must be on the same device (CUDA or CPU)")
+    return False
+
+
+def _check_host(x, name, kind):
     _check_contig(x, name)
     (_check_float if kind == "f" else _check_int)(x, name)
 
@@ -119,6 +138,10 @@ class _timed:
 # --------------------------------------------------------------------------
 def avg_voxelize_forward(features: torch.Tensor, coords: torch.Tensor, resolution: int):
     """vox.cpp:17-43: -> [out f32 (b,c,r^3), ind i32 (b,n), cnt i32 (b,r^3)]"""
+    if _host(features, coords):
+        _check_host(features, "features", "f")
+        _check_host(coords, "coords", "i")
+        return cpu_ops.avg_voxelize_forward(features, coords, resolution)
     _check(features, "features", "f")
     _check(coords, "coords", "i")
     b, c, n = features.shape
@@ -137,6 +160,11 @@ def avg_voxelize_forward(features: torch.Tensor, coords: torch.Tensor, resolutio
 
 def avg_voxelize_backward(grad_y: torch.Tensor, indices: torch.Tensor, cnt: torch.Tensor):
     """vox.cpp:54-76: grad_y (b,c,s) -> grad_x (b,c,n)"""
+    if _host(grad_y, indices, cnt):
+        _check_host(grad_y, "grad_y", "f")
+        _check_host(indices, "indices", "i")
+        _check_host(cnt, "cnt", "i")
+        return cpu_ops.avg_voxelize_backward(grad_y, indices, cnt)
     _check(grad_y, "grad_y", "f")
     _check(indices, "indices", "i")
     _check(cnt, "cnt", "i")
@@ -173,6 +201,10 @@ def avg_voxelize_backward_add(grad_y: torch.Tensor, indices: torch.Tensor, cnt: 
 def trilinear_devoxelize_forward(r: int, is_training: bool, coords: torch.Tensor,
                                  features: torch.Tensor):
     """trilinear_devox.cpp:18-55: -> [outs (b,c,n), inds (b,8,n)|(1,), wgts (b,8,n)|(1,)]"""
+    if _host(coords, features):
+        _check_host(features, "features", "f")
+        _check_host(coords, "coords", "f")
+        return cpu_ops.trilinear_devoxelize_forward(r, is_training, coords, features)
     _check(features, "features", "f")
     _check(coords, "coords", "f")
     b, c = features.shape[0], features.shape[1]
@@ -268,6 +300,11 @@ def rows_affine_(x: torch.Tensor, s: torch.Tensor, t) -> torch.Tensor:
 def trilinear_devoxelize_backward(grad_y: torch.Tensor, indices: torch.Tensor,
                                   weights: torch.Tensor, r: int):
     """trilinear_devox.cpp:67-91: grad_y (b,c,n) -> grad_x (b,c,r^3)"""
+    if _host(grad_y, indices, weights):
+        _check_host(grad_y, "grad_y", "f")
+        _check_host(weights, "weights", "f")
+        _check_host(indices, "indices", "i")
+        return cpu_ops.trilinear_devoxelize_backward(grad_y, indices, weights, r)
     _check(grad_y, "grad_y", "f")
     _check(weights, "weights", "f")
     _check(indices, "indices", "i")
@@ -286,6 +323,10 @@ def trilinear_devoxelize_backward(grad_y: torch.Tensor, indices: torch.Tensor,
 def ball_query(centers_coords: torch.Tensor, points_coords: torch.Tensor, radius: float,
                num_neighbors: int):
     """ball_query.cpp:6-30: centers (b,3,m), points (b,3,n) -> idx i32 (b,m,u)"""
+    if _host(centers_coords, points_coords):
+        _check_host(centers_coords, "centers_coords", "f")
+        _check_host(points_coords, "points_coords", "f")
+        return cpu_ops.ball_query(centers_coords, points_coords, radius, num_neighbors)
     _check(centers_coords, "centers_coords", "f")
     _check(points_coords, "points_coords", "f")
     b, m = centers_coords.shape[0], centers_coords.shape[2]
@@ -299,6 +340,10 @@ def ball_query(centers_coords: torch.Tensor, points_coords: torch.Tensor, radius
 
 def grouping_forward(features: torch.Tensor, indices: torch.Tensor):
     """grouping.cpp:6-22: features (b,c,n), indices (b,m,u) -> (b,c,m,u)"""
+    if _host(features, indices):
+        _check_host(features, "features", "f")
+        _check_host(indices, "indices", "i")
+        return cpu_ops.grouping_forward(features, indices)
     _check(features, "features", "f")
     _check(indices, "indices", "i")
     b, c, n = features.shape
@@ -311,6 +356,10 @@ def grouping_forward(features: torch.Tensor, indices: torch.Tensor):
 
 def grouping_backward(grad_y: torch.Tensor, indices: torch.Tensor, n: int):
     """grouping.cpp:24-44: grad_y (b,c,m,u) -> grad_x (b,c,n)"""
+    if _host(grad_y, indices):
+        _check_host(grad_y, "grad_y", "f")
+        _check_host(indices, "indices", "i")
+        return cpu_ops.grouping_backward(grad_y, indices, n)
     _check(grad_y, "grad_y", "f")
     _check(indices, "indices", "i")
     b, c = grad_y.shape[0], grad_y.shape[1]
@@ -356,9 +405,13 @@ backend = types.SimpleNamespace(
 # --------------------------------------------------------------------------
 def _chamfer_forward(xyz1, xyz2, dist1, dist2, idx1, idx2) -> int:
     try:
+        host = _host(xyz1, xyz2, dist1, dist2, idx1, idx2)
         for t, nm, k in ((xyz1, "xyz1", "f"), (xyz2, "xyz2", "f"), (dist1, "dist1", "f"),
                          (dist2, "dist2", "f"), (idx1, "idx1", "i"), (idx2, "idx2", "i")):
-            _check(t, nm, k)
+            (_check_host if host else _check)(t, nm, k)
+        if host:
+            cpu_ops.chamfer_forward(xyz1, xyz2, dist1, dist2, idx1, idx2)
+            return 1
         b, n, m = xyz1.shape[0], xyz1.shape[1], xyz2.shape[1]
         ws = _workspace(_lib.query("pcfm_chamfer_workspace_bytes", b, n, m), xyz1)
         _lib.call("pcfm_chamfer_fwd", _ptr(xyz1), _ptr(xyz2), b, n, m, _ptr(dist1), _ptr(dist2),
@@ -371,10 +424,15 @@ def _chamfer_forward(xyz1, xyz2, dist1, dist2, idx1, idx2) -> int:
 
 def _chamfer_backward(xyz1, xyz2, gradxyz1, gradxyz2, graddist1, graddist2, idx1, idx2) -> int:
     try:
+        host = _host(xyz1, xyz2, gradxyz1, gradxyz2, graddist1, graddist2, idx1, idx2)
         for t, nm, k in ((xyz1, "xyz1", "f"), (xyz2, "xyz2", "f"), (gradxyz1, "gradxyz1", "f"),
                          (gradxyz2, "gradxyz2", "f"), (graddist1, "graddist1", "f"),
                          (graddist2, "graddist2", "f"), (idx1, "idx1", "i"), (idx2, "idx2", "i")):
-            _check(t, nm, k)
+            (_check_host if host else _check)(t, nm, k)
+        if host:
+            cpu_ops.chamfer_backward(xyz1, xyz2, gradxyz1, gradxyz2, graddist1, graddist2, idx1,
+                                     idx2)
+            return 1
         b, n, m = xyz1.shape[0], xyz1.shape[1], xyz2.shape[1]
         _lib.call("pcfm_chamfer_bwd", _ptr(xyz1), _ptr(xyz2), b, n, m, _ptr(graddist1),
                   _ptr(graddist2), _ptr(idx1), _ptr(idx2), _ptr(gradxyz1), _ptr(gradxyz2),
@@ -391,14 +449,18 @@ chamfer_3D = types.SimpleNamespace(forward=_chamfer_forward, backward=_chamfer_b
 # --------------------------------------------------------------------------
 # emd_cuda (PyTorchEMD/cuda/emd.cpp:8-27): float and double
 # --------------------------------------------------------------------------
-def _emd_args(xyz1, xyz2):
-    _check_cuda(xyz1, "xyz1")
-    _check_cuda(xyz2, "xyz2")
+def _emd_check(xyz1, xyz2):
     if xyz2.shape[0] != xyz1.shape[0] or xyz1.shape[2] != 3 or xyz2.shape[2] != 3:
         raise RuntimeError(f"emd: expected (B,N,3) and (B,M,3), got {tuple(xyz1.shape)} "
                            f"and {tuple(xyz2.shape)}")
     if xyz1.dtype not in (torch.float32, torch.float64) or xyz2.dtype != xyz1.dtype:
         raise RuntimeError("emd: xyz1/xyz2 must both be float32 or both float64")
+
+
+def _emd_args(xyz1, xyz2):
+    _check_cuda(xyz1, "xyz1")
+    _check_cuda(xyz2, "xyz2")
+    _emd_check(xyz1, xyz2)
     sfx = "f32" if xyz1.dtype == torch.float32 else "f64"
     b, n, m = xyz1.shape[0], xyz1.shape[1], xyz2.shape[1]
     ws = _workspace(_lib.query("pcfm_emd_workspace_bytes", b, n, m, xyz1.element_size()), xyz1)
@@ -408,6 +470,9 @@ def _emd_args(xyz1, xyz2):
 def approxmatch_forward(xyz1: torch.Tensor, xyz2: torch.Tensor) -> torch.Tensor:
     """emd_kernel.cu:169-191: -> match (B, M, N)"""
     xyz1, xyz2 = xyz1.contiguous(), xyz2.contiguous()
+    if _host(xyz1, xyz2):
+        _emd_check(xyz1, xyz2)
+        return cpu_ops.approxmatch_forward(xyz1, xyz2)
     sfx, b, n, m, ws = _emd_args(xyz1, xyz2)
     match = torch.empty((b, m, n), dtype=xyz1.dtype, device=xyz1.device)
     if n == 0 or m == 0:
@@ -420,6 +485,9 @@ def approxmatch_forward(xyz1: torch.Tensor, xyz2: torch.Tensor) -> torch.Tensor:
 def matchcost_forward(xyz1: torch.Tensor, xyz2: torch.Tensor, match: torch.Tensor):
     """emd_kernel.cu:255-277: -> cost (B,)"""
     xyz1, xyz2, match = xyz1.contiguous(), xyz2.contiguous(), match.contiguous()
+    if _host(xyz1, xyz2, match):
+        _emd_check(xyz1, xyz2)
+        return cpu_ops.matchcost_forward(xyz1, xyz2, match)
     sfx, b, n, m, ws = _emd_args(xyz1, xyz2)
     cost = torch.empty((b,), dtype=xyz1.dtype, device=xyz1.device)
     _lib.call(f"pcfm_emd_matchcost_{sfx}", _ptr(xyz1), _ptr(xyz2), _ptr(match), b, n, m,
@@ -432,6 +500,9 @@ def matchcost_backward(grad_cost: torch.Tensor, xyz1: torch.Tensor, xyz2: torch.
     """emd_kernel.cu:371-396: -> [grad1 (B,N,3), grad2 (B,M,3)]"""
     xyz1, xyz2, match = xyz1.contiguous(), xyz2.contiguous(), match.contiguous()
     grad_cost = grad_cost.contiguous().to(xyz1.dtype)
+    if _host(grad_cost, xyz1, xyz2, match):
+        _emd_check(xyz1, xyz2)
+        return cpu_ops.matchcost_backward(grad_cost, xyz1, xyz2, match)
     sfx, b, n, m, ws = _emd_args(xyz1, xyz2)
     g1 = torch.empty((b, n, 3), dtype=xyz1.dtype, device=xyz1.device)
     g2 = torch.empty((b, m, 3), dtype=xyz1.dtype, device=xyz1.device)

@@ -1,6 +1,7 @@
 """The drop-in `modules` package and the flow models against goldens produced by
-the reference's own Python (tests/golden/make_golden.py), on the CPU with the
-oracle swapped in behind modules.functional (fixture `oracle_backend`)."""
+the reference's own Python (tests/golden/make_golden.py), on the CPU -- with the
+product's pure-PyTorch backend (pcfm.cpu_ops, BASELINE configs[0]) and, as a
+cross-check, with the C oracle swapped in behind modules.functional."""
 import numpy as np
 import pytest
 import torch
@@ -10,7 +11,15 @@ def _param_sums(module):
     return np.array([p.detach().double().sum().item() for _, p in module.named_parameters()])
 
 
-def test_pvconv_matches_reference(oracle_backend, golden):
+@pytest.fixture(params=["product", "oracle"])
+def cpu_backend(request):
+    """The product's own CPU backend, or the oracle behind modules.functional."""
+    if request.param == "oracle":
+        request.getfixturevalue("oracle_backend")
+    return request.param
+
+
+def test_pvconv_matches_reference(cpu_backend, golden):
     from modules.pvconv import PVConv
     g = golden("pvconv_r8.npz")
     torch.set_num_threads(1)
@@ -40,7 +49,7 @@ def test_state_dict_keys_match_reference_layout():
 
 
 @pytest.mark.parametrize("film_per_point", [True, False])
-def test_hybrid_matches_reference(oracle_backend, golden, film_per_point):
+def test_hybrid_matches_reference(cpu_backend, golden, film_per_point):
     from pcfm.models import HybridMLP
     g = golden("model_hybrid_c1.npz")
     torch.set_num_threads(1)
@@ -61,17 +70,24 @@ def test_hybrid_matches_reference(oracle_backend, golden, film_per_point):
     np.testing.assert_allclose(norms, g["grad_norms"], rtol=2e-3, atol=1e-6)
 
 
-def test_product_ops_refuse_cpu_tensors():
-    """No CPU path: the product raises like the reference's CHECK_CUDA."""
+def test_product_ops_check_arguments_on_cpu():
+    """CPU tensors run the pure-PyTorch backend, with the reference's argument
+    checks (utils.hpp:7-18 -> RuntimeError); PointNet++-only ops stay out."""
     from pcfm import ops
     x = torch.zeros(1, 4, 10)
-    with pytest.raises(RuntimeError, match="must be a CUDA tensor"):
-        ops.avg_voxelize_forward(x, torch.zeros(1, 3, 10, dtype=torch.int32), 2)
-    with pytest.raises(RuntimeError, match="must be a CUDA tensor"):
-        ops.trilinear_devoxelize_forward(2, True, torch.zeros(1, 3, 10), torch.zeros(1, 4, 8))
+    with pytest.raises(RuntimeError, match="must be an int tensor"):
+        ops.avg_voxelize_forward(x, torch.zeros(1, 3, 10), 2)
+    with pytest.raises(RuntimeError, match="must be a contiguous tensor"):
+        ops.trilinear_devoxelize_forward(2, True, torch.zeros(1, 10, 3).transpose(1, 2),
+                                         torch.zeros(1, 4, 8))
+    with pytest.raises(RuntimeError, match="must be a float tensor"):
+        ops.ball_query(torch.zeros(1, 3, 4, dtype=torch.float64), torch.zeros(1, 3, 10), 0.1, 2)
     with pytest.raises(NotImplementedError):
         ops.backend.furthest_point_sampling(x, 3)
     from chamfer3D.dist_chamfer_3D import chamfer_3D
     d = torch.zeros(1, 10)
     i = torch.zeros(1, 10, dtype=torch.int32)
-    assert chamfer_3D.forward(torch.zeros(1, 10, 3), torch.zeros(1, 10, 3), d, d, i, i) == 0
+    assert chamfer_3D.forward(torch.zeros(1, 10, 3), torch.zeros(1, 10, 3), d, d, i, i) == 1
+    # chamfer reports a bad argument like the reference (prints, returns 0)
+    assert chamfer_3D.forward(torch.zeros(1, 10, 3), torch.zeros(1, 10, 3), d, d, i.long(),
+                              i) == 0

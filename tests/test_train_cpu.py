@@ -1,5 +1,5 @@
-"""Train-step plumbing on the CPU (config C1: B=2, N=1024, xyz+rgb, hybrid),
-with the oracle behind modules.functional."""
+"""Train-step plumbing on the CPU (config C1: B=2, N=1024, xyz+rgb, hybrid) on the
+product's pure-PyTorch CPU backend (no oracle involved)."""
 import math
 
 import torch
@@ -15,7 +15,7 @@ def small_cfg(**kw):
     return TrainConfig(**base)
 
 
-def test_train_step_c1_full_size_model(oracle_backend):
+def test_train_step_c1_full_size_model():
     """C1 with the default (full-width) hybrid model: one step, finite losses."""
     torch.manual_seed(0)
     cfg = TrainConfig(batch_size=2, num_points=1024, steps_per_epoch=1, epochs=1)
@@ -25,7 +25,7 @@ def test_train_step_c1_full_size_model(oracle_backend):
     assert math.isfinite(out["loss_point"].item()) and math.isfinite(out["loss_latent"].item())
 
 
-def test_train_steps_reduce_loss(oracle_backend):
+def test_train_steps_reduce_loss():
     cfg = small_cfg(lr_pf=1e-3, lr_enc=1e-3, lr_lf=1e-3, warmup_steps=0, use_cosine_lr=False)
     tr = Trainer(cfg, "cpu")
     tr.train_mode()
@@ -35,7 +35,7 @@ def test_train_steps_reduce_loss(oracle_backend):
     assert losses[-1] < losses[0]
 
 
-def test_warmup_epoch_uses_geometry_only(oracle_backend):
+def test_warmup_epoch_uses_geometry_only():
     cfg = small_cfg()
     tr = Trainer(cfg, "cpu")
     tr.train_mode()
