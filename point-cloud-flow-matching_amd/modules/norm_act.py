@@ -39,7 +39,10 @@ def _fusable(x: torch.Tensor, bn) -> bool:
             and bn.running_mean is not None and not torch.is_autocast_enabled("cuda")):
         return False
     s = x[0, 0].numel()
-    return s % 4 == 0 and x.shape[0] * x.shape[1] < 65536 and x.numel() > 0
+    # one value per channel: torch's batch_norm raises ("Expected more than 1 value
+    # per channel"), so such a call takes the module path and raises the same way
+    return (s % 4 == 0 and x.shape[0] * x.shape[1] < 65536 and x.numel() > 0
+            and x.shape[0] * s > 1)
 
 
 def bn_act(x: torch.Tensor, bn, slope: float) -> torch.Tensor:
@@ -171,7 +174,8 @@ def conv_bn_act_pair(conv1, bn1, slope1: float, conv2, bn2, slope2: float,
           and _fusable_pre(bn1) and _fusable_pre(bn2) and hasattr(conv1, "x3_ok")
           and hasattr(conv2, "x3_ok") and conv1.x3_ok(x) and conv1.bias is not None
           and conv2.bias is not None and conv1.out_channels % 64 == 0
-          and x[0, 0].numel() % 64 == 0 and x.shape[0] * conv2.out_channels < 65536)
+          and x[0, 0].numel() % 64 == 0 and x.shape[0] * conv2.out_channels < 65536
+          and x.shape[0] * conv1.out_channels < 65536 and x.shape[0] * x[0, 0].numel() > 1)
     if ok:
         from pcfm import ops
         # shape / dtype / device stand-in for conv1's output (no allocation)
@@ -193,7 +197,8 @@ def conv_bn_act(conv, bn, x: torch.Tensor, slope: float) -> torch.Tensor:
     """act(bn(conv(x))) for a PointwiseConv1d / VoxelConv3d `conv`: one fused
     autograd node on the GPU path, the modules' own forwards otherwise."""
     if _fusable_pre(bn) and hasattr(conv, "x3_ok") and conv.x3_ok(x) and conv.bias is not None:
-        out_shape_ok = x[0, 0].numel() % 4 == 0 and x.shape[0] * conv.out_channels < 65536
+        out_shape_ok = (x[0, 0].numel() % 4 == 0 and x.shape[0] * conv.out_channels < 65536
+                        and x.shape[0] * x[0, 0].numel() > 1)
         if out_shape_ok:
             from modules.shared_mlp import PointwiseConv1d
             fn = _PwBnAct if isinstance(conv, PointwiseConv1d) else _Conv3dBnAct

@@ -104,6 +104,9 @@ class TrainConfig:
     # ~94-113 TFLOP/s fp32 on the PVConv Conv3d shapes vs 12-68 TFLOP/s with
     # the default heuristic pick (tools/conv3d_probe.py on MI355X); same math.
     miopen_find: bool = True
+    # parity mode: fp32 convolutions on exact fp32 arithmetic instead of the
+    # bf16x3 matrix-core kernels (pcfm.precision); process-wide when set
+    exact_fp32: bool = False
 
     @property
     def enc_in_ch(self) -> int:
@@ -273,6 +276,9 @@ class Trainer:
         if self.device.type == "cuda" and cfg.tunableop:
             out = os.environ.get("PCFM_TUNE_GEMMS")  # tools/tune_gemms.sh: measure, write here
             enable_tunableop(out, tune=True) if out else enable_tunableop()
+        if cfg.exact_fp32:
+            from pcfm.precision import set_exact_fp32
+            set_exact_fp32(True)
         self.rank, self.world_size = rank, world_size
         seed_all(cfg.seed + rank)
         self.enc, self.pf, self.lf = build_models(cfg, self.device)
@@ -334,15 +340,38 @@ class Trainer:
             z[..., 3:] = 0.0
         return z
 
+    def _pf_prior_from(self, raw: torch.Tensor) -> torch.Tensor:
+        """make_pf_prior_like (train.py:266-279) on injected raw draws."""
+        cfg = self.cfg
+        if raw.shape[-1] == 3:
+            return raw * cfg.point_prior_std
+        z = torch.empty_like(raw)
+        z[..., :3] = raw[..., :3] * cfg.point_prior_std
+        if cfg.color_prior == "gauss":
+            z[..., 3:] = raw[..., 3:] * cfg.color_prior_std
+        elif cfg.color_prior == "uniform":
+            z[..., 3:] = raw[..., 3:]
+        else:
+            z[..., 3:] = 0.0
+        return z
+
     def train_mode(self):
         self.enc.train()
         self.pf.train()
         self.lf.train()
 
     # -- one iteration ------------------------------------------------------
-    def step(self, batch: Dict[str, torch.Tensor], epoch: int) -> Dict[str, torch.Tensor]:
+    def step(self, batch: Dict[str, torch.Tensor], epoch: int,
+             draws: Optional[Dict[str, torch.Tensor]] = None) -> Dict[str, torch.Tensor]:
+        """One iteration.  `draws` injects the step's random numbers instead of
+        sampling them (parity tests replay a recorded reference step,
+        tests/golden/make_train_golden.py): z_pts (B, N, D) raw prior draws (xyz
+        randn | rgb rand), t_pts (B,), drop_u (B,) CFG-drop uniforms, eps_z
+        (B, latent) randn, t_z (B,) -- scaled by the configured stds here as the
+        reference scales its own draws (train.py:271-276, :595, :617, :637)."""
         cfg = self.cfg
         dev = self.device
+        dr = None if draws is None else {k: v.to(dev) for k, v in draws.items()}
         pts = batch["train_points"].to(dev).float()
         rgb = batch.get("train_rgb")
         rgb = rgb.to(dev).float() if rgb is not None else None
@@ -363,17 +392,19 @@ class Trainer:
         if cfg.pf_point_dim == 6:
             if rgb is not None and use_rgb:
                 data_pf = torch.cat([pts, rgb], dim=-1)
-                z_pts = self._pf_prior(data_pf)
+                z_pts = self._pf_prior(data_pf) if dr is None else self._pf_prior_from(dr["z_pts"])
             else:
                 data_pf = torch.cat([pts, torch.zeros_like(pts)], dim=-1)
                 z_pts = torch.empty_like(data_pf)
-                z_pts[..., :3] = torch.randn_like(pts) * cfg.point_prior_std
+                xyz = torch.randn_like(pts) if dr is None else dr["z_pts"][..., :3]
+                z_pts[..., :3] = xyz * cfg.point_prior_std
                 z_pts[..., 3:] = 0.0
         else:
             data_pf = pts
-            z_pts = torch.randn_like(data_pf) * cfg.point_prior_std
+            z = torch.randn_like(data_pf) if dr is None else dr["z_pts"]
+            z_pts = z * cfg.point_prior_std
         b, n, d = data_pf.shape
-        t_pts = self._sample_t(b, data_pf.dtype)
+        t_pts = self._sample_t(b, data_pf.dtype) if dr is None else dr["t_pts"].to(data_pf.dtype)
         x_t = (1.0 - t_pts)[:, None, None] * z_pts + t_pts[:, None, None] * data_pf
         target_v = data_pf - z_pts
 
@@ -382,7 +413,8 @@ class Trainer:
         if cfg.cfg_drop_p > 0.0:
             p_now = cfg.cfg_drop_p * min(1.0, max(0.0, epoch / max(1, cfg.cfg_drop_warmup_epochs)))
             if p_now > 0.0:
-                cond_drop_mask = (torch.rand(b, device=dev) < p_now).to(data_pf.dtype)[:, None]
+                u = torch.rand(b, device=dev) if dr is None else dr["drop_u"]
+                cond_drop_mask = (u < p_now).to(data_pf.dtype)[:, None]
 
         with self._autocast():
             pred_v = self.model_pf(x_t, t_pts, cond_full, cond_drop_mask=cond_drop_mask)
@@ -396,8 +428,8 @@ class Trainer:
 
         # latent FM (train.py:636-645)
         z_det = z.detach()
-        eps_z = torch.randn_like(z_det) * cfg.latent_prior_std
-        t_z = self._sample_t(b, z_det.dtype)
+        eps_z = (torch.randn_like(z_det) if dr is None else dr["eps_z"]) * cfg.latent_prior_std
+        t_z = self._sample_t(b, z_det.dtype) if dr is None else dr["t_z"].to(z_det.dtype)
         y_t = (1.0 - t_z)[:, None] * eps_z + t_z[:, None] * z_det
         target_v_z = z_det - eps_z
         with self._autocast():

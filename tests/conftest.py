@@ -6,6 +6,7 @@
 * `oracle_backend` fixture: CPU tests swap the C oracle in behind
   modules.functional (the product itself has no CPU path).
 """
+import json
 import os
 import sys
 
@@ -38,6 +39,26 @@ def golden():
     def load(name):
         return np.load(os.path.join(GOLDEN, name), allow_pickle=False)
     return load
+
+
+_REPORT = {}
+
+
+@pytest.fixture(scope="session")
+def report():
+    """report(key, value): measured deviations / timings, written as JSON to
+    $PCFM_REPORT at the end of the session (the GPU runs copy it to profiles/)."""
+    def rec(key, value):
+        _REPORT[key] = value
+    return rec
+
+
+def pytest_sessionfinish(session, exitstatus):
+    path = os.environ.get("PCFM_REPORT")
+    if path and _REPORT:
+        os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+        with open(path, "w") as f:
+            json.dump(_REPORT, f, indent=1, sort_keys=True, default=float)
 
 
 def have_gpu():

@@ -32,23 +32,46 @@ def test_native_library_is_what_runs():
     assert lib._name.endswith("libpcfm_hip.so")
 
 
-def test_pvconv_gpu_matches_reference(golden):
+def _rel_max(got, ref):
+    """max |got - ref| / max |ref|: the norm-wise relative error the tolerances use."""
+    return float(np.abs(got - ref).max() / np.abs(ref).max())
+
+
+# biases of convolutions that feed a BatchNorm: analytically zero gradient
+_NOISE_BIAS = ("layers.0.bias", "voxel_layers.0.bias", "voxel_layers.3.bias")
+
+
+@pytest.mark.parametrize("mode", ["exact_fp32", "bf16x3"])
+def test_pvconv_gpu_matches_reference(golden, report, mode):
+    """PVConv(16, 16, r=8, SE) vs the reference module's output (pvconv_r8.npz):
+    exact-fp32 convolutions within 1e-5, the bf16x3 default within 1e-4."""
     from modules.pvconv import PVConv
+    from pcfm.precision import exact_fp32
     g = golden("pvconv_r8.npz")
     torch.manual_seed(int(g["seed"]))
     blk = PVConv(16, 16, kernel_size=3, resolution=8, with_se=True, normalize=True, eps=1e-6)
     np.testing.assert_allclose(_param_sums(blk), g["param_sums"], rtol=1e-12, atol=1e-12)
     blk = blk.to(DEV)
     feats = torch.from_numpy(g["feats"]).to(DEV).requires_grad_(True)
-    out, _ = blk((feats, torch.from_numpy(g["coords"]).to(DEV)))
-    np.testing.assert_allclose(out.detach().cpu().numpy(), g["out"], rtol=1e-4, atol=1e-5)
-    loss = (out * torch.linspace(-1, 1, out.numel(), device=DEV).view_as(out)).sum()
-    loss.backward()
-    np.testing.assert_allclose(feats.grad.cpu().numpy(), g["grad_feats"], rtol=1e-3, atol=1e-4)
+    with exact_fp32(mode == "exact_fp32"):
+        out, _ = blk((feats, torch.from_numpy(g["coords"]).to(DEV)))
+        loss = (out * torch.linspace(-1, 1, out.numel(), device=DEV).view_as(out)).sum()
+        loss.backward()
+    e_out = _rel_max(out.detach().cpu().numpy(), g["out"])
+    e_grad = _rel_max(feats.grad.cpu().numpy(), g["grad_feats"])
+    report(f"pvconv_r8_{mode}", {"out": e_out, "grad_feats": e_grad})
+    tol = 1e-5 if mode == "exact_fp32" else 1e-4
+    assert e_out < tol and e_grad < tol, (e_out, e_grad)
 
 
-def test_hybrid_gpu_matches_reference(golden):
+@pytest.mark.parametrize("mode", ["exact_fp32", "bf16x3"])
+def test_hybrid_gpu_matches_reference(golden, report, mode):
+    """HybridMLP (C1, fp32) vs the reference model's velocity, loss and gradient
+    norms (model_hybrid_c1.npz).  exact-fp32: v and the loss within 1e-5
+    (north_star), gradient norms within 1e-4; bf16x3: the measured deviation is
+    reported and bounded at 1e-4 (v, loss) / 1e-3 (gradients)."""
     from pcfm.models import HybridMLP
+    from pcfm.precision import exact_fp32
     g = golden("model_hybrid_c1.npz")
     torch.manual_seed(int(g["seed"]))
     pf = HybridMLP(cond_dim=129, point_dim=6)
@@ -56,16 +79,25 @@ def test_hybrid_gpu_matches_reference(golden):
     np.testing.assert_allclose(_param_sums(pf), g["param_sums"], rtol=1e-12, atol=1e-12)
     pf = pf.to(DEV).train()
     x = torch.from_numpy(g["x"]).to(DEV)
-    v = pf(x, torch.from_numpy(g["t"]).to(DEV), torch.from_numpy(g["cond"]).to(DEV),
-           cond_drop_mask=torch.from_numpy(g["mask"]).to(DEV))
-    np.testing.assert_allclose(v.detach().cpu().numpy(), g["v"], rtol=1e-3, atol=1e-4)
-    loss = torch.nn.functional.mse_loss(v, torch.from_numpy(g["target"]).to(DEV))
-    np.testing.assert_allclose(loss.item(), float(g["loss"]), rtol=1e-4)
-    loss.backward()
+    with exact_fp32(mode == "exact_fp32"):
+        v = pf(x, torch.from_numpy(g["t"]).to(DEV), torch.from_numpy(g["cond"]).to(DEV),
+               cond_drop_mask=torch.from_numpy(g["mask"]).to(DEV))
+        loss = torch.nn.functional.mse_loss(v, torch.from_numpy(g["target"]).to(DEV))
+        loss.backward()
+    e_v = _rel_max(v.detach().cpu().numpy(), g["v"])
+    e_loss = abs(loss.item() - float(g["loss"])) / abs(float(g["loss"]))
+    names = [n for n, _ in pf.named_parameters()]
     norms = np.array([p.grad.double().norm().item() if p.grad is not None else 0.0
                       for p in pf.parameters()])
-    # fp32 GPU convolutions vs CPU: gradients agree to ~1e-3 relative per tensor
-    np.testing.assert_allclose(norms, g["grad_norms"], rtol=1e-2, atol=1e-5)
+    live = np.array([not n.endswith(_NOISE_BIAS) for n in names])
+    gdev = np.abs(norms - g["grad_norms"]) / np.maximum(g["grad_norms"], 1e-30)
+    e_g = float(gdev[live].max())
+    report(f"hybrid_c1_{mode}", {"v": e_v, "loss": e_loss, "grad_norms": e_g,
+                                 "worst_grad": names[int(np.argmax(np.where(live, gdev, 0)))]})
+    if mode == "exact_fp32":
+        assert e_v < 1e-5 and e_loss < 1e-5 and e_g < 1e-4, (e_v, e_loss, e_g)
+    else:
+        assert e_v < 1e-4 and e_loss < 1e-4 and e_g < 1e-3, (e_v, e_loss, e_g)
 
 
 def test_train_step_gpu_small():
