@@ -12,10 +12,18 @@ Prints ONE JSON line on rank 0.  value = points/s of the whole job
 in HBM before the timed region.  Besides the contract fields it carries:
   roofline      the dominant hot-path kernel (by time inside the step), its
                 algorithmic bytes / its HIP-event time, vs 8 TB/s
-  cpu_baseline  the same train step on the host CPU (torch CPU + the C oracle
-                behind modules.functional), on a bounded sample
-  chamfer       Chamfer-3D fwd+bwd ms at the reference's published shape
-                (32x2000 / 32x1000, 1.4 ms) and at the C2 shape
+  cpu_baseline  the same train step on the host CPU -- the reference's model
+                math (per-point FiLM as models.py:135/594 computes it, fp32
+                torch CPU convolutions) on this build's pure-PyTorch CPU
+                backend (pcfm.cpu_ops) -- plus the reference's CPU Chamfer
+                (train.py:80-84 cdist form), on bounded samples; the host CPU
+                model, cores and threads are stated
+  chamfer       Chamfer-3D fwd / fwd+bwd ms at the reference's published shape
+                (32x2000 / 32x1000, 1.4 ms), at C2 and at C5, with the VALU
+                roofline of the forward (8 FLOP per pair)
+  emd, ball_query   EMD (approxmatch + matchcost, and backward) at N = 2048 / 4096
+                and ball query at the C2 / C5 cloud sizes
+  distributed   torch.distributed backend and world size as the run saw them
 Progress goes to stderr.
 """
 from __future__ import annotations
@@ -37,6 +45,7 @@ import torch.distributed as dist  # noqa: E402
 
 METRIC = "train-step points/sec (B=8, N=20000, xyz+rgb) at 1/2/4/8 MI355X; Chamfer ms"
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+FP32_VALU_TF = 157.3            # MI355X fp32 vector peak (Chamfer / ball query: VALU-bound)
 BF16_DENSE_TF = 2500.0          # MI355X dense bf16 MFMA peak (no sparsity)
 VOXEL_OPS = ("avg_voxelize_fwd", "avg_voxelize_bwd", "trilinear_devoxelize_fwd",
              "trilinear_devoxelize_bwd")  # the PVConv scatter/gather
@@ -46,12 +55,16 @@ H100_DERIVED_PTS = 1.88e6       # 25 s/epoch at <= 293 steps/epoch 
 TRAFFIC_FILE = os.path.join(REPO, "profiles", "r01_traffic.json")
 
 
-def measured_traffic(op):
+def measured_traffic(op, batch, points):
     """Mean PMC traffic per launch of `op` over the bench's three stage shapes
-    (each runs twice per step), or None when no PMC summary is committed."""
+    (each runs twice per step), or None when no PMC summary is committed for
+    this run's (B, N) -- the committed counters are per shape."""
     try:
-        data = json.load(open(TRAFFIC_FILE))["ops"]
+        blob = json.load(open(TRAFFIC_FILE))
+        data = blob["ops"]
     except (OSError, ValueError, KeyError):
+        return None
+    if (blob.get("batch", 8), blob.get("points", 20000)) != (batch, points):
         return None
     vals = [v["traffic_bytes"] for k, v in data.items() if k.split("@")[0] == op]
     return sum(vals) / len(vals) if len(vals) == 3 else None
@@ -71,7 +84,7 @@ def parse():
     p.add_argument("--backbone", default="hybrid", choices=["hybrid", "mlp"])
     p.add_argument("--surface", action="store_true", help="points near the unit sphere")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-batch", type=int, default=2, help="CPU baseline sample batch")
+    p.add_argument("--cpu-batch", type=int, default=8, help="CPU baseline sample batch")
     p.add_argument("--no-chamfer", action="store_true")
     p.add_argument("--no-event-timing", action="store_true")
     p.add_argument("--profile-steps", type=int, default=2,
@@ -105,34 +118,100 @@ def chamfer_ms(dev, b, n, m, iters=20):
     return res
 
 
+def host_cpu():
+    """lscpu's model name, sockets, cores and threads of the host."""
+    info = {}
+    try:
+        import subprocess
+        txt = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in txt.splitlines():
+            k, _, v = line.partition(":")
+            info[k.strip()] = v.strip()
+    except Exception:  # noqa: BLE001 -- informational only
+        pass
+    out = {"model": info.get("Model name"), "logical_cpus": os.cpu_count()}
+    try:
+        out["physical_cores"] = int(info["Core(s) per socket"]) * int(info["Socket(s)"])
+        out["threads_per_core"] = int(info["Thread(s) per core"])
+    except (KeyError, ValueError):
+        pass
+    return out
+
+
 def cpu_baseline(args, cfg_kwargs):
-    """The reference's CPU-capable path (torch CPU, PVCNN ops through the C
-    oracle), one train step on a bounded sample after one warm-up step."""
-    from oracle.oracle import TorchBackend
-    import modules.functional.backend as be
+    """The reference's CPU-capable path: one train step of the same model on the
+    host (fp32 torch CPU, the reference's per-point FiLM form, PVCNN ops on the
+    pure-PyTorch CPU backend pcfm.cpu_ops -- the reference itself has no CPU
+    backend), timed after one small warm-up step; and the reference's CPU
+    Chamfer (train.py:80-84: cdist, squared, min both ways) on one cloud pair."""
     from pcfm.train import TrainConfig, Trainer, synthetic_batch
 
-    threads = min(16, os.cpu_count() or 1)
-    torch.set_num_threads(threads)
-    saved = be._backend
-    be._backend = TorchBackend()
-    try:
-        cfg = TrainConfig(**{**cfg_kwargs, "batch_size": args.cpu_batch})
-        tr = Trainer(cfg, "cpu")
-        tr.train_mode()
-        batch = synthetic_batch(cfg, "cpu", surface=args.surface)
-        tr.step(batch, epoch=201)
-        t0 = time.perf_counter()
-        tr.step(batch, epoch=201)
-        dt = time.perf_counter() - t0
-    finally:
-        be._backend = saved
+    threads = torch.get_num_threads()  # OMP_NUM_THREADS: the box's CPU share
+    cfg = TrainConfig(**{**cfg_kwargs, "batch_size": args.cpu_batch, "film_per_point": True})
+    tr = Trainer(cfg, "cpu")
+    tr.train_mode()
+    warm = TrainConfig(**{**cfg_kwargs, "batch_size": 1, "num_points": 2048})
+    tr.step(synthetic_batch(warm, "cpu", surface=args.surface), epoch=201)
+    batch = synthetic_batch(cfg, "cpu", surface=args.surface)
+    t0 = time.perf_counter()
+    tr.step(batch, epoch=201)
+    dt = time.perf_counter() - t0
     pts = cfg.batch_size * cfg.num_points
+    n = cfg.num_points
+    g = torch.Generator().manual_seed(0)
+    a, b = torch.rand(1, n, 3, generator=g), torch.rand(1, n, 3, generator=g)
+    t1 = time.perf_counter()
+    d2 = torch.cdist(a, b, p=2).pow(2)
+    _ = d2.min(dim=2).values.mean(dim=1) + d2.min(dim=1).values.mean(dim=1)
+    cd = time.perf_counter() - t1
+    del d2
     return {"value": pts / dt, "unit": "points/s", "cores": threads, "kind": "port",
-            "sample": f"1 timed train step (after 1 warm-up) at B={cfg.batch_size}, "
-                      f"N={cfg.num_points}, {cfg.pf_backbone} backbone, fp32 torch CPU + C "
-                      f"oracle voxel ops; {dt:.2f} s/step",
-            "seconds_per_step": dt}
+            "host_cpu": host_cpu(),
+            "sample": f"1 timed train step (after a B=1, N=2048 warm-up) at B={cfg.batch_size}, "
+                      f"N={n}, {cfg.pf_backbone} backbone, fp32 torch CPU, per-point FiLM, "
+                      f"pcfm.cpu_ops voxel ops, {threads} threads; {dt:.2f} s/step",
+            "seconds_per_step": dt,
+            "chamfer_cdist_fwd_ms": {"shape": f"1x{n}x{n}", "ms": cd * 1e3,
+                                     "c2_equivalent_ms": cd * 1e3 * cfg_kwargs["batch_size"]}}
+
+
+def emd_ms(dev, b, n, iters=3):
+    """EMD (PyTorchEMD/emd.py: approxmatch + matchcost) forward and fwd+bwd ms."""
+    from PyTorchEMD.emd import earth_mover_distance
+    g = torch.Generator(device=dev).manual_seed(0)
+    p1 = torch.rand(b, n, 3, device=dev, generator=g)
+    p2 = torch.rand(b, n, 3, device=dev, generator=g)
+    res = {}
+    for bwd in (False, True):
+        for i in range(iters + 1):
+            if i == 1:
+                torch.cuda.synchronize(dev)
+                t0 = time.perf_counter()
+            x = p1.detach().requires_grad_(bwd)
+            d = earth_mover_distance(x, p2, transpose=False)
+            if bwd:
+                d.sum().backward()
+        torch.cuda.synchronize(dev)
+        res["fwd_bwd_ms" if bwd else "fwd_ms"] = (time.perf_counter() - t0) * 1e3 / iters
+    # 10 levels x 3 passes over the B*N*M pairs, one exp each (emd_kernel.cu:44-154)
+    res["exps_per_s_fwd"] = 30.0 * b * n * n / (res["fwd_ms"] * 1e-3)
+    return res
+
+
+def ball_query_ms(dev, b, n, m, radius, u, iters=5):
+    from pcfm import ops
+    g = torch.Generator(device=dev).manual_seed(0)
+    pts = torch.rand(b, 3, n, device=dev, generator=g)
+    ctr = torch.rand(b, 3, m, device=dev, generator=g)
+    ops.ball_query(ctr, pts, radius, u)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        ops.ball_query(ctr, pts, radius, u)
+    torch.cuda.synchronize(dev)
+    ms = (time.perf_counter() - t0) * 1e3 / iters
+    return {"shape": f"B={b} N={n} M={m} radius={radius} U={u}", "ms": ms,
+            "distance_tests_per_s_upper": b * m * n / (ms * 1e-3)}
 
 
 def main():
@@ -227,7 +306,7 @@ def main():
             sec = d["ms"] * 1e-3
             if d["kind"] == "hbm":
                 achieved = d["amount"] / sec / 1e9
-                traffic = measured_traffic(op)
+                traffic = measured_traffic(op, cfg.batch_size, cfg.num_points)
                 return {"kernel": op, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                         "traffic_unit": "bytes per launch (PMC, profiles/r01_traffic.json)"
@@ -241,7 +320,7 @@ def main():
                         "frac": achieved / BF16_DENSE_TF, "traffic": None,
                         "algorithmic_flops_per_launch": d["amount"] / d["launches"],
                         "avg_launch_ms": d["ms"] / d["launches"]}
-            traffic = measured_traffic(op)
+            traffic = measured_traffic(op, cfg.batch_size, cfg.num_points)
             return {"kernel": op, "bound": "mfma", "achieved": achieved, "peak": BF16X3_PEAK_TF,
                     "unit": "TFLOP/s", "frac": achieved / BF16X3_PEAK_TF, "traffic": traffic,
                     "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE + WRITE_SIZE, "
@@ -257,19 +336,35 @@ def main():
         roofline_scatter = roof(max(hbm_ops, key=lambda k: summary[k]["ms"])) if hbm_ops else None
         log(f"{ms:.2f} ms/step, {value / 1e6:.3f} M points/s; losses {loss_p:.4f} {loss_z:.4f}")
         cham = None
+        extra = {}
         if not args.no_chamfer:
             cham = {"published_shape_32x2000x1000": chamfer_ms(dev, 32, 2000, 1000),
                     "published_fwd_bwd_ms": 1.4,
                     "c2_shape_8x20000x20000": chamfer_ms(dev, 8, 20000, 20000, iters=5),
                     "c5_shape_4x100000x100000": chamfer_ms(dev, 4, 100000, 100000, iters=2)}
+            for key, (b_, n_) in (("c2_shape_8x20000x20000", (8, 20000)),
+                                  ("c5_shape_4x100000x100000", (4, 100000))):
+                fwd = cham[key]["fwd"] * 1e-3
+                flops = 8.0 * 2 * b_ * n_ * n_  # 2*B*N*M pairs x 8 FLOP
+                cham[key]["roofline_fwd"] = {
+                    "bound": "valu", "achieved": flops / fwd / 1e12, "peak": FP32_VALU_TF,
+                    "unit": "TFLOP/s", "frac": flops / fwd / 1e12 / FP32_VALU_TF,
+                    "pairs_per_s": 2 * b_ * n_ * n_ / fwd,
+                    "note": "wall clock of the op incl. launch; 8 FLOP per pair (SURVEY 8d)"}
             log(f"chamfer: {cham}")
+            extra["emd"] = {f"B8_N{n_}": emd_ms(dev, 8, n_) for n_ in (2048, 4096)}
+            extra["ball_query"] = {"c2": ball_query_ms(dev, 8, 20000, 2048, 0.1, 32),
+                                   "c5": ball_query_ms(dev, 4, 100000, 4096, 0.05, 32)}
+            log(f"emd / ball query: {extra}")
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             log("cpu baseline: running one warm-up + one timed CPU step ...")
             cpu = cpu_baseline(args, cfg_kwargs)
             log(f"cpu baseline: {cpu['seconds_per_step']:.2f} s/step")
+        metric = METRIC if (cfg.batch_size, cfg.num_points) == (8, 20000) else METRIC.replace(
+            "B=8, N=20000", f"B={cfg.batch_size}, N={cfg.num_points}")
         line = {
-            "metric": METRIC, "value": value, "unit": "points/s", "n_gpus": world,
+            "metric": metric, "value": value, "unit": "points/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "vs_h100_derived_upper_bound": value / H100_DERIVED_PTS,
@@ -284,8 +379,10 @@ def main():
                        "global_batch": world * cfg.batch_size, "points_per_cloud": cfg.num_points,
                        "backbone": cfg.pf_backbone, "parallelism": f"dp{world}"},
             "roofline": roofline, "roofline_voxel_scatter_gather": roofline_scatter,
-            "kernels": kernels, "cpu_baseline": cpu, "chamfer": cham,
+            "kernels": kernels, "cpu_baseline": cpu, "chamfer": cham, **extra,
             "loss_point": loss_p, "loss_latent": loss_z,
+            "distributed": {"backend": dist.get_backend() if ddp else None,
+                            "world_size": dist.get_world_size() if ddp else 1},
         }
         print(json.dumps(line), flush=True)
     if ddp:

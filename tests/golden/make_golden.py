@@ -17,7 +17,8 @@ What is pinned by what:
     its inputs and its exact-assignment ground truth `gt_dist` and gradients
     (the script's own arithmetic, restated here because the script imports the
     JIT-built extension at import time).
-  * pvconv_r8.npz / model_hybrid_c1.npz -- the reference's Python modules
+  * pvconv_r8.npz / model_hybrid_c1.npz / model_hybrid_c1_perturbed.npz --
+    the reference's Python modules
     (pvcnn modules.PVConv; models.HybridMLP) run on the CPU with the native
     `_pvcnn_backend` replaced by this build's C oracle (oracle/pcfm_oracle.c).
     These pin the Python composition (coordinate normalisation and rounding,
@@ -147,12 +148,58 @@ def pvcnn_fixtures(ref: str) -> None:
                              for p in pf.parameters()]))
 
 
+def perturb_zero_init_(module, seed: int = 5, std: float = 0.05) -> None:
+    """Give every all-zero parameter (zero-initialised FiLM affines, head_out,
+    output biases, ...) seeded N(0, std^2) values, in named_parameters order.  At
+    the reference's initialisation ContextNet.head_out is zero, so the velocity
+    does not depend on the PVConv pyramid at all (models.py:450-451); the
+    perturbed golden makes every branch visible in v.  tests/ restate this
+    helper (same generator, same order)."""
+    g = torch.Generator().manual_seed(seed)
+    with torch.no_grad():
+        for _, p in module.named_parameters():
+            if not bool(p.detach().abs().sum()):
+                p.copy_(torch.randn(p.shape, generator=g) * std)
+
+
+def hybrid_perturbed_fixture(ref: str) -> None:
+    """model_hybrid_c1_perturbed.npz: as model_hybrid_c1.npz, with the zero-init
+    parameters perturbed (perturb_zero_init_) so v depends on every branch."""
+    import models  # reference (already on sys.path from pvcnn_fixtures)
+    torch.manual_seed(1234)
+    pf = models.HybridMLP(cond_dim=129, point_dim=6)
+    perturb_zero_init_(pf)
+    pf.train()
+    g = torch.Generator().manual_seed(77)
+    x = torch.randn(2, 1024, 6, generator=g)
+    t = torch.rand(2, generator=g)
+    cond = torch.randn(2, 129, generator=g)
+    mask = torch.tensor([[1.0], [0.0]])
+    v = pf(x, t, cond, cond_drop_mask=mask)
+    target = torch.randn(2, 1024, 6, generator=g)
+    loss = torch.nn.functional.mse_loss(v, target)
+    loss.backward()
+    np.savez_compressed(
+        os.path.join(HERE, "model_hybrid_c1_perturbed.npz"), seed=1234, perturb_seed=5,
+        x=x.numpy(), t=t.numpy(), cond=cond.numpy(), mask=mask.numpy(), target=target.numpy(),
+        v=v.detach().numpy(), loss=np.float32(loss.item()), param_sums=_param_sums(pf),
+        grad_norms=np.array([p.grad.double().norm().item() if p.grad is not None else 0.0
+                             for p in pf.parameters()]))
+
+
 def main() -> None:
     ref = sys.argv[1] if len(sys.argv) > 1 else "/root/reference"
     torch.set_num_threads(1)  # deterministic CPU reductions
-    chamfer_fixtures(ref)
-    emd_fixture()
-    pvcnn_fixtures(ref)
+    only = sys.argv[2:]  # optional subset, e.g. `hybrid_perturbed`
+    if not only:
+        chamfer_fixtures(ref)
+        emd_fixture()
+        pvcnn_fixtures(ref)
+    else:
+        _install_oracle_backend()
+        sys.path.insert(0, os.path.join(ref, "third_party", "pvcnn"))
+        sys.path.insert(0, ref)
+    hybrid_perturbed_fixture(ref)
     print("wrote", sorted(f for f in os.listdir(HERE) if f.endswith(".npz")))
 
 

@@ -64,17 +64,24 @@ def test_pvconv_gpu_matches_reference(golden, report, mode):
     assert e_out < tol and e_grad < tol, (e_out, e_grad)
 
 
+@pytest.mark.parametrize("perturbed", [False, True])
 @pytest.mark.parametrize("mode", ["exact_fp32", "bf16x3"])
-def test_hybrid_gpu_matches_reference(golden, report, mode):
+def test_hybrid_gpu_matches_reference(golden, report, mode, perturbed):
     """HybridMLP (C1, fp32) vs the reference model's velocity, loss and gradient
     norms (model_hybrid_c1.npz).  exact-fp32: v and the loss within 1e-5
     (north_star), gradient norms within 1e-4; bf16x3: the measured deviation is
-    reported and bounded at 1e-4 (v, loss) / 1e-3 (gradients)."""
+    reported and bounded at 1e-4 (v, loss) / 1e-3 (gradients).  `perturbed`:
+    model_hybrid_c1_perturbed.npz, the zero-init parameters perturbed so that v
+    depends on the PVConv pyramid (at the reference's init ContextNet.head_out
+    is zero and v does not see it)."""
+    from golden_util import perturb_zero_init_
     from pcfm.models import HybridMLP
     from pcfm.precision import exact_fp32
-    g = golden("model_hybrid_c1.npz")
+    g = golden("model_hybrid_c1_perturbed.npz" if perturbed else "model_hybrid_c1.npz")
     torch.manual_seed(int(g["seed"]))
     pf = HybridMLP(cond_dim=129, point_dim=6)
+    if perturbed:
+        perturb_zero_init_(pf, int(g["perturb_seed"]))
     # same seed -> same weights (float64 sums: summation order may differ per host CPU)
     np.testing.assert_allclose(_param_sums(pf), g["param_sums"], rtol=1e-12, atol=1e-12)
     pf = pf.to(DEV).train()
@@ -92,7 +99,7 @@ def test_hybrid_gpu_matches_reference(golden, report, mode):
     live = np.array([not n.endswith(_NOISE_BIAS) for n in names])
     gdev = np.abs(norms - g["grad_norms"]) / np.maximum(g["grad_norms"], 1e-30)
     e_g = float(gdev[live].max())
-    report(f"hybrid_c1_{mode}", {"v": e_v, "loss": e_loss, "grad_norms": e_g,
+    report(f"hybrid_c1{'_perturbed' if perturbed else ''}_{mode}", {"v": e_v, "loss": e_loss, "grad_norms": e_g,
                                  "worst_grad": names[int(np.argmax(np.where(live, gdev, 0)))]})
     if mode == "exact_fp32":
         assert e_v < 1e-5 and e_loss < 1e-5 and e_g < 1e-4, (e_v, e_loss, e_g)

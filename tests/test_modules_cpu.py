@@ -70,6 +70,34 @@ def test_hybrid_matches_reference(cpu_backend, golden, film_per_point):
     np.testing.assert_allclose(norms, g["grad_norms"], rtol=2e-3, atol=1e-6)
 
 
+def test_hybrid_perturbed_matches_reference(cpu_backend, golden):
+    """model_hybrid_c1_perturbed.npz: zero-init parameters perturbed, so the
+    velocity depends on the PVConv pyramid (at the reference's init it does not)."""
+    from golden_util import perturb_zero_init_
+    from pcfm.models import HybridMLP
+    g = golden("model_hybrid_c1_perturbed.npz")
+    torch.set_num_threads(1)
+    torch.manual_seed(int(g["seed"]))
+    pf = HybridMLP(cond_dim=129, point_dim=6)
+    perturb_zero_init_(pf, int(g["perturb_seed"]))
+    np.testing.assert_allclose(_param_sums(pf), g["param_sums"], rtol=1e-12, atol=1e-12)
+    pf.train()
+    v = pf(torch.from_numpy(g["x"]), torch.from_numpy(g["t"]), torch.from_numpy(g["cond"]),
+           cond_drop_mask=torch.from_numpy(g["mask"]))
+    e_v = float((v.detach() - torch.from_numpy(g["v"])).abs().max() / np.abs(g["v"]).max())
+    assert e_v < 1e-5, e_v
+    loss = torch.nn.functional.mse_loss(v, torch.from_numpy(g["target"]))
+    assert abs(loss.item() - float(g["loss"])) < 1e-5 * abs(float(g["loss"]))
+    loss.backward()
+    names = [n for n, _ in pf.named_parameters()]
+    norms = np.array([p.grad.double().norm().item() if p.grad is not None else 0.0
+                      for p in pf.parameters()])
+    live = np.array([not n.endswith(("layers.0.bias", "voxel_layers.0.bias",
+                                     "voxel_layers.3.bias")) for n in names])
+    dev = np.abs(norms - g["grad_norms"]) / np.maximum(g["grad_norms"], 1e-30)
+    assert dev[live].max() < 1e-4, names[int(np.argmax(np.where(live, dev, 0)))]
+
+
 def test_product_ops_check_arguments_on_cpu():
     """CPU tensors run the pure-PyTorch backend, with the reference's argument
     checks (utils.hpp:7-18 -> RuntimeError); PointNet++-only ops stay out."""
