@@ -4,9 +4,10 @@
 // The reference runs a <<<(32,16),512>>> grid per direction in which only
 // B*16 blocks work, with 512-point LDS tiles read by every thread.  Here:
 //   * both directions are one launch (grid.z = 2*B);
-//   * each lane owns Q query points in registers; the candidate loop is
-//     wave-uniform, so candidates arrive through scalar loads and every VALU
-//     op reads them straight from SGPRs (no LDS, no per-lane address math);
+//   * each lane owns Q = 8 query points in registers, paired into packed-fp32
+//     operands; the candidate loop is wave-uniform, so candidates arrive
+//     through scalar loads and every VALU op reads them straight from SGPRs
+//     (no LDS, no per-lane address math);
 //   * when B*N queries alone cannot fill 256 CUs the candidate range is split
 //     and the per-split winners merge through a 64-bit atomicMin on
 //     (float bits of d) << 32 | index.  d >= 0, so the packed order is exactly
@@ -20,15 +21,20 @@
 namespace pcfm {
 namespace {
 
-constexpr int kQ = 4;          // queries per lane
+constexpr int kQ = 8;          // queries per lane (4 packed pairs)
 constexpr int kThreads = 256;  // 4 waves
 constexpr int kPerBlock = kQ * kThreads;
+
+typedef float f2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ unsigned long long pack_key(float d, int idx) {
   return ((unsigned long long)__float_as_uint(d) << 32) | (unsigned)idx;
 }
 
-// grid = (query blocks, splits, 2*b).
+// grid = (query blocks, splits, 2*b).  Two queries share each packed-fp32
+// instruction (v_pk_add_f32 / v_pk_mul_f32 / v_pk_fma_f32): the distance costs
+// 6 packed ops per 2 pairs, the same per-component fma chain as sqdist3 (so
+// the same bits as the oracle), leaving the compare / select per pair.
 __global__ void __launch_bounds__(kThreads)
     nn_kernel(const float* __restrict__ xyz1, const float* __restrict__ xyz2, int b, int n, int m,
               int splits, float* __restrict__ dist1, int* __restrict__ idx1,
@@ -46,34 +52,59 @@ __global__ void __launch_bounds__(kThreads)
   const int k0 = (int)(((long long)nc * s) / splits);
   const int k1 = (int)(((long long)nc * (s + 1)) / splits);
 
-  float qx[kQ], qy[kQ], qz[kQ], best[kQ];
+  constexpr int kP = kQ / 2;
+  f2 qx[kP], qy[kP], qz[kP];
+  float best[kQ];
   int bi[kQ];
 #pragma unroll
   for (int q = 0; q < kQ; ++q) {
     const int j = qbase + q * kThreads + threadIdx.x;
     const int jj = j < nq ? j : nq - 1;
     const float* p = qp + ((size_t)bb * nq + jj) * 3;
-    qx[q] = p[0];
-    qy[q] = p[1];
-    qz[q] = p[2];
+    qx[q >> 1][q & 1] = p[0];
+    qy[q >> 1][q & 1] = p[1];
+    qz[q >> 1][q & 1] = p[2];
     best[q] = __builtin_inff();
     bi[q] = k0;
   }
   const float* __restrict__ cb = cp + (size_t)bb * nc * 3;
-#pragma unroll 4
-  for (int k = k0; k < k1; ++k) {
-    const float cx = cb[3 * k + 0];
-    const float cy = cb[3 * k + 1];
-    const float cz = cb[3 * k + 2];
+  // one candidate: the same fma chain as sqdist3 on two queries at once
+  auto visit = [&](float x, float y, float z, int k) {
+    const f2 cx = x, cy = y, cz = z;
 #pragma unroll
-    for (int q = 0; q < kQ; ++q) {
-      const float d = sqdist3(cx - qx[q], cy - qy[q], cz - qz[q]);
-      if (d < best[q]) {
-        best[q] = d;
-        bi[q] = k;
+    for (int p = 0; p < kP; ++p) {
+      // dx = candidate - query (chamfer3D.cu:32-35); fma(dz, dz, fma(dx, dx, dy * dy))
+      const f2 dx = cx - qx[p], dy = cy - qy[p], dz = cz - qz[p];
+      const f2 d = __builtin_elementwise_fma(dz, dz, __builtin_elementwise_fma(dx, dx, dy * dy));
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        if (d[h] < best[2 * p + h]) {
+          best[2 * p + h] = d[h];
+          bi[2 * p + h] = k;
+        }
       }
     }
+  };
+  // groups of kG candidates through wide scalar loads (uniform address), the
+  // next group's loads issued before the current group's arithmetic
+  constexpr int kG = 8;
+  const int kg1 = k0 + (k1 - k0) / kG * kG;
+  int k = __builtin_amdgcn_readfirstlane(k0);
+  if (k < kg1) {
+    float c[3 * kG], nx[3 * kG];
+#pragma unroll
+    for (int e = 0; e < 3 * kG; ++e) c[e] = cb[3 * k + e];
+    for (; k < kg1; k += kG) {
+      const int kn = k + kG < kg1 ? k + kG : k;
+#pragma unroll
+      for (int e = 0; e < 3 * kG; ++e) nx[e] = cb[3 * kn + e];
+#pragma unroll
+      for (int g = 0; g < kG; ++g) visit(c[3 * g], c[3 * g + 1], c[3 * g + 2], k + g);
+#pragma unroll
+      for (int e = 0; e < 3 * kG; ++e) c[e] = nx[e];
+    }
   }
+  for (; k < k1; ++k) visit(cb[3 * k], cb[3 * k + 1], cb[3 * k + 2], k);
   float* __restrict__ dist = dir ? dist2 : dist1;
   int* __restrict__ idx = dir ? idx2 : idx1;
   unsigned long long* __restrict__ key = dir ? key2 : key1;

@@ -8,16 +8,27 @@
 namespace pcfm {
 namespace {
 
-// One lane per center; the point scan is wave-uniform (the same point k for
-// all 64 lanes), so the three coordinates come in through scalar loads and the
-// wave leaves the scan as soon as every lane holds u hits.  Hits are written
-// in index order; unfilled slots repeat the first hit (ball_query.cu:40-45) or
-// stay zero when there is none (the reference's torch::zeros output).
-__global__ void __launch_bounds__(256)
+// One WAVE per center, 64 candidate points per step (lane = point): the hits
+// of a step come out of one ballot, in index order, so the first u hits of the
+// reference's sequential scan (ball_query.cu:33-47) are the first u set bits
+// seen; the wave leaves as soon as it holds u.  The candidates stream through
+// an LDS tile shared by the block's 16 waves (16 centers): each tile is read
+// from global memory once per block instead of once per center, and a block
+// stops loading tiles when all its centers are full (__syncthreads_count).
+// Unfilled slots repeat the first hit (:40-45) or stay zero when there is none
+// (the reference's torch::zeros output).  Distances: sqdist3 (dx = center -
+// point), strict d2 < r2, as the oracle.
+constexpr int kBQWaves = 16;      // centers per block
+constexpr int kBQTile = 2048;     // candidate points per LDS tile (24 KiB)
+
+__global__ void __launch_bounds__(kBQWaves * 64)
     ball_query_kernel(const float* __restrict__ centers, const float* __restrict__ points,
                       int m, int n, float r2, int u, int* __restrict__ out) {
+  __shared__ float sx[kBQTile], sy[kBQTile], sz[kBQTile];
   const int b = blockIdx.y;
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int j = blockIdx.x * kBQWaves + w;
   const bool active = j < m;
   const float* cb = centers + (size_t)b * 3 * m;
   const float* __restrict__ pb = points + (size_t)b * 3 * n;
@@ -26,26 +37,36 @@ __global__ void __launch_bounds__(256)
   const float cz = active ? cb[j + 2 * m] : 0.0f;
   int* o = out + ((size_t)b * m + (active ? j : 0)) * u;
   int cnt = 0, first = 0;
-  bool open = active && u > 0;
-  for (int k0 = 0; k0 < n; k0 += 64) {
-    if (!__any(open)) break;
-    const int kend = min(n, k0 + 64);
-    for (int k = k0; k < kend; ++k) {
-      const float dx = cx - pb[k];
-      const float dy = cy - pb[k + n];
-      const float dz = cz - pb[k + 2 * n];
-      const float d2 = sqdist3(dx, dy, dz);
-      if (open && d2 < r2) {
-        if (cnt == 0) first = k;
-        o[cnt] = k;
-        ++cnt;
+  bool open = active;
+  for (int k0 = 0; k0 < n; k0 += kBQTile) {
+    if (__syncthreads_count(open ? 1 : 0) == 0) break;  // every center of the block is full
+    const int len = min(kBQTile, n - k0);
+    for (int e = threadIdx.x; e < len; e += kBQWaves * 64) {
+      sx[e] = pb[k0 + e];
+      sy[e] = pb[(size_t)n + k0 + e];
+      sz[e] = pb[(size_t)2 * n + k0 + e];
+    }
+    __syncthreads();
+    for (int c0 = 0; open && c0 < len; c0 += 64) {
+      const int e = c0 + lane;
+      bool hit = false;
+      if (e < len) {
+        const float d2 = sqdist3(cx - sx[e], cy - sy[e], cz - sz[e]);
+        hit = d2 < r2;
+      }
+      const unsigned long long bal = __ballot(hit);
+      if (bal) {
+        if (cnt == 0) first = k0 + c0 + __ffsll((long long)bal) - 1;
+        const int pos = cnt + __popcll(bal & ((1ull << lane) - 1ull));
+        if (hit && pos < u) o[pos] = k0 + e;
+        cnt += __popcll(bal);
         open = cnt < u;
       }
     }
   }
   if (active) {
     const int fill = cnt > 0 ? first : 0;
-    for (int v = cnt; v < u; ++v) o[v] = fill;
+    for (int v = min(cnt, u) + lane; v < u; v += 64) o[v] = fill;
   }
 }
 
@@ -59,9 +80,9 @@ extern "C" int pcfm_ball_query(const float* centers, const float* points, int b,
   PCFM_CHECK_ARG(b >= 0 && m >= 0 && n >= 0 && u >= 0, "ball_query: negative size");
   if (b == 0 || m == 0 || u == 0) return PCFM_OK;
   const float r2 = radius * radius;  // host float product, as ball_query.cpp:25
-  dim3 grid(ceil_div(m, 256), b);
-  hipLaunchKernelGGL(ball_query_kernel, grid, dim3(256), 0, (hipStream_t)stream, centers, points,
-                     m, n, r2, u, idx);
+  dim3 grid(ceil_div(m, kBQWaves), b);
+  hipLaunchKernelGGL(ball_query_kernel, grid, dim3(kBQWaves * 64), 0, (hipStream_t)stream, centers,
+                     points, m, n, r2, u, idx);
   return check_launch("ball_query");
 }
 

@@ -7,9 +7,9 @@
 // instruction (measured, tools/voxel_probe.py), so the scatters are recast as
 // gathers over items sorted by their target cell:
 //
-//   1. seg_sort     counting sort, one block per batch element, histogram in
-//                   LDS: start[b, 0..V] and rank[b, i] (sorted position of
-//                   item i; written coalesced, in item order)
+//   1. seg_sort     stable counting sort, up to 16 blocks per batch element,
+//                   per-wave histograms in LDS: start[b, 0..V] and rank[b, i]
+//                   (sorted position of item i, item order kept inside a key)
 //   2. seg_units    tiles of kTV voxels -> balanced work units (device-built)
 //   3. seg_rows     xs[b, rank[i], :] = in[b, :, i]: channels-last rows in
 //                   SORTED order, plus the item's key and tap weights at the
@@ -23,9 +23,9 @@
 // Used by avg_voxelize forward (key = voxel, term = feat * (1/cnt)),
 // trilinear devoxelize backward (key = base cell inds[b,0,:], term = wgt * g
 // for the 8 corners) and grouping backward (key = neighbour index, term = g).
-// The order of items inside one key comes from the sort's LDS atomics, so
-// float sums are order-nondeterministic at the last bit -- exactly like the
-// reference's float atomics.
+// The sort is stable (items inside one key keep their index order) and every
+// float sum runs in a fixed order, so the scatters are deterministic -- unlike
+// the reference's float atomics.
 #pragma once
 
 #include <algorithm>
@@ -36,21 +36,33 @@ namespace pcfm {
 namespace {  // kernels get internal linkage: this header is included by several .hip files
 
 // --------------------------------------------------------------------------
-// 1: counting sort by key.  Block (p, b) owns the key range [p, p+1) * span of
-// batch element b (grid = (P, B), 1024 threads): every block reads all n keys
-// of its batch element (L2-resident, 80 KB at N = 20000), counts the keys
-// BELOW its range itself -- its base in the sorted order, so the P blocks never
-// wait for each other -- and histograms / ranks its own keys in LDS
-// (kSortKeys ints = 128 KiB; a wider range takes several passes).  One block
-// per batch element left 248 of 256 CUs idle for the ~23 us of the sort.
+// 1: STABLE counting sort by key.  Block (p, b) owns the key range [p, p+1) *
+// span of batch element b (grid = (P, B), 1024 threads = 16 waves): every block
+// reads all n keys of its batch element (L2-resident, 80 KB at N = 20000) and
+// counts the keys BELOW its range itself -- its base in the sorted order, so
+// the P blocks never wait for each other.  Keys are handled in chunks of
+// kSortChunk (a wider range takes several passes).  Wave w owns the item
+// segment [w n / 16, (w+1) n / 16) and keeps its own per-key counts in LDS:
+//   A  count:  per-wave histograms of the chunk (LDS int atomics; counts are
+//              order-free);
+//   B  scan:   per key the exclusive prefix over keys (-> start) and over the
+//              waves (-> each wave's first rank of that key);
+//   C  rank:   each wave walks its segment in index order, 64 items per step;
+//              the items of one step that share a key are ranked by lane
+//              (ballot + popcount), and only the owning wave advances its
+//              counter -- so rank[i] = start[key_i] + #{j < i : key_j = key_i}:
+//              the order inside a key is the item order, independent of
+//              scheduling.  Every float sum downstream (unit gathers, partial
+//              tiles) then runs in a fixed order: the scatters are
+//              deterministic (the reference's float atomics are not).
 //   start[b, 0..V]  exclusive prefix of the counts (start[b, V] = total)
 //   cnt_out[b, v]   the counts (optional: the voxelization's `cnt` output)
 //   vinv[b, v]      (float)(1.0 / (double)cnt) (optional, vox.cu:66)
-//   rank[b, i]      start[key_i] + arrival rank within the key; -1 when the
-//                   key is outside [0, V) (the item contributes nothing)
+//   rank[b, i]      start[key_i] + rank within the key; -1 when the key is
+//                   outside [0, V) (the item contributes nothing)
 // --------------------------------------------------------------------------
-constexpr int kSortKeys = 32768;
-constexpr int kSortBatch = 8;     // keys per thread in flight
+constexpr int kSortWaves = 16;
+constexpr int kSortChunk = 2048;   // keys per pass: 16 waves x 2048 ints = 128 KiB of LDS
 constexpr int kSortMinSpan = 256;  // keys per block at least
 constexpr int kSortMaxParts = 16;  // blocks per batch element at most
 
@@ -58,37 +70,38 @@ inline int seg_sort_parts(int V) {
   return std::max(1, std::min(kSortMaxParts, V / kSortMinSpan));
 }
 inline int seg_sort_span(int V) { return (V + seg_sort_parts(V) - 1) / seg_sort_parts(V); }
+inline size_t seg_sort_lds(int V) {
+  return (size_t)kSortWaves * std::min(seg_sort_span(V), kSortChunk) * sizeof(int);
+}
 
 __global__ void __launch_bounds__(1024)
     seg_sort_kernel(const int* __restrict__ key, long long key_bstride, int n, int V, int span,
                     int* __restrict__ start, int* __restrict__ cnt_out, float* __restrict__ vinv,
                     int* __restrict__ rank) {
-  extern __shared__ int hist[];  // [min(span, kSortKeys)]
-  __shared__ int wsum[16];
+  extern __shared__ int hw[];  // [kSortWaves][len]
+  __shared__ int wsum[kSortWaves];
   const int p = blockIdx.x, b = blockIdx.y;
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   const int* __restrict__ kb = key + (size_t)b * key_bstride;
   int* __restrict__ sb = start + (size_t)b * (V + 1);
   int* __restrict__ rb = rank + (size_t)b * n;
   const int pk0 = min(V, p * span), pk1 = min(V, pk0 + span);
+  const int i_lo = (int)((long long)n * w / kSortWaves);
+  const int i_hi = (int)((long long)n * (w + 1) / kSortWaves);
+  const unsigned long long lt = (1ull << lane) - 1ull;
   int carry = 0;
-  for (int k0 = pk0; k0 < pk1; k0 += kSortKeys) {
-    const int len = min(kSortKeys, pk1 - k0);
-    for (int e = t; e < len; e += 1024) hist[e] = 0;
+  for (int k0 = pk0; k0 < pk1; k0 += kSortChunk) {
+    const int len = min(kSortChunk, pk1 - k0);
+    for (int e = t; e < kSortWaves * len; e += 1024) hw[e] = 0;
     __syncthreads();
-    int below = 0;  // first chunk: keys in [0, pk0) -> this block's base
-    for (int i0 = 0; i0 < n; i0 += 1024 * kSortBatch) {
-      int kk[kSortBatch];  // keys first (independent loads), then the LDS atomics
-#pragma unroll
-      for (int q = 0; q < kSortBatch; ++q) {
-        const int i = i0 + q * 1024 + t;
-        kk[q] = i < n ? kb[i] : -1;
-      }
-#pragma unroll
-      for (int q = 0; q < kSortBatch; ++q) {
-        if ((unsigned)(kk[q] - k0) < (unsigned)len) atomicAdd(hist + (kk[q] - k0), 1);
-        below += (k0 == pk0 && (unsigned)kk[q] < (unsigned)pk0) ? 1 : 0;
-      }
+    // A: per-wave counts (+ the keys below the block's range: its base)
+    int* hmine = hw + w * len;
+    int below = 0;
+    for (int i = i_lo + lane; i < i_hi; i += 64) {
+      const int k = kb[i];
+      if ((unsigned)(k - k0) < (unsigned)len) atomicAdd(hmine + (k - k0), 1);
+      below += (k0 == pk0 && (unsigned)k < (unsigned)pk0) ? 1 : 0;
     }
     if (k0 == pk0) {
 #pragma unroll
@@ -98,28 +111,35 @@ __global__ void __launch_bounds__(1024)
     __syncthreads();
     if (k0 == pk0) {
 #pragma unroll
-      for (int g = 0; g < 16; ++g) carry += wsum[g];
+      for (int g = 0; g < kSortWaves; ++g) carry += wsum[g];
     }
     __syncthreads();
-    // exclusive scan: wave w owns the 64-aligned segment [lo, hi)
-    const int seg = ((len + 15) / 16 + 63) & ~63;
+    // B: wave w owns the 64-aligned key segment [lo, hi)
+    const int seg = ((len + kSortWaves - 1) / kSortWaves + 63) & ~63;
     const int lo = min(len, w * seg), hi = min(len, lo + seg);
     int part = 0;
-    for (int e = lo + lane; e < hi; e += 64) part += hist[e];
+    for (int e = lo + lane; e < hi; e += 64) {
+#pragma unroll
+      for (int g = 0; g < kSortWaves; ++g) part += hw[g * len + e];
+    }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
     if (lane == 0) wsum[w] = part;
     __syncthreads();
     int run = carry, total = 0;
 #pragma unroll
-    for (int g = 0; g < 16; ++g) {
+    for (int g = 0; g < kSortWaves; ++g) {
       const int x = wsum[g];
       run += g < w ? x : 0;
       total += x;
     }
     for (int e0 = lo; e0 < hi; e0 += 64) {
       const int e = e0 + lane;
-      const int c = e < hi ? hist[e] : 0;
+      int c = 0;
+      if (e < hi) {
+#pragma unroll
+        for (int g = 0; g < kSortWaves; ++g) c += hw[g * len + e];
+      }
       int x = c;
 #pragma unroll
       for (int o = 1; o < 64; o <<= 1) {
@@ -127,28 +147,37 @@ __global__ void __launch_bounds__(1024)
         if (lane >= o) x += y;
       }
       if (e < hi) {
-        const int pos = run + x - c;
-        hist[e] = pos;
+        int pos = run + x - c;
         sb[k0 + e] = pos;
         if (cnt_out != nullptr) cnt_out[(size_t)b * V + k0 + e] = c;
         if (vinv != nullptr) vinv[(size_t)b * V + k0 + e] = c > 0 ? (float)(1.0 / (double)c) : 0.0f;
+#pragma unroll
+        for (int g = 0; g < kSortWaves; ++g) {  // first rank of key e for wave g
+          const int cg = hw[g * len + e];
+          hw[g * len + e] = pos;
+          pos += cg;
+        }
       }
       run += __shfl(x, 63, 64);
     }
     __syncthreads();
-    for (int i0 = 0; i0 < n; i0 += 1024 * kSortBatch) {
-      int kk[kSortBatch];
-#pragma unroll
-      for (int q = 0; q < kSortBatch; ++q) {
-        const int i = i0 + q * 1024 + t;
-        kk[q] = i < n ? kb[i] : -1;
+    // C: ranks in item order (only wave w touches its counters)
+    for (int i0 = i_lo; i0 < i_hi; i0 += 64) {
+      const int i = i0 + lane;
+      const int k = i < i_hi ? kb[i] : -1;
+      const bool inr = i < i_hi && (unsigned)(k - k0) < (unsigned)len;
+      unsigned long long act = __ballot(inr);
+      while (act) {
+        const int leader = __ffsll((long long)act) - 1;
+        const int kk = __builtin_amdgcn_readlane(k, leader);
+        const bool mine = inr && k == kk;
+        const unsigned long long m = __ballot(mine);
+        const int base = hmine[kk - k0];  // same address for every lane: broadcast
+        if (mine) rb[i] = base + __popcll(m & lt);
+        if (lane == leader) hmine[kk - k0] = base + __popcll(m);
+        act &= ~m;
       }
-#pragma unroll
-      for (int q = 0; q < kSortBatch; ++q) {
-        const int i = i0 + q * 1024 + t;
-        if ((unsigned)(kk[q] - k0) < (unsigned)len) rb[i] = atomicAdd(hist + (kk[q] - k0), 1);
-        else if (p == 0 && k0 == pk0 && i < n && (unsigned)kk[q] >= (unsigned)V) rb[i] = -1;
-      }
+      if (p == 0 && k0 == pk0 && i < i_hi && (unsigned)k >= (unsigned)V) rb[i] = -1;
     }
     carry += total;
     __syncthreads();
@@ -624,7 +653,7 @@ inline int seg_scatter(const float* in, const int* key, long long key_bstride, b
   if (B == 0 || V == 0) return PCFM_OK;
   SegWs w = seg_ws_carve(ws, B, C, n, V, TAPS);
   const int span = seg_sort_span(V);
-  const size_t sort_lds = (size_t)std::min(span, kSortKeys) * sizeof(int);
+  const size_t sort_lds = seg_sort_lds(V);
   int e = allow_big_lds((const void*)seg_sort_kernel);
   if (e) return e;
   hipLaunchKernelGGL(seg_sort_kernel, dim3(seg_sort_parts(V), B), dim3(1024), sort_lds, st, key,

@@ -28,14 +28,19 @@ bool cube_fits(int r, int* s) {
 }
 
 // out[r] = scale * sum_v a[r][v] * (b ? b[r][v] : 1): one block per row,
-// fixed per-thread order + tree, deterministic.
+// fixed per-thread order + tree, deterministic.  Accumulated in fp64 (the
+// products of two floats are exact in fp64): SE3d's channel mean and its scale
+// gradient sum_v grid * g cancel heavily, and an fp32 sum over R^3 voxels
+// would carry its rounding times that cancellation into the SE weights'
+// gradients.  The row is read once either way (HBM-bound, the fp64 adds are
+// free beside the loads).
 __global__ void __launch_bounds__(256)
     rows_dot_kernel(const float* __restrict__ a, const float* __restrict__ b, int len, float scale,
                     float* __restrict__ out) {
   const size_t r = blockIdx.x;
   const float* ar = a + r * len;
   const float* br = b != nullptr ? b + r * len : nullptr;
-  float acc = 0.0f;
+  double acc = 0.0;
   if ((len & 3) == 0) {
     const float4* a4 = reinterpret_cast<const float4*>(ar);
     const float4* b4 = reinterpret_cast<const float4*>(br);
@@ -43,26 +48,26 @@ __global__ void __launch_bounds__(256)
       const float4 x = a4[v];
       if (br != nullptr) {
         const float4 y = b4[v];
-        acc = __builtin_fmaf(x.x, y.x, acc);
-        acc = __builtin_fmaf(x.y, y.y, acc);
-        acc = __builtin_fmaf(x.z, y.z, acc);
-        acc = __builtin_fmaf(x.w, y.w, acc);
+        acc = __builtin_fma((double)x.x, (double)y.x, acc);
+        acc = __builtin_fma((double)x.y, (double)y.y, acc);
+        acc = __builtin_fma((double)x.z, (double)y.z, acc);
+        acc = __builtin_fma((double)x.w, (double)y.w, acc);
       } else {
-        acc += (x.x + x.y) + (x.z + x.w);
+        acc += ((double)x.x + (double)x.y) + ((double)x.z + (double)x.w);
       }
     }
   } else {
     for (int v = threadIdx.x; v < len; v += 256)
-      acc = br != nullptr ? __builtin_fmaf(ar[v], br[v], acc) : acc + ar[v];
+      acc = br != nullptr ? __builtin_fma((double)ar[v], (double)br[v], acc) : acc + (double)ar[v];
   }
-  __shared__ float red[256];
+  __shared__ double red[256];
   red[threadIdx.x] = acc;
   __syncthreads();
   for (int o = 128; o > 0; o >>= 1) {
     if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
     __syncthreads();
   }
-  if (threadIdx.x == 0) out[r] = red[0] * scale;
+  if (threadIdx.x == 0) out[r] = (float)(red[0] * (double)scale);
 }
 
 // x[r][v] = s[r] * x[r][v] + t[r]  (in place; t may be null)
