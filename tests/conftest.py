@@ -18,6 +18,9 @@ GOLDEN = os.path.join(REPO, "tests", "golden")
 for p in (REPO, PKG):
     if p not in sys.path:
         sys.path.insert(0, p)
+# Chamfer: take the culled search from 16M pairs per batch element in tests (the
+# product default is 2^31), so test-sized clouds exercise both search paths
+os.environ.setdefault("PCFM_CHAMFER_CULL_PAIRS", str(16 << 20))
 
 
 def pytest_configure(config):

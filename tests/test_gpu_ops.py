@@ -262,6 +262,43 @@ def test_chamfer_vs_oracle(b, n, m):
         np.testing.assert_allclose(np_(g2), e2, rtol=1e-5, atol=1e-5)
 
 
+@pytest.mark.parametrize("case", ["randn", "ties", "clusters", "degenerate", "uneven"])
+def test_chamfer_culled_bit_exact(case):
+    """The Morton-sorted tile-culled search (forced on with
+    PCFM_CHAMFER_CULL_PAIRS, set for the whole GPU test session in conftest)
+    must return the brute-force answer -- every distance and index equal to
+    the oracle's full scan, lowest index on ties."""
+    import os
+    assert os.environ.get("PCFM_CHAMFER_CULL_PAIRS") == str(16 << 20)
+    from pcfm import ops
+    g = rng(hash(case) % 1000)
+    b, n, m = 2, 4500, 4000
+    if case == "uneven":
+        n, m = 300, 60000
+    a = g.standard_normal((b, n, 3)).astype(np.float32)
+    c = g.standard_normal((b, m, 3)).astype(np.float32)
+    if case == "ties":  # exact duplicates at several indices, queries on points
+        c[:, 1000:1500] = c[:, :500]
+        c[:, 3000:3100] = c[:, :100]
+        a[:, :700] = c[:, 800:1500]
+    elif case == "clusters":
+        a = (g.integers(0, 4, (b, n, 1)) * 10.0 + 0.01 * g.standard_normal((b, n, 3))).astype(
+            np.float32)
+        c = (g.integers(0, 4, (b, m, 1)) * 10.0 + 0.01 * g.standard_normal((b, m, 3))).astype(
+            np.float32)
+    elif case == "degenerate":  # one point repeated: zero extent, every distance tied
+        a[:] = 0.5
+        c[:] = 0.5
+    d1 = torch.empty(b, n, device=DEV)
+    d2 = torch.empty(b, m, device=DEV)
+    i1 = torch.empty(b, n, dtype=torch.int32, device=DEV)
+    i2 = torch.empty(b, m, dtype=torch.int32, device=DEV)
+    assert ops.chamfer_3D.forward(cu(a), cu(c), d1, d2, i1, i2) == 1
+    e = O.chamfer_fwd(a, c)
+    for got, exp in zip((d1, d2, i1, i2), e):
+        np.testing.assert_array_equal(np_(got), exp)
+
+
 def test_chamfer_full_size_sampled():
     """C2 size (B=8, N=M=20000): a sample of queries checked bit-exactly against
     the oracle run on the full candidate cloud."""
