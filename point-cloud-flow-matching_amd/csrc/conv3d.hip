@@ -443,7 +443,12 @@ __global__ void __launch_bounds__(512)
       const int x = bxyz[q] & 1023, yy = (bxyz[q] >> 10) & 1023, z = bxyz[q] >> 20;
       const bool inb = (unsigned)(x + dx) < (unsigned)R && (unsigned)(yy + dy) < (unsigned)R &&
                        (unsigned)(z + dz) < (unsigned)R;
-      glds16(inb ? bbase[q] + bofs : zbase[q],
+      // branch-free select of the source row (a divergent ?: on the pointer
+      // compiled to an exec-mask branch around every piece)
+      const unsigned long long src = (unsigned long long)(bbase[q] + bofs);
+      const unsigned long long zsrc = (unsigned long long)zbase[q];
+      const unsigned long long msk = 0ull - (unsigned long long)inb;
+      glds16((const void*)((src & msk) | (zsrc & ~msk)),
              base + 2 * G::A + (I / G::BPI) * G::B + (I % G::BPI) * 1024);
     }
   };
@@ -478,6 +483,32 @@ __global__ void __launch_bounds__(512)
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's stage-s reads done
     __builtin_amdgcn_s_barrier();
+#ifndef PCFM_CONV_DMA_LATE
+#define PCFM_CONV_DMA_LATE 3  // MFMAs per LDS-DMA piece; 0: the burst after the barrier
+#endif
+#if PCFM_CONV_DMA_LATE > 0
+    // LDS-DMA issue (~60-185 cycles per piece) between the MFMAs instead of in
+    // a burst after the barrier, where both waves of a SIMD issue theirs at the
+    // same time and the MFMA pipe idles: 0.711 -> 0.694 ms (C128 R32 fwd),
+    // 0.368 -> 0.357 ms (C256 R16), tools/conv_ab.py on MI355X
+    glds_frags<KT>(lds, (s + 1) % kGStages, wr, wc, r, h, Fn);
+    glds_mfma<KT>(Fc, acc);
+    // unconditional (same basic block as the MFMAs, so the scheduler can place
+    // the pieces between them): past the last step it reloads the final
+    // step's data into the buffer step s just drained (never read again)
+    issue(min(s + 3, nsteps - 1), s % kGStages);
+#pragma unroll
+    for (int g = 0; g < 4 * (KT / 16); ++g) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+    }
+#pragma unroll
+    for (int g = 0; g < G::APW + G::BPW; ++g) {
+      __builtin_amdgcn_sched_group_barrier(0x008, PCFM_CONV_DMA_LATE, 0);
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 8 * (KT / 16), 0);
+#else
 #ifndef PCFM_EXP_NOLOAD
     if (s + 3 < nsteps) issue(s + 3, s % kGStages);
 #endif
@@ -491,6 +522,7 @@ __global__ void __launch_bounds__(512)
       __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
     }
     __builtin_amdgcn_sched_group_barrier(0x008, 12 * (KT / 16) - 4 * (KT / 16), 0);
+#endif
   };
   int s = 0;
   for (; s + 2 < nsteps; s += 2) {
@@ -503,6 +535,9 @@ __global__ void __launch_bounds__(512)
   } else {
     glds_mfma<KT>(F0, acc);
   }
+  // the interleaved schedule issues (redundant) pieces in the last steps too:
+  // none may still be writing LDS when the wave ends
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #else
   issue(0, 0);
   if (nsteps > 1) issue(1, 1);

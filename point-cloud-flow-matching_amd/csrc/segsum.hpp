@@ -33,6 +33,16 @@
 #include "pcfm_common.hpp"
 
 namespace pcfm {
+
+inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+// Step 1 for the scatters: the stable radix sort of sort.hip (rocPRIM).  Same
+// outputs as seg_sort_kernel (start, cnt_out, vinv, rank), workspace from
+// seg_sort_stable_ws.
+size_t seg_sort_stable_ws(int B, int n, int V);
+int seg_sort_stable(const int* key, long long key_bstride, int B, int n, int V, int* start,
+                    int* cnt_out, float* vinv, int* rank, void* ws, hipStream_t st);
+
 namespace {  // kernels get internal linkage: this header is included by several .hip files
 
 // --------------------------------------------------------------------------
@@ -48,9 +58,9 @@ namespace {  // kernels get internal linkage: this header is included by several
 //   B  scan:   per key the exclusive prefix over keys (-> start) and over the
 //              waves (-> each wave's first rank of that key);
 //   C  rank:   each wave walks its segment in index order, 64 items per step;
-//              the items of one step that share a key are ranked by lane
-//              (ballot + popcount), and only the owning wave advances its
-//              counter -- so rank[i] = start[key_i] + #{j < i : key_j = key_i}:
+//              the items of one step that share a key are ranked by lane, and
+//              only the owning wave advances its counters -- so
+//              rank[i] = start[key_i] + #{j < i : key_j = key_i}:
 //              the order inside a key is the item order, independent of
 //              scheduling.  Every float sum downstream (unit gathers, partial
 //              tiles) then runs in a fixed order: the scatters are
@@ -63,7 +73,11 @@ namespace {  // kernels get internal linkage: this header is included by several
 // --------------------------------------------------------------------------
 constexpr int kSortWaves = 16;
 constexpr int kSortChunk = 2048;   // keys per pass: 16 waves x 2048 ints = 128 KiB of LDS
-constexpr int kSortMinSpan = 256;  // keys per block at least
+constexpr int kSortBatch = 8;      // 64-item key loads per wave in flight
+#ifndef PCFM_SORT_MIN_SPAN
+#define PCFM_SORT_MIN_SPAN 32
+#endif
+constexpr int kSortMinSpan = PCFM_SORT_MIN_SPAN;  // keys per block at least
 constexpr int kSortMaxParts = 16;  // blocks per batch element at most
 
 inline int seg_sort_parts(int V) {
@@ -89,7 +103,6 @@ __global__ void __launch_bounds__(1024)
   const int pk0 = min(V, p * span), pk1 = min(V, pk0 + span);
   const int i_lo = (int)((long long)n * w / kSortWaves);
   const int i_hi = (int)((long long)n * (w + 1) / kSortWaves);
-  const unsigned long long lt = (1ull << lane) - 1ull;
   int carry = 0;
   for (int k0 = pk0; k0 < pk1; k0 += kSortChunk) {
     const int len = min(kSortChunk, pk1 - k0);
@@ -98,10 +111,20 @@ __global__ void __launch_bounds__(1024)
     // A: per-wave counts (+ the keys below the block's range: its base)
     int* hmine = hw + w * len;
     int below = 0;
-    for (int i = i_lo + lane; i < i_hi; i += 64) {
-      const int k = kb[i];
-      if ((unsigned)(k - k0) < (unsigned)len) atomicAdd(hmine + (k - k0), 1);
-      below += (k0 == pk0 && (unsigned)k < (unsigned)pk0) ? 1 : 0;
+    for (int i0 = i_lo; i0 < i_hi; i0 += 64 * kSortBatch) {
+      int kk[kSortBatch];  // keys first (independent loads in flight), then the atomics
+#pragma unroll
+      for (int q = 0; q < kSortBatch; ++q) {
+        const int i = i0 + 64 * q + lane;
+        kk[q] = i < i_hi ? kb[i] : -1;
+      }
+#pragma unroll
+      for (int q = 0; q < kSortBatch; ++q) {
+#ifndef PCFM_SORT_SKIP_A
+        if ((unsigned)(kk[q] - k0) < (unsigned)len) atomicAdd(hmine + (kk[q] - k0), 1);
+#endif
+        below += (k0 == pk0 && (unsigned)kk[q] < (unsigned)pk0) ? 1 : 0;
+      }
     }
     if (k0 == pk0) {
 #pragma unroll
@@ -162,22 +185,42 @@ __global__ void __launch_bounds__(1024)
     }
     __syncthreads();
     // C: ranks in item order (only wave w touches its counters)
-    for (int i0 = i_lo; i0 < i_hi; i0 += 64) {
-      const int i = i0 + lane;
-      const int k = i < i_hi ? kb[i] : -1;
-      const bool inr = i < i_hi && (unsigned)(k - k0) < (unsigned)len;
-      unsigned long long act = __ballot(inr);
-      while (act) {
-        const int leader = __ffsll((long long)act) - 1;
-        const int kk = __builtin_amdgcn_readlane(k, leader);
-        const bool mine = inr && k == kk;
-        const unsigned long long m = __ballot(mine);
-        const int base = hmine[kk - k0];  // same address for every lane: broadcast
-        if (mine) rb[i] = base + __popcll(m & lt);
-        if (lane == leader) hmine[kk - k0] = base + __popcll(m);
-        act &= ~m;
+    const int nbits = len > 1 ? 32 - __clz(len - 1) : 0;
+    for (int j0 = i_lo; j0 < i_hi; j0 += 64 * kSortBatch) {
+      int kq[kSortBatch];
+#pragma unroll
+      for (int q = 0; q < kSortBatch; ++q) {
+        const int i = j0 + 64 * q + lane;
+        kq[q] = i < i_hi ? kb[i] : -1;
       }
-      if (p == 0 && k0 == pk0 && i < i_hi && (unsigned)k >= (unsigned)V) rb[i] = -1;
+#pragma unroll
+      for (int q = 0; q < kSortBatch; ++q) {
+        const int i = j0 + 64 * q + lane;
+        const int k = kq[q];
+        const bool inr = i < i_hi && (unsigned)(k - k0) < (unsigned)len;
+        const unsigned long long act = __ballot(inr);
+        if (act) {
+          // lanes of this step with the same key, by bit-plane ballots of the
+          // chunk-local key (nbits of them); the lane's rank among them is the
+          // count of lower lanes (mbcnt), and the LAST lane of each group alone
+          // advances the wave's counter: no lane-order-dependent atomics
+          const unsigned kl = inr ? (unsigned)(k - k0) : 0u;
+          unsigned long long same = act;
+          for (int bit = 0; bit < nbits; ++bit) {
+            const bool on = (kl >> bit) & 1u;
+            const unsigned long long m = __ballot(on);
+            same &= on ? m : ~m;
+          }
+          if (inr) {
+            const int within = __builtin_amdgcn_mbcnt_hi(
+                (unsigned)(same >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)same, 0u));
+            const int base = hmine[kl];
+            rb[i] = base + within;
+            if ((same >> lane) >> 1 == 0ull) hmine[kl] = base + __popcll(same);
+          }
+        }
+        if (p == 0 && k0 == pk0 && i < i_hi && (unsigned)k >= (unsigned)V) rb[i] = -1;
+      }
     }
     carry += total;
     __syncthreads();
@@ -584,7 +627,6 @@ __global__ void __launch_bounds__(256)
 // --------------------------------------------------------------------------
 // host driver
 // --------------------------------------------------------------------------
-inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 // Upper bound of work units per batch element: one per tile plus one per
 // kItems of range items (an item lies in at most 2 tiles per stencil column).
@@ -604,6 +646,7 @@ struct SegWs {
   int* nunits;     // B
   float* xs;       // B*n*C
   float* partial;  // B*slots*C*kTV
+  void* sort;      // seg_sort_stable workspace
 };
 
 inline size_t seg_ws_bytes(int B, int C, int n, int V, int taps) {
@@ -617,6 +660,7 @@ inline size_t seg_ws_bytes(int B, int C, int n, int V, int taps) {
   s += align256((size_t)B * 4);
   s += align256((size_t)B * n * std::max(C, 1) * 4);
   s += align256((size_t)B * (umax - tiles) * std::max(C, 1) * kTV * 4);
+  s += align256(seg_sort_stable_ws(B, n, V));
   return s;
 }
 
@@ -639,6 +683,7 @@ inline SegWs seg_ws_carve(void* ws, int B, int C, int n, int V, int taps) {
   w.nunits = (int*)take((size_t)B * 4);
   w.xs = (float*)take((size_t)B * n * std::max(C, 1) * 4);
   w.partial = (float*)take((size_t)B * (umax - tiles) * std::max(C, 1) * kTV * 4);
+  w.sort = take(seg_sort_stable_ws(B, n, V));
   return w;
 }
 
@@ -652,12 +697,17 @@ inline int seg_scatter(const float* in, const int* key, long long key_bstride, b
                        float* out, void* ws, hipStream_t st, const char* what) {
   if (B == 0 || V == 0) return PCFM_OK;
   SegWs w = seg_ws_carve(ws, B, C, n, V, TAPS);
-  const int span = seg_sort_span(V);
-  const size_t sort_lds = seg_sort_lds(V);
+#ifdef PCFM_SORT_ROCPRIM
+  int e = seg_sort_stable(key, key_bstride, B, n, V, w.start, cnt_out, avg ? w.vinv : nullptr,
+                          w.rank, w.sort, st);
+  if (e) return e;
+#else
   int e = allow_big_lds((const void*)seg_sort_kernel);
   if (e) return e;
-  hipLaunchKernelGGL(seg_sort_kernel, dim3(seg_sort_parts(V), B), dim3(1024), sort_lds, st, key,
-                     key_bstride, n, V, span, w.start, cnt_out, avg ? w.vinv : nullptr, w.rank);
+  hipLaunchKernelGGL(seg_sort_kernel, dim3(seg_sort_parts(V), B), dim3(1024), seg_sort_lds(V), st,
+                     key, key_bstride, n, V, seg_sort_span(V), w.start, cnt_out,
+                     avg ? w.vinv : nullptr, w.rank);
+#endif
   if (C == 0) return check_launch(what);
   const int tiles = seg_tiles(V), umax = seg_umax(n, V, TAPS), slots = umax - tiles;
   hipLaunchKernelGGL(seg_units_kernel<TAPS>, dim3(B), dim3(1024), 0, st, w.start, V, r, tiles,

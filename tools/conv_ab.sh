@@ -1,0 +1,10 @@
+# A/B the conv variants built by `make variant` (names in $VARIANTS) against main.
+set -e
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+: > gpurun_out/${AB:-conv_ab}.jsonl
+for V in main ${VARIANTS}; do
+  if [ $V = main ]; then unset PCFM_LIB; else export PCFM_LIB=$PWD/point-cloud-flow-matching_amd/csrc/build/variants/libpcfm_$V.so; fi
+  timeout -k 10 120 python tools/${AB:-conv_ab}.py $V >> gpurun_out/${AB:-conv_ab}.jsonl
+done
