@@ -40,7 +40,7 @@ extern "C" {
  * split-operand convolution entry points; fused BatchNorm + activation;
  * 7: channel-segmented pointwise GEMMs, SE3d folded into the devoxelization;
  * 8: per-batch input bias of the head FiLM kernels; 9: split-K workspace of
- * pcfm_conv3d_igemm_cl). */
+ * pcfm_conv3d_igemm_cl; 10: fused AdamW + clip + EMA parameter update). */
 int pcfm_abi_version(void);
 /* Thread-local text of the last non-zero return code. */
 const char* pcfm_last_error(void);
@@ -462,6 +462,51 @@ int pcfm_gn_silu_fwd(const float* x, const float* w, const float* bias, int b, i
 int pcfm_gn_silu_bwd(const float* dout, const float* x, const float* w, const float* bias,
                      const float* mean, const float* rstd, int b, int c, int n, int groups,
                      float* dx, float* dw, float* dbias, void* ws, size_t ws_bytes, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Parameter update of the train step (reference train.py:652-661):
+ * GradScaler.unscale_ -> clip_grad_norm_(all parameters) -> AdamW.step
+ * (torch.optim.AdamW, train.py:249-253; its foreach arithmetic) -> EMA update
+ * of the new parameters (util.py:17-21) -- three launches over a device table
+ * of parameters instead of torch's per-list multi-tensor passes.
+ * ---------------------------------------------------------------------- */
+#define PCFM_ADAMW_CHUNK 4096     /* elements per block of the update kernels */
+#define PCFM_ADAMW_MAX_GROUPS 8   /* optimizer parameter groups */
+/* flags */
+#define PCFM_ADAMW_VEC4 1  /* every pointer 16-B aligned and n % 4 == 0 */
+#define PCFM_ADAMW_SKIP 2  /* no gradient (grad None): no update, not in the norm */
+#define PCFM_ADAMW_EMA 4   /* ema points at the parameter's EMA shadow */
+typedef struct {
+  float* p;        /* parameter f32 [n] */
+  const float* g;  /* gradient f32 [n] (scaled by the GradScaler scale) */
+  float* m;        /* AdamW exp_avg f32 [n] */
+  float* v;        /* AdamW exp_avg_sq f32 [n] */
+  float* ema;      /* EMA shadow f32 [n] or NULL */
+  long long n;
+  int group;       /* parameter group (lr, weight decay) */
+  int flags;
+} pcfm_adamw_tensor;
+
+/* Chunk length (PCFM_ADAMW_CHUNK) and scratch of pcfm_adamw_grad_norm. */
+int pcfm_adamw_chunk_elems(void);
+size_t pcfm_adamw_workspace_bytes(int nchunks);
+/* tensors: device table [ntensors]; chunks: device int [nchunks][2] = (tensor
+ * index, first element), one per PCFM_ADAMW_CHUNK elements of every tensor.
+ * scale: device f32 [1] GradScaler scale or NULL; max_norm <= 0: no clipping.
+ * steps: device f32 [ntensors] per-tensor AdamW step counts (+1 for every tensor
+ * with a gradient unless found_inf).  state: device f32 [4]: [0] total gradient
+ * norm (clip_grad_norm_'s return value), [1] gradient multiplier (1/scale * clip
+ * coefficient), [2] found_inf (GradScaler: skip the step). */
+int pcfm_adamw_grad_norm(const pcfm_adamw_tensor* tensors, int ntensors, const int* chunks,
+                         int nchunks, const float* scale, float max_norm, float* steps,
+                         float* state, void* ws, size_t ws_bytes, void* stream);
+/* AdamW step with the state pcfm_adamw_grad_norm wrote (no update when found_inf),
+ * then shadow = shadow * d + (1 - d) * p for the entries with an EMA shadow (also
+ * when the step is skipped).  lr / weight_decay: HOST arrays [ngroups]. */
+int pcfm_adamw_ema_step(const pcfm_adamw_tensor* tensors, const int* chunks, int nchunks,
+                        const float* steps, const float* state, int ngroups, const double* lr,
+                        const double* weight_decay, double beta1, double beta2, double eps,
+                        double ema_decay, void* stream);
 
 #ifdef __cplusplus
 }

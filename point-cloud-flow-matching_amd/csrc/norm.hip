@@ -158,30 +158,55 @@ __device__ __forceinline__ void bn_bwd_fin(const float* part, int P, int c, floa
   }
 }
 
-// y = act((x - mean) * invstd * gamma + beta), float4 per thread;
-// grid = (ceil(S4 / 256), B * C).
+// y = act((x - mean) * invstd * gamma + beta), kApplyU float4 per thread;
+// grid = (bn_apply_blocks(S), B * C).  Thread 0 derives the channel's
+// statistics from the P partials once per block (LDS broadcast).
+#ifndef PCFM_BN_APPLY_U
+#define PCFM_BN_APPLY_U 4
+#endif
+#ifndef PCFM_BN_BWD_U
+#define PCFM_BN_BWD_U 2
+#endif
+constexpr int kApplyU = PCFM_BN_APPLY_U;
+constexpr int kBwdU = PCFM_BN_BWD_U;
+inline int bn_apply_blocks(int s) { return ceil_div(s / 4, 256 * kApplyU); }
+inline int bn_bwd_blocks(int s) { return ceil_div(s / 4, 256 * kBwdU); }
+
 __global__ void __launch_bounds__(256)
     bn_act_apply_kernel(const float* __restrict__ x, BnFwdFin fin, float* __restrict__ mean,
                         float* __restrict__ invstd, const float* __restrict__ gamma,
                         const float* __restrict__ beta, int C, int S4, float slope,
                         float* __restrict__ y) {
+  __shared__ float st[2];
   const int c = (int)(blockIdx.y % C);
-  float m, is, var;
-  double n;
-  fin.get(x, c, m, is, var, n);
-  if (blockIdx.x == 0 && blockIdx.y < (unsigned)C && threadIdx.x == 0)
-    fin.publish(c, m, is, var, n, mean, invstd);
-  const int s4 = blockIdx.x * 256 + threadIdx.x;
-  if (s4 >= S4) return;
-  const size_t i = (size_t)blockIdx.y * S4 + s4;
+  if (threadIdx.x == 0) {
+    float m, is, var;
+    double n;
+    fin.get(x, c, m, is, var, n);
+    if (blockIdx.x == 0 && blockIdx.y < (unsigned)C) fin.publish(c, m, is, var, n, mean, invstd);
+    st[0] = m;
+    st[1] = is;
+  }
   const float g = gamma[c], bt = beta[c];
-  const float4 v = reinterpret_cast<const float4*>(x)[i];
-  float4 o;
-  o.x = act(__builtin_fmaf((v.x - m) * is, g, bt), slope);
-  o.y = act(__builtin_fmaf((v.y - m) * is, g, bt), slope);
-  o.z = act(__builtin_fmaf((v.z - m) * is, g, bt), slope);
-  o.w = act(__builtin_fmaf((v.w - m) * is, g, bt), slope);
-  reinterpret_cast<float4*>(y)[i] = o;
+  const float4* __restrict__ x4 = reinterpret_cast<const float4*>(x) + (size_t)blockIdx.y * S4;
+  float4* __restrict__ y4 = reinterpret_cast<float4*>(y) + (size_t)blockIdx.y * S4;
+  const int s0 = blockIdx.x * 256 * kApplyU + threadIdx.x;
+  float4 v[kApplyU];
+#pragma unroll
+  for (int u = 0; u < kApplyU; ++u)
+    if (s0 + u * 256 < S4) v[u] = x4[s0 + u * 256];
+  __syncthreads();
+  const float m = st[0], is = st[1];
+#pragma unroll
+  for (int u = 0; u < kApplyU; ++u) {
+    if (s0 + u * 256 >= S4) break;
+    float4 o;
+    o.x = act(__builtin_fmaf((v[u].x - m) * is, g, bt), slope);
+    o.y = act(__builtin_fmaf((v[u].y - m) * is, g, bt), slope);
+    o.z = act(__builtin_fmaf((v[u].z - m) * is, g, bt), slope);
+    o.w = act(__builtin_fmaf((v[u].w - m) * is, g, bt), slope);
+    y4[s0 + u * 256] = o;
+  }
 }
 
 // grid = (C, P): part[c][p] = (sum g, sum g * xhat), g = dz * act'(bn(x)).
@@ -245,8 +270,9 @@ __global__ void __launch_bounds__(256)
   dgamma[c] = sgx;
 }
 
-// dx = gamma * invstd * (g - dbeta / n - xhat * dgamma / n); grid (ceil(S4/256), B*C).
-// With rowpart: the block's sum of dx -> rowpart[row][block] (producer bias grad).
+// dx = gamma * invstd * (g - dbeta / n - xhat * dgamma / n), kBwdU float4
+// per thread; grid (bn_bwd_blocks(S), B*C).  With rowpart: the block's sum of
+// dx -> rowpart[row][block] (producer bias grad).
 __global__ void __launch_bounds__(256)
     bn_bwd_apply_kernel(const float* __restrict__ dz, const float* __restrict__ x,
                         const float* __restrict__ mean, const float* __restrict__ invstd,
@@ -256,35 +282,53 @@ __global__ void __launch_bounds__(256)
                         int S4, float inv_n, float slope, float* __restrict__ dx,
                         float* __restrict__ rowpart) {
   __shared__ float sh[8];
-  const int s4 = blockIdx.x * 256 + threadIdx.x;
-  const bool ok = s4 < S4;
+  __shared__ float st[2];
   const int c = (int)(blockIdx.y % C);
-  const size_t i = (size_t)blockIdx.y * S4 + (ok ? s4 : 0);
-  float sg, sgx;
-  bn_bwd_fin(part, P, c, sg, sgx);
-  if (blockIdx.x == 0 && blockIdx.y < (unsigned)C && threadIdx.x == 0) {
-    dbeta[c] = sg;
-    dgamma[c] = sgx;
+  if (threadIdx.x == 0) {
+    float sg, sgx;
+    bn_bwd_fin(part, P, c, sg, sgx);
+    if (blockIdx.x == 0 && blockIdx.y < (unsigned)C) {
+      dbeta[c] = sg;
+      dgamma[c] = sgx;
+    }
+    st[0] = sg;
+    st[1] = sgx;
   }
   const float m = mean[c], is = invstd[c], gm = gamma[c], bt = beta[c];
-  const float mg = sg * inv_n, mgx = sgx * inv_n, k = gm * is;
-  float o[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-  if (ok) {
-    const float4 v = reinterpret_cast<const float4*>(x)[i];
-    const float4 d = reinterpret_cast<const float4*>(dz)[i];
-    const float xv[4] = {v.x, v.y, v.z, v.w}, dv[4] = {d.x, d.y, d.z, d.w};
+  const size_t row = (size_t)blockIdx.y * S4;
+  const float4* __restrict__ x4 = reinterpret_cast<const float4*>(x) + row;
+  const float4* __restrict__ d4 = reinterpret_cast<const float4*>(dz) + row;
+  float4* __restrict__ o4 = reinterpret_cast<float4*>(dx) + row;
+  const int s0 = blockIdx.x * 256 * kBwdU + threadIdx.x;
+  float4 v[kBwdU], d[kBwdU];
+#pragma unroll
+  for (int u = 0; u < kBwdU; ++u)
+    if (s0 + u * 256 < S4) {
+      v[u] = x4[s0 + u * 256];
+      d[u] = d4[s0 + u * 256];
+    }
+  __syncthreads();
+  const float mg = st[0] * inv_n, mgx = st[1] * inv_n, k = gm * is;
+  float tsum = 0.0f;
+#pragma unroll
+  for (int u = 0; u < kBwdU; ++u) {
+    if (s0 + u * 256 >= S4) break;
+    const float xv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+    const float dv[4] = {d[u].x, d[u].y, d[u].z, d[u].w};
+    float o[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const float xh = (xv[e] - m) * is;
       const float g = __builtin_fmaf(xh, gm, bt) > 0.0f ? dv[e] : dv[e] * slope;
       o[e] = k * ((g - mg) - xh * mgx);
     }
-    reinterpret_cast<float4*>(dx)[i] = make_float4(o[0], o[1], o[2], o[3]);
+    o4[s0 + u * 256] = make_float4(o[0], o[1], o[2], o[3]);
+    tsum += (o[0] + o[1]) + (o[2] + o[3]);
   }
   if (rowpart != nullptr) {  // block-uniform branch: every thread takes part
-    float t = (o[0] + o[1]) + (o[2] + o[3]), z = 0.0f;
-    block_sum2(t, z, sh);
-    if (threadIdx.x == 0) rowpart[(size_t)blockIdx.y * gridDim.x + blockIdx.x] = t;
+    float z = 0.0f;
+    block_sum2(tsum, z, sh);
+    if (threadIdx.x == 0) rowpart[(size_t)blockIdx.y * gridDim.x + blockIdx.x] = tsum;
   }
 }
 
@@ -701,7 +745,7 @@ using namespace pcfm;
 
 extern "C" size_t pcfm_bn_workspace_bytes(int b, int c, int s) {
   if (!bn_ok(b, c, s)) return 0;
-  const size_t rowpart = (size_t)b * c * ceil_div(s / 4, 256);
+  const size_t rowpart = (size_t)b * c * bn_bwd_blocks(s);
   return ((size_t)c * bn_parts(b) * 2 + rowpart) * sizeof(float);
 }
 
@@ -718,7 +762,7 @@ extern "C" int pcfm_bn_act_fwd(const float* x, const float* gamma, const float* 
   float* part = (float*)ws;
   hipLaunchKernelGGL(bn_stats_kernel, dim3(c, bn_parts(b)), dim3(256), 0, st, x, b, c, s, part);
   const BnFwdFin fin{part, b, s, bn_parts(b), eps, momentum, running_mean, running_var};
-  hipLaunchKernelGGL(bn_act_apply_kernel, dim3(ceil_div(s / 4, 256), b * c), dim3(256), 0, st, x,
+  hipLaunchKernelGGL(bn_act_apply_kernel, dim3(bn_apply_blocks(s), b * c), dim3(256), 0, st, x,
                      fin, mean, invstd, gamma, beta, c, s / 4, slope, y);
   return check_launch("bn_act_fwd");
 }
@@ -734,7 +778,7 @@ extern "C" int pcfm_bn_act_bwd(const float* dz, const float* x, const float* gam
   float* part = (float*)ws;
   hipLaunchKernelGGL(bn_bwd_stats_kernel, dim3(c, bn_parts(b)), dim3(256), 0, st, dz, x, mean,
                      invstd, gamma, beta, b, c, s, slope, part);
-  const int nch = ceil_div(s / 4, 256);
+  const int nch = bn_bwd_blocks(s);
   float* rowpart = dbias_in != nullptr ? part + (size_t)c * bn_parts(b) * 2 : nullptr;
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(nch, b * c), dim3(256), 0, st, dz, x, mean, invstd,
                      gamma, beta, (const float*)part, bn_parts(b), dgamma, dbeta, c, s / 4,

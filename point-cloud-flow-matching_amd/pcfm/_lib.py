@@ -21,6 +21,8 @@ _I = ctypes.c_int
 _F = ctypes.c_float
 _Z = ctypes.c_size_t
 _L = ctypes.c_longlong
+_D = ctypes.c_double
+_DP = ctypes.POINTER(ctypes.c_double)  # host array
 
 # name -> (restype, argtypes); must list every symbol of include/pcfm.h.
 SIGNATURES = {
@@ -102,9 +104,13 @@ SIGNATURES = {
                                   _P]),
     "pcfm_gn_film_res_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P,
                                   _P, _P, _Z, _P]),
+    "pcfm_adamw_chunk_elems": (_I, []),
+    "pcfm_adamw_workspace_bytes": (_Z, [_I]),
+    "pcfm_adamw_grad_norm": (_I, [_P, _I, _P, _I, _P, _F, _P, _P, _P, _Z, _P]),
+    "pcfm_adamw_ema_step": (_I, [_P, _P, _I, _P, _P, _I, _DP, _DP, _D, _D, _D, _D, _P]),
 }
 
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 _lock = threading.Lock()
 _lib = None

@@ -12,6 +12,10 @@ Deliberate, result-preserving differences (all switchable in TrainConfig):
     per element it is the same mul_ then add_(alpha=1-d).
   * `fused_adamw`: AdamW(fused=True) takes GradScaler's inf check on the
     device instead of the host round trip of GradScaler.step; same update rule.
+  * `fused_step` (HIP devices): unscale + clip + AdamW + the parameters' EMA
+    update run as three HIP launches (pcfm.optim.FusedAdamWEMA, csrc/optim.hip)
+    instead of ~40 multi-tensor launches; same arithmetic, inf check on the
+    device as with `fused_adamw`.  The EMA of buffers stays a foreach update.
   * `device_rng`: t ~ Beta(a, 1) is sampled on the device (the reference
     samples on the CPU and copies, train.py:604-605, :639-640); same law.
   * `tunableop`: the autocast Linears use library GEMM algorithms measured on
@@ -98,6 +102,7 @@ class TrainConfig:
     # result-preserving implementation switches (module docstring)
     ema_foreach: bool = True
     fused_adamw: bool = True
+    fused_step: bool = True
     device_rng: bool = True
     film_per_point: bool = False
     # MIOpen exhaustive solver search for every conv shape (cudnn.benchmark):
@@ -168,6 +173,13 @@ class EMA:
         self.shadow = {k: v.detach().clone() for k, v in model.state_dict().items()}
         self._keys = None
         self._lists = None  # (model id, shadow list, live tensor list), built once
+        # keys whose update another component performs (the fused parameter
+        # update, pcfm.optim): update() leaves them alone
+        self.external = frozenset()
+
+    def param_shadows(self, model: nn.Module) -> Dict[torch.Tensor, torch.Tensor]:
+        """{parameter: its shadow tensor} for model's parameters."""
+        return {p: self.shadow[k] for k, p in model.named_parameters()}
 
     @torch.no_grad()
     def update(self, model: nn.Module) -> None:
@@ -178,16 +190,20 @@ class EMA:
             # identity across steps (in-place optimizer updates), so list them once
             if self._lists is None or self._lists[0] != id(model):
                 sd = model.state_dict()
-                keys = [k for k, v in sd.items() if v.dtype.is_floating_point]
+                keys = [k for k, v in sd.items()
+                        if v.dtype.is_floating_point and k not in self.external]
                 self._lists = (id(model), [self.shadow[k] for k in keys],
                                [sd[k].detach() for k in keys])
             _, shadow, cur = self._lists
+            if not shadow:
+                return
             torch._foreach_mul_(shadow, d)
             torch._foreach_add_(shadow, cur, alpha=1.0 - d)
             return
         sd = model.state_dict()
         if self._keys is None:
-            self._keys = [k for k, v in sd.items() if v.dtype.is_floating_point]
+            self._keys = [k for k, v in sd.items()
+                          if v.dtype.is_floating_point and k not in self.external]
         for k in self._keys:
             self.shadow[k].mul_(d).add_(sd[k].detach(), alpha=1.0 - d)
 
@@ -293,18 +309,30 @@ class Trainer:
             self.model_enc = DDP(self.enc, **kw)
             self.model_pf = DDP(self.pf, **kw)
             self.model_lf = DDP(self.lf, **kw)
-        fused = bool(cfg.fused_adamw and self.device.type == "cuda")
-        self.opt = torch.optim.AdamW([
-            {"params": self.enc.parameters(), "lr": cfg.lr_enc},
-            {"params": self.pf.parameters(), "lr": cfg.lr_pf},
-            {"params": self.lf.parameters(), "lr": cfg.lr_lf},
-        ], weight_decay=cfg.weight_decay, fused=fused)
+        groups = [
+            {"params": list(self.enc.parameters()), "lr": cfg.lr_enc},
+            {"params": list(self.pf.parameters()), "lr": cfg.lr_pf},
+            {"params": list(self.lf.parameters()), "lr": cfg.lr_lf},
+        ]
+        self.fused_step = bool(cfg.fused_step and self.device.type == "cuda")
+        if self.fused_step:
+            from pcfm.optim import FusedAdamWEMA
+            for g in groups:
+                g["weight_decay"] = cfg.weight_decay
+            shadows = {**self.ema_pf.param_shadows(self.pf), **self.ema_lf.param_shadows(self.lf)}
+            self.opt = FusedAdamWEMA(groups, ema_shadows=shadows, ema_decay=cfg.ema_decay)
+            self.ema_pf.external = frozenset(k for k, _ in self.pf.named_parameters())
+            self.ema_lf.external = frozenset(k for k, _ in self.lf.named_parameters())
+        else:
+            fused = bool(cfg.fused_adamw and self.device.type == "cuda")
+            self.opt = torch.optim.AdamW(groups, weight_decay=cfg.weight_decay, fused=fused)
         self.scaler = torch.amp.GradScaler(self.device.type, enabled=cfg.amp)
         self.total_steps = cfg.epochs * max(1, cfg.steps_per_epoch)
         self.global_step = 0
         self._clip_params = (list(self.enc.parameters()) + list(self.pf.parameters())
                              + list(self.lf.parameters()))
         self._beta = None
+        self.last_grad_norm = None  # clip_grad_norm_'s value of the last step
 
     # -- helpers ------------------------------------------------------------
     def _autocast(self):
@@ -359,6 +387,21 @@ class Trainer:
         self.enc.train()
         self.pf.train()
         self.lf.train()
+
+    def _update_params(self) -> None:
+        """unscale + clip + AdamW step + scale update + zero_grad (train.py:652-657);
+        with `fused_step` also the parameters' EMA update (pcfm.optim)."""
+        cfg = self.cfg
+        clip = float(cfg.grad_clip_norm) if cfg.grad_clip_norm and cfg.grad_clip_norm > 0 else 0.0
+        if self.fused_step:
+            self.last_grad_norm = self.opt.step(clip, self.scaler)
+        else:
+            if clip > 0:
+                self.scaler.unscale_(self.opt)
+                self.last_grad_norm = torch.nn.utils.clip_grad_norm_(self._clip_params, clip)
+            self.scaler.step(self.opt)
+            self.scaler.update()
+        self.opt.zero_grad(set_to_none=True)
 
     # -- one iteration ------------------------------------------------------
     def step(self, batch: Dict[str, torch.Tensor], epoch: int,
@@ -438,12 +481,7 @@ class Trainer:
 
         loss = cfg.lambda_point * loss_point + cfg.lambda_latent * loss_latent
         self.scaler.scale(loss).backward()
-        if cfg.grad_clip_norm and cfg.grad_clip_norm > 0:
-            self.scaler.unscale_(self.opt)
-            torch.nn.utils.clip_grad_norm_(self._clip_params, cfg.grad_clip_norm)
-        self.scaler.step(self.opt)
-        self.scaler.update()
-        self.opt.zero_grad(set_to_none=True)
+        self._update_params()
 
         self.ema_pf.update(self.pf)
         self.ema_lf.update(self.lf)

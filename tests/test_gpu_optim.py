@@ -1,0 +1,141 @@
+"""GPU: the fused parameter update (pcfm.optim.FusedAdamWEMA, csrc/optim.hip)
+against the reference's own sequence on the same tensors: GradScaler unscale,
+clip_grad_norm_, torch.optim.AdamW (foreach, the reference's default,
+train.py:249-253) and util.EMA's mul_/add_ (util.py:17-21)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+SHAPES = [(256, 128, 3, 3, 3), (7,), (3,), (513, 9), (4096,), (4097,), (64, 64), (1,)]
+
+
+def _setup(seed):
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    ps = [torch.randn(s, device=DEV, generator=g) * 0.1 for s in SHAPES]
+    shadows = [p.clone() + 0.01 for p in ps]
+    return g, ps, shadows
+
+
+def _reference_step(ps, grads, shadows, opt, scale, max_norm, decay, ema_mask):
+    for p, gr in zip(ps, grads):
+        p.grad = None if gr is None else gr.clone()
+    live = [p for p in ps if p.grad is not None]
+    inv = 1.0 / scale  # a power of two, as GradScaler's scales are
+    found = any(not torch.isfinite(p.grad).all() for p in live)
+    torch._foreach_mul_([p.grad for p in live], inv)
+    # the Trainer clips only for grad_clip_norm > 0 (train.py:653-656)
+    total = torch.nn.utils.clip_grad_norm_(live, max_norm) if max_norm > 0 else 0.0
+    if not found:
+        opt.step()
+    with torch.no_grad():
+        for p, s, on in zip(ps, shadows, ema_mask):
+            if on:
+                s.mul_(decay).add_(p, alpha=1.0 - decay)
+    return float(total), found
+
+
+class _Scaler:
+    """The GradScaler attributes FusedAdamWEMA.step reads and updates."""
+
+    def __init__(self, scale):
+        self._scale = torch.full((1,), float(scale), device=DEV)
+        self._growth_tracker = torch.zeros(1, dtype=torch.int32, device=DEV)
+        self._growth_factor, self._backoff_factor, self._growth_interval = 2.0, 0.5, 2000
+
+    def is_enabled(self):
+        return True
+
+
+@pytest.mark.parametrize("max_norm", [1.0, 1e4, 0.0])
+def test_fused_adamw_ema_matches_torch(max_norm):
+    from pcfm.optim import FusedAdamWEMA
+    g, ps, shadows = _setup(1)
+    ref_ps = [p.clone() for p in ps]
+    ref_sh = [s.clone() for s in shadows]
+    lrs, wd, decay = (3e-4, 1e-3, 5e-4), 1e-4, 0.999
+    split = [slice(0, 3), slice(3, 6), slice(6, len(ps))]
+    ema_mask = [i % 3 != 1 for i in range(len(ps))]
+    fused = FusedAdamWEMA(
+        [{"params": ps[s], "lr": lr, "weight_decay": wd} for s, lr in zip(split, lrs)],
+        ema_shadows={p: sh for p, sh, on in zip(ps, shadows, ema_mask) if on},
+        ema_decay=decay)
+    ref_opt = torch.optim.AdamW([{"params": ref_ps[s], "lr": lr} for s, lr in zip(split, lrs)],
+                                weight_decay=wd, foreach=True)
+    scale = 2.0 ** 10
+    scaler = _Scaler(scale)
+    for step in range(4):
+        grads = [torch.randn(p.shape, device=DEV, generator=g) * scale * 0.05 for p in ps]
+        grads[5] = None if step == 2 else grads[5]  # a parameter without gradient
+        for p, gr in zip(ps, grads):
+            p.grad = gr
+        # the cosine schedule rewrites the group lrs between steps
+        for grp, rgrp in zip(fused.param_groups, ref_opt.param_groups):
+            grp["lr"] = rgrp["lr"] = grp["lr"] * 0.9
+        norm = fused.step(max_norm, scaler)
+        tot, _ = _reference_step(ref_ps, grads, ref_sh, ref_opt, scale, max_norm, decay, ema_mask)
+        if max_norm > 0:
+            assert abs(float(norm) - tot) <= 1e-5 * tot
+        for a, b in zip(ps, ref_ps):
+            torch.testing.assert_close(a, b, rtol=2e-6, atol=1e-8)
+        for a, b in zip(shadows, ref_sh):
+            torch.testing.assert_close(a, b, rtol=2e-6, atol=1e-8)
+        for a, b in zip(ps, ref_ps):  # keep the two on identical values
+            a.copy_(b)
+        for a, b in zip(shadows, ref_sh):
+            a.copy_(b)
+    steps = fused.steps.cpu().tolist()
+    assert steps[5] == 3.0 and all(v == 4.0 for i, v in enumerate(steps) if i != 5)
+    assert float(scaler._scale) == scale  # no inf: no backoff (growth after 2000)
+
+
+def test_fused_adamw_skips_on_inf_and_backs_off():
+    from pcfm.optim import FusedAdamWEMA
+    g, ps, shadows = _setup(2)
+    fused = FusedAdamWEMA([{"params": ps, "lr": 1e-3, "weight_decay": 1e-4}],
+                          ema_shadows=dict(zip(ps, shadows)), ema_decay=0.9)
+    scaler = _Scaler(2.0 ** 16)
+    before = [p.clone() for p in ps]
+    sh_before = [s.clone() for s in shadows]
+    for p in ps:
+        p.grad = torch.randn(p.shape, device=DEV, generator=g)
+    ps[3].grad[0, 0] = float("inf")
+    fused.step(1.0, scaler)
+    for a, b in zip(ps, before):
+        assert torch.equal(a, b)  # update skipped
+    for s, s0, p in zip(shadows, sh_before, before):  # the EMA still moves
+        torch.testing.assert_close(s, s0 * 0.9 + 0.1 * p, rtol=1e-6, atol=1e-7)
+    assert float(fused.steps.max()) == 0.0 and float(fused.found_inf) == 1.0
+    assert float(scaler._scale) == 2.0 ** 15
+    for p in ps:
+        p.grad = torch.randn(p.shape, device=DEV, generator=g)
+    fused.step(1.0, scaler)
+    assert float(fused.steps.min()) == 1.0 and float(fused.found_inf) == 0.0
+    assert not all(torch.equal(a, b) for a, b in zip(ps, before))
+
+
+def test_trainer_fused_step_matches_torch_path():
+    """Two Trainer steps at a small config: fused update vs torch AdamW + clip +
+    foreach EMA from the same initial state and batch."""
+    from pcfm.train import TrainConfig, Trainer, synthetic_batch
+    cfg = dict(batch_size=2, num_points=1024, steps_per_epoch=4, epochs=1, tunableop=False,
+               miopen_find=False, device_rng=False)
+    out = {}
+    for fused in (True, False):
+        tr = Trainer(TrainConfig(fused_step=fused, **cfg), DEV)
+        tr.train_mode()
+        batch = synthetic_batch(tr.cfg, DEV, generator=torch.Generator(device=DEV).manual_seed(3))
+        torch.manual_seed(5)
+        for _ in range(2):
+            tr.step(batch, epoch=201)
+        out[fused] = ([p.detach().double().sum().item() for p in tr._clip_params],
+                      [v.double().sum().item() for v in tr.ema_pf.shadow.values()
+                       if v.dtype.is_floating_point], float(tr.last_grad_norm))
+    pf, ef, nf = out[True]
+    pt, et, nt = out[False]
+    # identical forward/backward (same seeds); the updates differ only in rounding
+    assert abs(nf - nt) <= 1e-4 * nt
+    d = np.abs(np.array(pf) - np.array(pt))
+    assert d.max() <= 1e-3 * 3e-4 * 2 * max(1.0, np.abs(pt).max()), d.max()
+    np.testing.assert_allclose(ef, et, rtol=1e-6, atol=1e-6)

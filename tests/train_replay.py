@@ -34,21 +34,23 @@ def golden_config(**kw) -> TrainConfig:
 
 
 @contextlib.contextmanager
-def _record_clip(store):
-    orig = torch.nn.utils.clip_grad_norm_
+def _record_update(tr, store):
+    """Record, around Trainer._update_params, the per-parameter norms of the
+    unscaled gradients (what clip_grad_norm_ sees) and the total norm it returns."""
+    orig = tr._update_params
+    params = _params(tr)
 
-    def clip(params, *a, **kw):
-        params = list(params)
-        store["grad_norms"] = np.array([p.grad.double().norm().item() if p.grad is not None
-                                        else 0.0 for p in params])
-        total = orig(params, *a, **kw)
-        store["total_norm"] = float(total)
-        return total
-    torch.nn.utils.clip_grad_norm_ = clip
+    def update():
+        inv = 1.0 / tr.scaler.get_scale() if tr.scaler.is_enabled() else 1.0
+        store["grad_norms"] = np.array([p.grad.double().norm().item() * inv
+                                        if p.grad is not None else 0.0 for p in params])
+        orig()
+        store["total_norm"] = float(tr.last_grad_norm)
+    tr._update_params = update
     try:
         yield
     finally:
-        torch.nn.utils.clip_grad_norm_ = orig
+        del tr._update_params
 
 
 def _params(tr):
@@ -118,7 +120,7 @@ def replay(g, device, n_steps=None, **cfg_kw):
                                                          "t_z")}
         pre = np.array([q.detach().double().sum().item() for q in params])
         rec = {}
-        with _record_clip(rec):
+        with _record_update(tr, rec):
             losses = tr.step(batch, epoch=1, draws=draws)
         post = np.array([q.detach().double().sum().item() for q in params])
         mse = g[p + "mse"]

@@ -24,19 +24,24 @@ def timeit(fn, it=20):
     return e0.elapsed_time(e1) / it
 
 
-res = {"tag": sys.argv[1] if len(sys.argv) > 1 else "main"}
-g = torch.Generator(device="cuda").manual_seed(0)
-b, n = 8, 20000
-for c, r in ((128, 32), (256, 16), (256, 8)):
-    x = torch.randn(b, 3, n, device="cuda", generator=g)
-    x = x - x.mean(2, keepdim=True)
-    x = x / (x.norm(dim=1, keepdim=True).max(dim=2, keepdim=True).values * 2.0 + 1e-6) + 0.5
-    nc = torch.clamp(x * r, 0, r - 1)
-    vc = torch.round(nc).to(torch.int32)
-    feat = torch.randn(b, c, n, device="cuda", generator=g)
-    grid = torch.randn(b, c, r ** 3, device="cuda", generator=g)
-    _, inds, wgts = ops.trilinear_devoxelize_forward(r, True, nc, grid)
-    res[f"C{c}R{r}"] = {
-        "vox_fwd_ms": timeit(lambda: ops.avg_voxelize_forward(feat, vc, r)),
-        "devox_bwd_ms": timeit(lambda: ops.trilinear_devoxelize_backward(feat, inds, wgts, r))}
-print(json.dumps(res), flush=True)
+def main():
+    res = {"tag": sys.argv[1] if len(sys.argv) > 1 else "main"}
+    g = torch.Generator(device="cuda").manual_seed(0)
+    b, n = 8, 20000
+    for c, r in ((128, 32), (256, 16), (256, 8)):
+        x = torch.randn(b, 3, n, device="cuda", generator=g)
+        x = x - x.mean(2, keepdim=True)
+        x = x / (x.norm(dim=1, keepdim=True).max(dim=2, keepdim=True).values * 2.0 + 1e-6) + 0.5
+        nc = torch.clamp(x * r, 0, r - 1)
+        vc = torch.round(nc).to(torch.int32)
+        feat = torch.randn(b, c, n, device="cuda", generator=g)
+        grid = torch.randn(b, c, r ** 3, device="cuda", generator=g)
+        _, inds, wgts = ops.trilinear_devoxelize_forward(r, True, nc, grid)
+        res[f"C{c}R{r}"] = {
+            "vox_fwd_ms": timeit(lambda: ops.avg_voxelize_forward(feat, vc, r)),
+            "devox_bwd_ms": timeit(lambda: ops.trilinear_devoxelize_backward(feat, inds, wgts, r))}
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()
