@@ -40,7 +40,8 @@ extern "C" {
  * split-operand convolution entry points; fused BatchNorm + activation;
  * 7: channel-segmented pointwise GEMMs, SE3d folded into the devoxelization;
  * 8: per-batch input bias of the head FiLM kernels; 9: split-K workspace of
- * pcfm_conv3d_igemm_cl; 10: fused AdamW + clip + EMA parameter update). */
+ * pcfm_conv3d_igemm_cl; 10: fused AdamW + clip + EMA parameter update; 11: segment
+ * plans shared by scatters over the same points). */
 int pcfm_abi_version(void);
 /* Thread-local text of the last non-zero return code. */
 const char* pcfm_last_error(void);
@@ -462,6 +463,35 @@ int pcfm_gn_silu_fwd(const float* x, const float* w, const float* bias, int b, i
 int pcfm_gn_silu_bwd(const float* dout, const float* x, const float* w, const float* bias,
                      const float* mean, const float* rstd, int b, int c, int n, int groups,
                      float* dx, float* dw, float* dbias, void* ws, size_t ws_bytes, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Segment plans.  avg_voxelize_fwd and trilinear_devoxelize_bwd are scatters:
+ * a stable sort of the points by target voxel + a list of work units (the
+ * plan), then the deterministic segment sums of the features (the apply).  The
+ * plan depends on the coordinates only, and the hybrid backbone runs two PVConv
+ * blocks per stage on the SAME points (models.py:371-389 _PVStage: PVConv
+ * passes `coords` through, pvconv.py:35-38), so it is built once per
+ * (points, resolution) and applied to every block's features.  The one-shot
+ * entry points above are plan + apply in one workspace; results are identical.
+ * taps: 1 (voxelization: key = voxel of the rounded coordinate) or 8
+ * (devoxelization backward: key = base cell inds[b][0][i], 8 trilinear taps).
+ * ---------------------------------------------------------------------- */
+size_t pcfm_seg_plan_bytes(int b, int n, int r, int taps);
+size_t pcfm_seg_apply_workspace_bytes(int b, int c, int n, int r, int taps);
+/* Voxelization plan from integer coords [b][3][n]: also writes ind [b][n] and
+ * cnt [b][r^3] exactly as pcfm_avg_voxelize_fwd does. */
+int pcfm_avg_voxelize_plan(const int* coords, int b, int n, int r, int* ind, int* cnt,
+                           void* plan, size_t plan_bytes, void* stream);
+/* out [b][c][r^3] of pcfm_avg_voxelize_fwd on a voxelization plan. */
+int pcfm_avg_voxelize_fwd_planned(const float* feat, const void* plan, int b, int c, int n, int r,
+                                  float* out, void* ws, size_t ws_bytes, void* stream);
+/* Devoxelization-backward plan from the forward's inds i32 / wgts f32 [b][8][n]. */
+int pcfm_trilinear_devoxelize_bwd_plan(const int* inds, const float* wgts, int b, int n, int r,
+                                       void* plan, size_t plan_bytes, void* stream);
+/* grad_x [b][c][r^3] of pcfm_trilinear_devoxelize_bwd on a devoxelization plan. */
+int pcfm_trilinear_devoxelize_bwd_planned(const float* grad_y, const void* plan, int b, int c,
+                                          int n, int r, float* grad_x, void* ws, size_t ws_bytes,
+                                          void* stream);
 
 /* ------------------------------------------------------------------------
  * Parameter update of the train step (reference train.py:652-661):

@@ -259,7 +259,7 @@ __global__ void __launch_bounds__(256)
     const int j = j0 + jj;
     const int r = j < n ? rank[(size_t)b * n + j] : -1;
     rk[jj] = r;
-    if (blockIdx.y == 0 && r >= 0) {
+    if (skey != nullptr && blockIdx.y == 0 && r >= 0) {
       const size_t o = (size_t)b * n + r;
       skey[o] = key[(size_t)b * key_bstride + j];
       if (tapw != nullptr) {
@@ -330,6 +330,28 @@ __global__ void __launch_bounds__(256)
       const int r = rk[jr];
       if (r >= 0) xs[((size_t)b * n + r) * C + c] = tile[lane][jr];
     }
+  }
+}
+
+// Plan-side part of step 3: the sorted keys (skey[b, rank[i]] = key[i]) and,
+// for the trilinear stencil, the sorted tap weights (ws8[b, rank[i], k] =
+// tapw[b, k, i]) -- built once per plan, reused by every scatter over it.
+// grid = (ceil(n / 256), B).
+__global__ void __launch_bounds__(256)
+    seg_plan_rows_kernel(const int* __restrict__ rank, const int* __restrict__ key,
+                         long long key_bstride, const float* __restrict__ tapw, int n,
+                         int* __restrict__ skey, float* __restrict__ ws8) {
+  const int b = blockIdx.y, i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int r = rank[(size_t)b * n + i];
+  if (r < 0) return;
+  const size_t o = (size_t)b * n + r;
+  skey[o] = key[(size_t)b * key_bstride + i];
+  if (tapw != nullptr) {
+    const float* tb = tapw + (size_t)b * 8 * n + i;
+    float4* d = reinterpret_cast<float4*>(ws8 + o * 8);
+    d[0] = make_float4(tb[0], tb[(size_t)n], tb[(size_t)2 * n], tb[(size_t)3 * n]);
+    d[1] = make_float4(tb[(size_t)4 * n], tb[(size_t)5 * n], tb[(size_t)6 * n], tb[(size_t)7 * n]);
   }
 }
 
@@ -635,7 +657,11 @@ inline int seg_umax(int n, int V, int taps) {
   return seg_tiles(V) + (int)(((long long)(taps == 8 ? 8 : 1) * n + kItems - 1) / kItems) + 1;
 }
 
-struct SegWs {
+// A scatter = plan (sort the items by key, cut the output into work units,
+// gather the sorted keys / tap weights) + apply (channels-last rows, unit
+// gather, partial sums).  The plan depends only on the keys, so scatters over
+// the same points share it (include/pcfm.h, "segment plans").
+struct SegPlan {
   int* start;      // B*(V+1)
   float* vinv;     // B*V (per-voxel 1/cnt)
   int* rank;       // B*n
@@ -644,12 +670,14 @@ struct SegWs {
   int4* units;     // B*umax
   int2* tinfo;     // B*tiles
   int* nunits;     // B
-  float* xs;       // B*n*C
-  float* partial;  // B*slots*C*kTV
   void* sort;      // seg_sort_stable workspace
 };
+struct SegApplyWs {
+  float* xs;       // B*n*C
+  float* partial;  // B*slots*C*kTV
+};
 
-inline size_t seg_ws_bytes(int B, int C, int n, int V, int taps) {
+inline size_t seg_plan_bytes(int B, int n, int V, int taps) {
   const int umax = seg_umax(n, V, taps), tiles = seg_tiles(V);
   size_t s = align256((size_t)B * (V + 1) * 4);
   s += align256((size_t)B * V * 4);
@@ -658,45 +686,58 @@ inline size_t seg_ws_bytes(int B, int C, int n, int V, int taps) {
   s += align256((size_t)B * umax * 16);
   s += align256((size_t)B * tiles * 8);
   s += align256((size_t)B * 4);
-  s += align256((size_t)B * n * std::max(C, 1) * 4);
-  s += align256((size_t)B * (umax - tiles) * std::max(C, 1) * kTV * 4);
   s += align256(seg_sort_stable_ws(B, n, V));
   return s;
 }
-
-inline SegWs seg_ws_carve(void* ws, int B, int C, int n, int V, int taps) {
+inline size_t seg_apply_bytes(int B, int C, int n, int V, int taps) {
   const int umax = seg_umax(n, V, taps), tiles = seg_tiles(V);
-  char* p = (char*)ws;
-  auto take = [&p](size_t bytes) {
+  return align256((size_t)B * n * std::max(C, 1) * 4) +
+         align256((size_t)B * (umax - tiles) * std::max(C, 1) * kTV * 4);
+}
+inline size_t seg_ws_bytes(int B, int C, int n, int V, int taps) {
+  return seg_plan_bytes(B, n, V, taps) + seg_apply_bytes(B, C, n, V, taps);
+}
+
+struct SegCarver {
+  char* p;
+  char* take(size_t bytes) {
     char* q = p;
     p += align256(bytes);
     return q;
-  };
-  SegWs w;
-  w.start = (int*)take((size_t)B * (V + 1) * 4);
-  w.vinv = (float*)take((size_t)B * V * 4);
-  w.rank = (int*)take((size_t)B * n * 4);
-  w.skey = (int*)take((size_t)B * n * 4);
-  w.ws8 = taps == 8 ? (float*)take((size_t)B * n * 8 * 4) : nullptr;
-  w.units = (int4*)take((size_t)B * umax * 16);
-  w.tinfo = (int2*)take((size_t)B * tiles * 8);
-  w.nunits = (int*)take((size_t)B * 4);
-  w.xs = (float*)take((size_t)B * n * std::max(C, 1) * 4);
-  w.partial = (float*)take((size_t)B * (umax - tiles) * std::max(C, 1) * kTV * 4);
-  w.sort = take(seg_sort_stable_ws(B, n, V));
+  }
+};
+inline SegPlan seg_plan_carve(void* mem, int B, int n, int V, int taps) {
+  const int umax = seg_umax(n, V, taps), tiles = seg_tiles(V);
+  SegCarver c{(char*)mem};
+  SegPlan w;
+  w.start = (int*)c.take((size_t)B * (V + 1) * 4);
+  w.vinv = (float*)c.take((size_t)B * V * 4);
+  w.rank = (int*)c.take((size_t)B * n * 4);
+  w.skey = (int*)c.take((size_t)B * n * 4);
+  w.ws8 = taps == 8 ? (float*)c.take((size_t)B * n * 8 * 4) : nullptr;
+  w.units = (int4*)c.take((size_t)B * umax * 16);
+  w.tinfo = (int2*)c.take((size_t)B * tiles * 8);
+  w.nunits = (int*)c.take((size_t)B * 4);
+  w.sort = c.take(seg_sort_stable_ws(B, n, V));
+  return w;
+}
+inline SegApplyWs seg_apply_carve(void* mem, int B, int C, int n, int V, int taps) {
+  const int umax = seg_umax(n, V, taps), tiles = seg_tiles(V);
+  SegCarver c{(char*)mem};
+  SegApplyWs w;
+  w.xs = (float*)c.take((size_t)B * n * std::max(C, 1) * 4);
+  w.partial = (float*)c.take((size_t)B * (umax - tiles) * std::max(C, 1) * kTV * 4);
   return w;
 }
 
-// out[b, c, v] = sum over items i whose key (+ stencil offset) is v of the tap term.
-//   key: ints at key + b*key_bstride (first n used); cnt_out: [b, V] counts are
-//   written there when non-null; avg: scale by 1/cnt[v] (average pooling);
-//   tapw: [b, 8, n] trilinear weights (TAPS == 8).
+// The plan of a scatter over items with keys at key + b*key_bstride (first n
+// used): the stable sort (+ cnt_out [b, V] counts when non-null; 1/cnt when
+// avg), the work units and the sorted keys / tap weights (tapw [b, 8, n] for
+// TAPS == 8).
 template <int TAPS>
-inline int seg_scatter(const float* in, const int* key, long long key_bstride, bool avg,
-                       const float* tapw, int r, int B, int C, int n, int V, int* cnt_out,
-                       float* out, void* ws, hipStream_t st, const char* what) {
-  if (B == 0 || V == 0) return PCFM_OK;
-  SegWs w = seg_ws_carve(ws, B, C, n, V, TAPS);
+inline int seg_plan_build(const int* key, long long key_bstride, bool avg, const float* tapw,
+                          int r, int B, int n, int V, int* cnt_out, const SegPlan& w,
+                          hipStream_t st) {
 #ifdef PCFM_SORT_ROCPRIM
   int e = seg_sort_stable(key, key_bstride, B, n, V, w.start, cnt_out, avg ? w.vinv : nullptr,
                           w.rank, w.sort, st);
@@ -708,23 +749,50 @@ inline int seg_scatter(const float* in, const int* key, long long key_bstride, b
                      key, key_bstride, n, V, seg_sort_span(V), w.start, cnt_out,
                      avg ? w.vinv : nullptr, w.rank);
 #endif
-  if (C == 0) return check_launch(what);
-  const int tiles = seg_tiles(V), umax = seg_umax(n, V, TAPS), slots = umax - tiles;
+  const int tiles = seg_tiles(V), umax = seg_umax(n, V, TAPS);
   hipLaunchKernelGGL(seg_units_kernel<TAPS>, dim3(B), dim3(1024), 0, st, w.start, V, r, tiles,
                      umax, w.units, w.tinfo, w.nunits);
   if (n > 0)
+    hipLaunchKernelGGL(seg_plan_rows_kernel, dim3(ceil_div(n, 256), B), dim3(256), 0, st, w.rank,
+                       key, key_bstride, TAPS == 8 ? tapw : nullptr, n, w.skey, w.ws8);
+  return PCFM_OK;
+}
+
+// out[b, c, v] = sum over items i whose key (+ stencil offset) is v of the tap
+// term, on a built plan (avg: scaled by the plan's 1/cnt).
+template <int TAPS>
+inline int seg_apply(const float* in, const SegPlan& w, bool avg, int r, int B, int C, int n,
+                     int V, float* out, const SegApplyWs& aw, hipStream_t st) {
+  if (C == 0) return PCFM_OK;
+  const int tiles = seg_tiles(V), umax = seg_umax(n, V, TAPS), slots = umax - tiles;
+  if (n > 0)
     hipLaunchKernelGGL(seg_rows_kernel,
                        dim3(ceil_div(n, kRowsItems), kRowsAllC ? 1 : ceil_div(C, 64), B),
-                       dim3(256), 0,
-                       st, in, w.rank, key, key_bstride, TAPS == 8 ? tapw : nullptr, C, n, w.xs,
-                       w.skey, w.ws8);
+                       dim3(256), 0, st, in, w.rank, nullptr, 0LL, nullptr, C, n, aw.xs, nullptr,
+                       nullptr);
   const int gx = ceil_div(umax, kUnitWaves);
   hipLaunchKernelGGL(seg_unit_gather_kernel<TAPS>, dim3(gx, ceil_div(C, 64), B),
-                     dim3(kUnitWaves * 64), 0, st, w.xs, w.skey, w.ws8, w.start,
+                     dim3(kUnitWaves * 64), 0, st, aw.xs, w.skey, w.ws8, w.start,
                      avg ? w.vinv : nullptr, w.units, w.nunits, C, n, V, r, umax, slots, out,
-                     w.partial);
+                     aw.partial);
   hipLaunchKernelGGL(seg_part_sum_kernel, dim3(tiles, ceil_div(C, 64), B), dim3(256), 0, st,
-                     w.tinfo, w.partial, C, V, tiles, slots, out);
+                     w.tinfo, aw.partial, C, V, tiles, slots, out);
+  return PCFM_OK;
+}
+
+// plan + apply in one workspace (seg_ws_bytes): the unshared scatter.
+template <int TAPS>
+inline int seg_scatter(const float* in, const int* key, long long key_bstride, bool avg,
+                       const float* tapw, int r, int B, int C, int n, int V, int* cnt_out,
+                       float* out, void* ws, hipStream_t st, const char* what) {
+  if (B == 0 || V == 0) return PCFM_OK;
+  const SegPlan w = seg_plan_carve(ws, B, n, V, TAPS);
+  const SegApplyWs aw =
+      seg_apply_carve((char*)ws + seg_plan_bytes(B, n, V, TAPS), B, C, n, V, TAPS);
+  int e = seg_plan_build<TAPS>(key, key_bstride, avg, tapw, r, B, n, V, cnt_out, w, st);
+  if (e) return e;
+  e = seg_apply<TAPS>(in, w, avg, r, B, C, n, V, out, aw, st);
+  if (e) return e;
   return check_launch(what);
 }
 

@@ -202,6 +202,84 @@ extern "C" int pcfm_trilinear_devoxelize_scale_add_fwd(const float* coords, cons
                        "trilinear_devoxelize_scale_add_fwd", epi);
 }
 
+// ---------------------------------------------------------------------------
+// Segment plans (include/pcfm.h): the scatter's sort + work units built once
+// and applied to every feature tensor over the same points.
+// ---------------------------------------------------------------------------
+static bool plan_taps_ok(int taps) { return taps == 1 || taps == 8; }
+
+extern "C" size_t pcfm_seg_plan_bytes(int b, int n, int r, int taps) {
+  int s = 0;
+  if (b < 0 || n < 0 || !cube_fits(r, &s) || !plan_taps_ok(taps)) return 0;
+  return seg_plan_bytes(b, n, s, taps);
+}
+
+extern "C" size_t pcfm_seg_apply_workspace_bytes(int b, int c, int n, int r, int taps) {
+  int s = 0;
+  if (b < 0 || c < 0 || n < 0 || !cube_fits(r, &s) || !plan_taps_ok(taps)) return 0;
+  return seg_apply_bytes(b, c, n, s, taps);
+}
+
+extern "C" int pcfm_avg_voxelize_plan(const int* coords, int b, int n, int r, int* ind, int* cnt,
+                                      void* plan, size_t plan_bytes, void* stream) {
+  int s = 0;
+  PCFM_CHECK_ARG(b >= 0 && n >= 0, "avg_voxelize_plan: negative size b=%d n=%d", b, n);
+  PCFM_CHECK_ARG(cube_fits(r, &s), "avg_voxelize_plan: bad resolution %d", r);
+  PCFM_CHECK_ARG(plan != nullptr && plan_bytes >= seg_plan_bytes(b, n, s, 1),
+                 "avg_voxelize_plan: plan buffer too small");
+  if (b == 0) return PCFM_OK;
+  hipStream_t st = (hipStream_t)stream;
+  if (n > 0)
+    hipLaunchKernelGGL(vox_ind_kernel, dim3(ceil_div(n, 256), b), dim3(256), 0, st, coords, n, r,
+                       ind);
+  const int e = seg_plan_build<1>(ind, n, true, nullptr, r, b, n, s, cnt,
+                                  seg_plan_carve(plan, b, n, s, 1), st);
+  return e ? e : check_launch("avg_voxelize_plan");
+}
+
+extern "C" int pcfm_avg_voxelize_fwd_planned(const float* feat, const void* plan, int b, int c,
+                                             int n, int r, float* out, void* ws, size_t ws_bytes,
+                                             void* stream) {
+  int s = 0;
+  PCFM_CHECK_ARG(b >= 0 && c >= 0 && n >= 0, "avg_voxelize_fwd_planned: negative size");
+  PCFM_CHECK_ARG(cube_fits(r, &s), "avg_voxelize_fwd_planned: bad resolution %d", r);
+  PCFM_CHECK_ARG(plan != nullptr && ws_bytes >= seg_apply_bytes(b, c, n, s, 1),
+                 "avg_voxelize_fwd_planned: workspace too small");
+  if (b == 0) return PCFM_OK;
+  const int e = seg_apply<1>(feat, seg_plan_carve(const_cast<void*>(plan), b, n, s, 1), true, r, b,
+                             c, n, s, out, seg_apply_carve(ws, b, c, n, s, 1), (hipStream_t)stream);
+  return e ? e : check_launch("avg_voxelize_fwd_planned");
+}
+
+extern "C" int pcfm_trilinear_devoxelize_bwd_plan(const int* inds, const float* wgts, int b, int n,
+                                                  int r, void* plan, size_t plan_bytes,
+                                                  void* stream) {
+  int s = 0;
+  PCFM_CHECK_ARG(b >= 0 && n >= 0, "trilinear_devoxelize_bwd_plan: negative size");
+  PCFM_CHECK_ARG(cube_fits(r, &s), "trilinear_devoxelize_bwd_plan: bad resolution %d", r);
+  PCFM_CHECK_ARG(plan != nullptr && plan_bytes >= seg_plan_bytes(b, n, s, 8),
+                 "trilinear_devoxelize_bwd_plan: plan buffer too small");
+  if (b == 0) return PCFM_OK;
+  const int e = seg_plan_build<8>(inds, 8LL * n, false, wgts, r, b, n, s, nullptr,
+                                  seg_plan_carve(plan, b, n, s, 8), (hipStream_t)stream);
+  return e ? e : check_launch("trilinear_devoxelize_bwd_plan");
+}
+
+extern "C" int pcfm_trilinear_devoxelize_bwd_planned(const float* grad_y, const void* plan, int b,
+                                                     int c, int n, int r, float* grad_x, void* ws,
+                                                     size_t ws_bytes, void* stream) {
+  int s = 0;
+  PCFM_CHECK_ARG(b >= 0 && c >= 0 && n >= 0, "trilinear_devoxelize_bwd_planned: negative size");
+  PCFM_CHECK_ARG(cube_fits(r, &s), "trilinear_devoxelize_bwd_planned: bad resolution %d", r);
+  PCFM_CHECK_ARG(plan != nullptr && ws_bytes >= seg_apply_bytes(b, c, n, s, 8),
+                 "trilinear_devoxelize_bwd_planned: workspace too small");
+  if (b == 0) return PCFM_OK;
+  const int e = seg_apply<8>(grad_y, seg_plan_carve(const_cast<void*>(plan), b, n, s, 8), false,
+                             r, b, c, n, s, grad_x, seg_apply_carve(ws, b, c, n, s, 8),
+                             (hipStream_t)stream);
+  return e ? e : check_launch("trilinear_devoxelize_bwd_planned");
+}
+
 extern "C" int pcfm_rows_dot(const float* a, const float* b, long long rows, int len, float scale,
                              float* out, void* stream) {
   PCFM_CHECK_ARG(rows >= 0 && rows < (1LL << 31) && len >= 0, "rows_dot: bad size %lld x %d",

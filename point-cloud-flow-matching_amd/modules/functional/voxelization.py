@@ -6,6 +6,19 @@ from torch.autograd import Function
 
 from modules.functional import backend as _be
 
+# On a HIP device the scatter runs on a shared segment plan (pcfm.plans): the
+# second PVConv block of a stage voxelizes the same points with the first
+# block's sort.
+
+
+def _voxelize(feats, vox, r):
+    if feats.is_cuda:
+        from pcfm import ops, plans
+        if plans.ENABLED:
+            plan = plans.voxel_plan(vox, r)
+            return ops.avg_voxelize_forward_planned(feats, plan), plan.ind, plan.cnt
+    return _be._backend.avg_voxelize_forward(feats, vox, r)
+
 __all__ = ["avg_voxelize", "avg_voxelize_tee"]
 
 
@@ -18,7 +31,7 @@ class AvgVoxelization(Function):
         vox = coords.int().contiguous()
         b, c = feats.shape[0], feats.shape[1]
         r = int(resolution)
-        grid, ind, cnt = _be._backend.avg_voxelize_forward(feats, vox, r)
+        grid, ind, cnt = _voxelize(feats, vox, r)
         ctx.save_for_backward(ind, cnt)
         return grid.view(b, c, r, r, r)
 
@@ -45,7 +58,7 @@ class AvgVoxelizationTee(Function):
         vox = coords.int().contiguous()
         b, c = feats.shape[0], feats.shape[1]
         r = int(resolution)
-        grid, ind, cnt = _be._backend.avg_voxelize_forward(feats, vox, r)
+        grid, ind, cnt = _voxelize(feats, vox, r)
         ctx.save_for_backward(ind, cnt)
         return grid.view(b, c, r, r, r), features.view_as(features)
 

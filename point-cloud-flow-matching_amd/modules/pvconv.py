@@ -44,25 +44,38 @@ class _SEDevoxAdd(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, grid, coords, pf, w1, w2, r, training):
-        from pcfm import ops
+        from pcfm import ops, plans
         b, c = grid.shape[0], grid.shape[1]
         v = grid[0, 0].numel()
         rows = grid.contiguous().view(b * c, v)
         m = ops.rows_dot(rows, None, 1.0 / v).view(b, c)
         s = _se_scale(m, w1, w2).contiguous()
-        out, inds, wgts = ops.trilinear_devoxelize_scale_add(r, training, coords, rows.view(
-            b, c, v), s, pf)
+        # the corner indices / weights depend on the points only: the second
+        # block of a stage reuses the first one's (pcfm.plans) and skips writing
+        shared = plans.devox_corners(coords, r) if training else None
+        out, inds, wgts = ops.trilinear_devoxelize_scale_add(
+            r, training and shared is None, coords, rows.view(b, c, v), s, pf)
+        if shared is not None:
+            inds, wgts = shared
+        elif training:
+            plans.put_devox_corners(coords, r, inds, wgts)
         if training:
             ctx.save_for_backward(rows, inds, wgts, m, s, w1, w2)
             ctx.r, ctx.shape = r, grid.shape
+            ctx.points = coords  # key of the shared backward plan (pcfm.plans)
         return out
 
     @staticmethod
     def backward(ctx, dout):
         from pcfm import ops
+        from pcfm import plans
         rows, inds, wgts, m, s, w1, w2 = ctx.saved_tensors
         dout = dout.contiguous()
-        g = ops.trilinear_devoxelize_backward(dout, inds, wgts, ctx.r).view_as(rows)
+        if plans.ENABLED:
+            plan = plans.devox_bwd_plan(ctx.points, inds, wgts, ctx.r)
+            g = ops.trilinear_devoxelize_backward_planned(dout, plan).view_as(rows)
+        else:
+            g = ops.trilinear_devoxelize_backward(dout, inds, wgts, ctx.r).view_as(rows)
         ds = ops.rows_dot(rows, g, 1.0).view_as(s)
         with torch.enable_grad():
             m_ = m.detach().requires_grad_(True)

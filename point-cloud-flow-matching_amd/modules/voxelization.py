@@ -30,16 +30,20 @@ class Voxelization(nn.Module):
             unit = (centred + 1) / 2.0
         return torch.clamp(unit * self.r, 0, self.r - 1)
 
+    def _coords(self, coords):
+        # shared per points on a HIP device (pcfm.plans): a stage's PVConv
+        # blocks normalise the same coordinates
+        from pcfm import plans
+        return plans.grid_coords(self, coords)
+
     def forward(self, features, coords):
-        norm_coords = self._grid_coords(coords.detach())
-        vox_coords = torch.round(norm_coords).to(torch.int32)
+        norm_coords, vox_coords = self._coords(coords)
         return F.avg_voxelize(features, vox_coords, self.r), norm_coords
 
     def forward_tee(self, features, coords):
         """forward() plus the features passed through for a second consumer, their
         two gradients summed inside the voxelization's backward gather."""
-        norm_coords = self._grid_coords(coords.detach())
-        vox_coords = torch.round(norm_coords).to(torch.int32)
+        norm_coords, vox_coords = self._coords(coords)
         grid, feats = F.avg_voxelize_tee(features, vox_coords, self.r)
         return grid, norm_coords, feats
 

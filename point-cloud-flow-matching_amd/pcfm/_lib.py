@@ -104,13 +104,19 @@ SIGNATURES = {
                                   _P]),
     "pcfm_gn_film_res_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P,
                                   _P, _P, _Z, _P]),
+    "pcfm_seg_plan_bytes": (_Z, [_I, _I, _I, _I]),
+    "pcfm_seg_apply_workspace_bytes": (_Z, [_I, _I, _I, _I, _I]),
+    "pcfm_avg_voxelize_plan": (_I, [_P, _I, _I, _I, _P, _P, _P, _Z, _P]),
+    "pcfm_avg_voxelize_fwd_planned": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, _Z, _P]),
+    "pcfm_trilinear_devoxelize_bwd_plan": (_I, [_P, _P, _I, _I, _I, _P, _Z, _P]),
+    "pcfm_trilinear_devoxelize_bwd_planned": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, _Z, _P]),
     "pcfm_adamw_chunk_elems": (_I, []),
     "pcfm_adamw_workspace_bytes": (_Z, [_I]),
     "pcfm_adamw_grad_norm": (_I, [_P, _I, _P, _I, _P, _F, _P, _P, _P, _Z, _P]),
     "pcfm_adamw_ema_step": (_I, [_P, _P, _I, _P, _P, _I, _DP, _DP, _D, _D, _D, _D, _P]),
 }
 
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 _lock = threading.Lock()
 _lib = None

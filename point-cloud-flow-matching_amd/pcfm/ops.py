@@ -266,6 +266,80 @@ def trilinear_devoxelize_scale_add(r: int, is_training: bool, coords: torch.Tens
     return [outs, inds, wgts]
 
 
+# --------------------------------------------------------------------------
+# segment plans (include/pcfm.h): the sort + work units of a scatter, built
+# once per (points, resolution) and applied to several feature tensors
+# --------------------------------------------------------------------------
+class SegPlan:
+    """A device-resident segment plan; `ind` / `cnt` for a voxelization plan."""
+
+    __slots__ = ("buf", "b", "n", "r", "taps", "ind", "cnt")
+
+    def __init__(self, buf, b, n, r, taps, ind=None, cnt=None):
+        self.buf, self.b, self.n, self.r, self.taps = buf, b, n, r, taps
+        self.ind, self.cnt = ind, cnt
+
+
+def avg_voxelize_plan(coords: torch.Tensor, resolution: int) -> SegPlan:
+    """Voxelization plan of integer coords (b, 3, n); plan.ind (b, n) and
+    plan.cnt (b, r^3) are avg_voxelize_forward's ind / cnt."""
+    _check(coords, "coords", "i")
+    b, n = coords.shape[0], coords.shape[2]
+    r = int(resolution)
+    dev = coords.device
+    ind = torch.empty((b, n), dtype=torch.int32, device=dev)
+    cnt = torch.empty((b, r ** 3), dtype=torch.int32, device=dev)
+    buf = _workspace(_lib.query("pcfm_seg_plan_bytes", b, n, r, 1), coords)
+    with _timed("avg_voxelize_plan", 4 * b * (3 * n + 3 * n + 2 * r ** 3), coords):
+        _lib.call("pcfm_avg_voxelize_plan", _ptr(coords), b, n, r, _ptr(ind), _ptr(cnt), _ptr(buf),
+                  buf.numel(), _stream(coords))
+    return SegPlan(buf, b, n, r, 1, ind, cnt)
+
+
+def avg_voxelize_forward_planned(features: torch.Tensor, plan: SegPlan) -> torch.Tensor:
+    """avg_voxelize_forward's `out` (b, c, r^3) on a voxelization plan."""
+    _check(features, "features", "f")
+    b, c, n = features.shape
+    if plan.taps != 1 or (b, n) != (plan.b, plan.n):
+        raise ValueError("avg_voxelize_forward_planned: plan does not match the features")
+    r = plan.r
+    out = torch.empty((b, c, r ** 3), dtype=torch.float32, device=features.device)
+    ws = _workspace(_lib.query("pcfm_seg_apply_workspace_bytes", b, c, n, r, 1), features)
+    with _timed("avg_voxelize_fwd", 4 * b * (c * n + c * r ** 3), features):
+        _lib.call("pcfm_avg_voxelize_fwd_planned", _ptr(features), _ptr(plan.buf), b, c, n, r,
+                  _ptr(out), _ptr(ws), ws.numel(), _stream(features))
+    return out
+
+
+def trilinear_devoxelize_backward_plan(indices: torch.Tensor, weights: torch.Tensor,
+                                       r: int) -> SegPlan:
+    """Devoxelization-backward plan from the forward's inds / wgts (b, 8, n)."""
+    _check(indices, "indices", "i")
+    _check(weights, "weights", "f")
+    b, n = indices.shape[0], indices.shape[2]
+    r = int(r)
+    buf = _workspace(_lib.query("pcfm_seg_plan_bytes", b, n, r, 8), indices)
+    with _timed("trilinear_devoxelize_bwd_plan", 4 * b * 16 * n * 2, indices):
+        _lib.call("pcfm_trilinear_devoxelize_bwd_plan", _ptr(indices), _ptr(weights), b, n, r,
+                  _ptr(buf), buf.numel(), _stream(indices))
+    return SegPlan(buf, b, n, r, 8)
+
+
+def trilinear_devoxelize_backward_planned(grad_y: torch.Tensor, plan: SegPlan) -> torch.Tensor:
+    """trilinear_devoxelize_backward's grad_x (b, c, r^3) on a devoxelization plan."""
+    _check(grad_y, "grad_y", "f")
+    b, c, n = grad_y.shape
+    if plan.taps != 8 or (b, n) != (plan.b, plan.n):
+        raise ValueError("trilinear_devoxelize_backward_planned: plan does not match grad_y")
+    r = plan.r
+    grad_x = torch.empty((b, c, r ** 3), dtype=torch.float32, device=grad_y.device)
+    ws = _workspace(_lib.query("pcfm_seg_apply_workspace_bytes", b, c, n, r, 8), grad_y)
+    with _timed("trilinear_devoxelize_bwd", 4 * b * (c * n + c * r ** 3), grad_y):
+        _lib.call("pcfm_trilinear_devoxelize_bwd_planned", _ptr(grad_y), _ptr(plan.buf), b, c, n,
+                  r, _ptr(grad_x), _ptr(ws), ws.numel(), _stream(grad_y))
+    return grad_x
+
+
 def rows_dot(a: torch.Tensor, b, scale: float = 1.0) -> torch.Tensor:
     """scale * sum over the last axis of a * b (b None: of a) for 2-D (rows, len)."""
     _check(a, "a", "f")

@@ -95,7 +95,75 @@ def test_pvconv_voxelize_tee_matches_separate_grads(ops, monkeypatch):
 
     monkeypatch.setattr(Voxelization, "forward_tee", plain)
     o0, g0 = run()
-    # the voxelization's scatter sums are order-nondeterministic at the last bit
-    # (segsum.hpp, like the reference's float atomics): compare at fp32 rounding
+    # same sums, the point-branch add done in another kernel: fp32 rounding
     assert _rel(o1, o0) < 1e-4
     assert _rel(g1, g0) < 1e-4
+
+
+@pytest.mark.parametrize("c,r,n", [(64, 8, 3000), (128, 32, 20000), (256, 16, 777)])
+def test_planned_scatters_match_one_shot(ops, c, r, n):
+    """Plan + apply (include/pcfm.h segment plans) == the one-shot scatters, bit
+    for bit (same sort, same units, same fixed-order sums)."""
+    g = torch.Generator(device="cuda").manual_seed(c + r)
+    b = 3
+    pts = torch.randn(b, 3, n, device="cuda", generator=g) * 0.3 + 0.5
+    nc = torch.clamp(pts * r, 0, r - 1)
+    vc = torch.round(nc).to(torch.int32)
+    feat = torch.randn(b, c, n, device="cuda", generator=g)
+    out0, ind0, cnt0 = ops.avg_voxelize_forward(feat, vc, r)
+    plan = ops.avg_voxelize_plan(vc, r)
+    assert torch.equal(plan.ind, ind0) and torch.equal(plan.cnt, cnt0)
+    assert torch.equal(ops.avg_voxelize_forward_planned(feat, plan), out0)
+    feat2 = torch.randn(b, c // 2, n, device="cuda", generator=g)  # the plan is C-free
+    assert torch.equal(ops.avg_voxelize_forward_planned(feat2, plan),
+                       ops.avg_voxelize_forward(feat2, vc, r)[0])
+    grid = torch.randn(b, c, r ** 3, device="cuda", generator=g)
+    _, inds, wgts = ops.trilinear_devoxelize_forward(r, True, nc, grid)
+    gy = torch.randn(b, c, n, device="cuda", generator=g)
+    ref = ops.trilinear_devoxelize_backward(gy, inds, wgts, r)
+    dplan = ops.trilinear_devoxelize_backward_plan(inds, wgts, r)
+    assert torch.equal(ops.trilinear_devoxelize_backward_planned(gy, dplan), ref)
+    assert torch.equal(ops.trilinear_devoxelize_backward_planned(gy * 2.0, dplan), ref * 2.0)
+
+
+def test_stage_blocks_share_plans(ops, monkeypatch):
+    """A hybrid stage (1x1 lift + two PV blocks on the same points): the second
+    block reuses the first one's grid coordinates, voxelization plan, corner
+    indices and devoxelization-backward plan -- one plan build per kind per
+    stage -- with outputs and gradients identical to building them per block."""
+    from pcfm import plans
+    from pcfm.models import _PVStage
+    torch.manual_seed(4)
+    st = _PVStage(64, 128, 2, 16, emb_dim=32, with_se=True).cuda().train()
+    state = {k: v.clone() for k, v in st.state_dict().items()}
+    feat = torch.randn(2, 64, 6000, device="cuda")
+    coords = torch.randn(2, 3, 6000, device="cuda")
+    emb = torch.randn(2, 32, device="cuda")
+    gy = torch.randn(2, 128, 6000, device="cuda")
+    builds = {"vox": 0, "devox": 0}
+    vplan, dplan = ops.avg_voxelize_plan, ops.trilinear_devoxelize_backward_plan
+
+    def count(kind, fn):
+        def wrapped(*a, **k):
+            builds[kind] += 1
+            return fn(*a, **k)
+        return wrapped
+    monkeypatch.setattr(ops, "avg_voxelize_plan", count("vox", vplan))
+    monkeypatch.setattr(ops, "trilinear_devoxelize_backward_plan", count("devox", dplan))
+
+    def run(enabled):
+        monkeypatch.setattr(plans, "ENABLED", enabled)
+        st.load_state_dict(state)
+        f = feat.clone().requires_grad_(True)
+        out, _ = st(f, coords, emb)
+        out.backward(gy)
+        grads = [f.grad] + [p.grad.clone() for p in st.parameters()]
+        st.zero_grad(set_to_none=True)
+        return out.detach(), grads
+
+    o1, g1 = run(True)
+    assert builds == {"vox": 1, "devox": 1}
+    o0, g0 = run(False)
+    assert torch.equal(o1, o0)
+    for a, b in zip(g1, g0):
+        assert torch.equal(a, b)
