@@ -118,7 +118,8 @@ def summarize(dfetch, dwrite):
         fb = sum(v for _, v in fs) / K * corr
         wb = sum(v for _, v in ws) / K
         res[f"{op}@C{c}R{r}"] = {"fetch_bytes": fb, "write_bytes": wb, "traffic_bytes": fb + wb}
-    return {"fetch_correction": corr, "calibration": "seg_rows reads B*C*N*4 bytes",
+    return {"batch": B, "points": N,
+            "fetch_correction": corr, "calibration": "seg_rows reads B*C*N*4 bytes",
             "shapes": f"B={B} N={N} randn coords through Voxelization normalisation",
             "ops": res}
 
