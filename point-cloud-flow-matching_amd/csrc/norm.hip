@@ -161,6 +161,18 @@ __device__ __forceinline__ void bn_bwd_fin(const float* part, int P, int c, floa
 // y = act((x - mean) * invstd * gamma + beta), kApplyU float4 per thread;
 // grid = (bn_apply_blocks(S), B * C).  Thread 0 derives the channel's
 // statistics from the P partials once per block (LDS broadcast).
+// The backward apply passes walk their blocks in REVERSE of the statistics
+// pass's order (which reads the last batch element last): the rows read most
+// recently are the ones still in the 256 MiB Infinity Cache (A/B on MI355X,
+// tools/bn_ab.py: 158 -> 147 us at B8 C256 S20000, 123 -> 112 us at C128
+// S32768; the forward apply, at 6.4 TB/s already, does not gain).
+#ifndef PCFM_BN_REV
+#define PCFM_BN_REV 1
+#endif
+__device__ __forceinline__ unsigned bn_rev(unsigned i, unsigned n) {
+  return PCFM_BN_REV ? n - 1 - i : i;
+}
+
 #ifndef PCFM_BN_APPLY_U
 #define PCFM_BN_APPLY_U 4
 #endif
@@ -178,19 +190,20 @@ __global__ void __launch_bounds__(256)
                         const float* __restrict__ beta, int C, int S4, float slope,
                         float* __restrict__ y) {
   __shared__ float st[2];
-  const int c = (int)(blockIdx.y % C);
+  const unsigned row = blockIdx.y, bx = blockIdx.x;
+  const int c = (int)(row % C);
   if (threadIdx.x == 0) {
     float m, is, var;
     double n;
     fin.get(x, c, m, is, var, n);
-    if (blockIdx.x == 0 && blockIdx.y < (unsigned)C) fin.publish(c, m, is, var, n, mean, invstd);
+    if (bx == 0 && row < (unsigned)C) fin.publish(c, m, is, var, n, mean, invstd);
     st[0] = m;
     st[1] = is;
   }
   const float g = gamma[c], bt = beta[c];
-  const float4* __restrict__ x4 = reinterpret_cast<const float4*>(x) + (size_t)blockIdx.y * S4;
-  float4* __restrict__ y4 = reinterpret_cast<float4*>(y) + (size_t)blockIdx.y * S4;
-  const int s0 = blockIdx.x * 256 * kApplyU + threadIdx.x;
+  const float4* __restrict__ x4 = reinterpret_cast<const float4*>(x) + (size_t)row * S4;
+  float4* __restrict__ y4 = reinterpret_cast<float4*>(y) + (size_t)row * S4;
+  const int s0 = bx * 256 * kApplyU + threadIdx.x;
   float4 v[kApplyU];
 #pragma unroll
   for (int u = 0; u < kApplyU; ++u)
@@ -283,11 +296,12 @@ __global__ void __launch_bounds__(256)
                         float* __restrict__ rowpart) {
   __shared__ float sh[8];
   __shared__ float st[2];
-  const int c = (int)(blockIdx.y % C);
+  const unsigned row = bn_rev(blockIdx.y, gridDim.y), bx = bn_rev(blockIdx.x, gridDim.x);
+  const int c = (int)(row % C);
   if (threadIdx.x == 0) {
     float sg, sgx;
     bn_bwd_fin(part, P, c, sg, sgx);
-    if (blockIdx.x == 0 && blockIdx.y < (unsigned)C) {
+    if (bx == 0 && row < (unsigned)C) {
       dbeta[c] = sg;
       dgamma[c] = sgx;
     }
@@ -295,11 +309,11 @@ __global__ void __launch_bounds__(256)
     st[1] = sgx;
   }
   const float m = mean[c], is = invstd[c], gm = gamma[c], bt = beta[c];
-  const size_t row = (size_t)blockIdx.y * S4;
-  const float4* __restrict__ x4 = reinterpret_cast<const float4*>(x) + row;
-  const float4* __restrict__ d4 = reinterpret_cast<const float4*>(dz) + row;
-  float4* __restrict__ o4 = reinterpret_cast<float4*>(dx) + row;
-  const int s0 = blockIdx.x * 256 * kBwdU + threadIdx.x;
+  const size_t r0 = (size_t)row * S4;
+  const float4* __restrict__ x4 = reinterpret_cast<const float4*>(x) + r0;
+  const float4* __restrict__ d4 = reinterpret_cast<const float4*>(dz) + r0;
+  float4* __restrict__ o4 = reinterpret_cast<float4*>(dx) + r0;
+  const int s0 = bx * 256 * kBwdU + threadIdx.x;
   float4 v[kBwdU], d[kBwdU];
 #pragma unroll
   for (int u = 0; u < kBwdU; ++u)
@@ -328,7 +342,7 @@ __global__ void __launch_bounds__(256)
   if (rowpart != nullptr) {  // block-uniform branch: every thread takes part
     float z = 0.0f;
     block_sum2(tsum, z, sh);
-    if (threadIdx.x == 0) rowpart[(size_t)blockIdx.y * gridDim.x + blockIdx.x] = tsum;
+    if (threadIdx.x == 0) rowpart[(size_t)row * gridDim.x + bx] = tsum;
   }
 }
 
@@ -408,7 +422,8 @@ __global__ void __launch_bounds__(256)
                               uint16_t* __restrict__ yh, uint16_t* __restrict__ yl) {
   __shared__ float tile[64][65];
   __shared__ float st_m[64], st_is[64];
-  const int v0 = blockIdx.x * 64, c0 = blockIdx.y * 64, b = blockIdx.z;
+  const unsigned bx = blockIdx.x;
+  const int v0 = bx * 64, c0 = blockIdx.y * 64, b = blockIdx.z;
   const int t = threadIdx.x, w = t >> 6, lane = t & 63;
   if (t < 64) {
     float m, is, var;
@@ -416,7 +431,7 @@ __global__ void __launch_bounds__(256)
     fin.get(x, c0 + t, m, is, var, n);
     st_m[t] = m;
     st_is[t] = is;
-    if (blockIdx.x == 0 && b == 0) fin.publish(c0 + t, m, is, var, n, mean, invstd);
+    if (bx == 0 && b == 0) fin.publish(c0 + t, m, is, var, n, mean, invstd);
   }
   __syncthreads();
   const size_t rbase = ((size_t)b * C + c0) * S + v0;
@@ -442,14 +457,15 @@ __global__ void __launch_bounds__(256)
                               uint16_t* __restrict__ dxl, float* __restrict__ rowpart) {
   __shared__ float tile[64][65];
   __shared__ float st_g[64], st_gx[64];
-  const int v0 = blockIdx.x * 64, c0 = blockIdx.y * 64, b = blockIdx.z;
+  const unsigned bx = bn_rev(blockIdx.x, gridDim.x);
+  const int v0 = bx * 64, c0 = blockIdx.y * 64, b = bn_rev(blockIdx.z, gridDim.z);
   const int t = threadIdx.x, w = t >> 6, lane = t & 63;
   if (t < 64) {
     float sg, sgx;
     bn_bwd_fin(part, P, c0 + t, sg, sgx);
     st_g[t] = sg;
     st_gx[t] = sgx;
-    if (blockIdx.x == 0 && b == 0) {
+    if (bx == 0 && b == 0) {
       dbeta[c0 + t] = sg;
       dgamma[c0 + t] = sgx;
     }
@@ -481,7 +497,7 @@ __global__ void __launch_bounds__(256)
     for (int q = 0; q < 16; ++q) sum += tile[c][vq + q];
     sum += __shfl_xor(sum, 1, 64);
     sum += __shfl_xor(sum, 2, 64);
-    if ((t & 3) == 0) rowpart[((size_t)b * C + c0 + c) * (S / 64) + blockIdx.x] = sum;
+    if ((t & 3) == 0) rowpart[((size_t)b * C + c0 + c) * (S / 64) + bx] = sum;
   }
 }
 
