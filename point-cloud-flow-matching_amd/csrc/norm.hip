@@ -166,12 +166,7 @@ __device__ __forceinline__ void bn_bwd_fin(const float* part, int P, int c, floa
 // recently are the ones still in the 256 MiB Infinity Cache (A/B on MI355X,
 // tools/bn_ab.py: 158 -> 147 us at B8 C256 S20000, 123 -> 112 us at C128
 // S32768; the forward apply, at 6.4 TB/s already, does not gain).
-#ifndef PCFM_BN_REV
-#define PCFM_BN_REV 1
-#endif
-__device__ __forceinline__ unsigned bn_rev(unsigned i, unsigned n) {
-  return PCFM_BN_REV ? n - 1 - i : i;
-}
+__device__ __forceinline__ unsigned bn_rev(unsigned i, unsigned n) { return rev_order(i, n); }
 
 #ifndef PCFM_BN_APPLY_U
 #define PCFM_BN_APPLY_U 4
@@ -715,9 +710,10 @@ __global__ void __launch_bounds__(256)
                              const float* __restrict__ kc, const float* __restrict__ w,
                              const float* __restrict__ bias, int C, int G, int N4,
                              float* __restrict__ dx) {
-  const int n4 = blockIdx.x * 256 + threadIdx.x;
+  // reverse of the statistics pass's row order (Infinity-cache reuse, as BN)
+  const int n4 = bn_rev(blockIdx.x, gridDim.x) * 256 + threadIdx.x;
   if (n4 >= N4) return;
-  const int row = blockIdx.y;
+  const int row = bn_rev(blockIdx.y, gridDim.y);
   const int b = row / C, c = row - b * C, g = c / (C / G);
   const float m = mean[b * G + g], rs = rstd[b * G + g];
   const float k0 = kc[3 * (size_t)row], k1 = kc[3 * (size_t)row + 1], k2 = kc[3 * (size_t)row + 2];

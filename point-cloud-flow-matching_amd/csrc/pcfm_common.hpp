@@ -48,4 +48,13 @@ __device__ __forceinline__ double sqdist3(double dx, double dy, double dz) {
   return __builtin_fma(dz, dz, __builtin_fma(dx, dx, dy * dy));
 }
 
+// Block index walked in reverse (a second pass over data a first pass just
+// read in forward order finds its most recent rows in the Infinity Cache).
+#ifndef PCFM_REV_APPLY
+#define PCFM_REV_APPLY 1
+#endif
+__device__ __forceinline__ unsigned rev_order(unsigned i, unsigned n) {
+  return PCFM_REV_APPLY ? n - 1 - i : i;
+}
+
 }  // namespace pcfm

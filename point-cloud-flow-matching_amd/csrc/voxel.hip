@@ -70,12 +70,14 @@ __global__ void __launch_bounds__(256)
   if (threadIdx.x == 0) out[r] = (float)(red[0] * (double)scale);
 }
 
-// x[r][v] = s[r] * x[r][v] + t[r]  (in place; t may be null)
+// x[r][v] = s[r] * x[r][v] + t[r]  (in place; t may be null).  Runs after
+// rows_dot over the same rows (SE3d's backward): blocks in reverse order.
 __global__ void __launch_bounds__(256)
     rows_affine_kernel(float* __restrict__ x, const float* __restrict__ s,
                        const float* __restrict__ t, int len4, int per_row_blocks) {
-  const size_t r = blockIdx.x / per_row_blocks;
-  const int v = (blockIdx.x % per_row_blocks) * 256 + threadIdx.x;
+  const unsigned blk = rev_order(blockIdx.x, gridDim.x);
+  const size_t r = blk / per_row_blocks;
+  const int v = (blk % per_row_blocks) * 256 + threadIdx.x;
   if (v >= len4) return;
   const float sv = s[r], tv = t != nullptr ? t[r] : 0.0f;
   float4* x4 = reinterpret_cast<float4*>(x) + r * len4;
