@@ -36,7 +36,8 @@ __device__ __forceinline__ unsigned long long pack_key(float d, int idx) {
 // grid = (query blocks, splits, 2*b).  Two queries share each packed-fp32
 // instruction (v_pk_add_f32 / v_pk_mul_f32 / v_pk_fma_f32): the distance costs
 // 6 packed ops per 2 pairs, the same per-component fma chain as sqdist3 (so
-// the same bits as the oracle), leaving the compare / select per pair.
+// the same bits as the oracle); per query only each group's minimum (v_min3)
+// meets the running best, the exact index is recovered at the end.
 __global__ void __launch_bounds__(kThreads)
     nn_kernel(const float* __restrict__ xyz1, const float* __restrict__ xyz2, int b, int n, int m,
               int splits, float* __restrict__ dist1, int* __restrict__ idx1,
@@ -70,26 +71,40 @@ __global__ void __launch_bounds__(kThreads)
     bi[q] = k0;
   }
   const float* __restrict__ cb = cp + (size_t)bb * nc * 3;
-  // one candidate: the same fma chain as sqdist3 on two queries at once
-  auto visit = [&](float x, float y, float z, int k) {
-    const f2 cx = x, cy = y, cz = z;
+  // Candidates in groups of kG (wide scalar loads, the next group's issued
+  // before the current group's arithmetic).  Per query only the group MINIMUM
+  // is compared with the running best (min3 chains: ~0.5 VALU op per pair
+  // instead of a compare + two selects per pair); the running best keeps the
+  // group's first candidate index, and the exact index inside the winning
+  // group is recovered at the end by recomputing its kG distances (same fma
+  // chain, same bits) and taking the first equal one.  Strict `<` across
+  // groups and first-equal inside a group = the reference's scan order.
+  constexpr int kG = 8;
+  int gk[kQ];
+#pragma unroll
+  for (int q = 0; q < kQ; ++q) gk[q] = k0;
+  auto group = [&](const float (&c)[3 * kG], int k, int valid) {
+    f2 gm[kP];
 #pragma unroll
     for (int p = 0; p < kP; ++p) {
-      // dx = candidate - query (chamfer3D.cu:32-35); fma(dz, dz, fma(dx, dx, dy * dy))
-      const f2 dx = cx - qx[p], dy = cy - qy[p], dz = cz - qz[p];
-      const f2 d = __builtin_elementwise_fma(dz, dz, __builtin_elementwise_fma(dx, dx, dy * dy));
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        if (d[h] < best[2 * p + h]) {
-          best[2 * p + h] = d[h];
-          bi[2 * p + h] = k;
-        }
+      for (int g = 0; g < kG; ++g) {
+        const f2 cx = c[3 * g], cy = c[3 * g + 1], cz = c[3 * g + 2];
+        // dx = candidate - query (chamfer3D.cu:32-35); fma(dz, dz, fma(dx, dx, dy * dy))
+        const f2 dx = cx - qx[p], dy = cy - qy[p], dz = cz - qz[p];
+        f2 d = __builtin_elementwise_fma(dz, dz, __builtin_elementwise_fma(dx, dx, dy * dy));
+        if (g >= valid) d = __builtin_inff();  // uniform: only the ragged tail group
+        gm[p] = g == 0 ? d : __builtin_elementwise_min(gm[p], d);
       }
     }
+#pragma unroll
+    for (int q = 0; q < kQ; ++q) {
+      const float m = gm[q >> 1][q & 1];
+      const bool better = m < best[q];
+      best[q] = better ? m : best[q];
+      gk[q] = better ? k : gk[q];
+    }
   };
-  // groups of kG candidates through wide scalar loads (uniform address), the
-  // next group's loads issued before the current group's arithmetic
-  constexpr int kG = 8;
   const int kg1 = k0 + (k1 - k0) / kG * kG;
   int k = __builtin_amdgcn_readfirstlane(k0);
   if (k < kg1) {
@@ -100,13 +115,36 @@ __global__ void __launch_bounds__(kThreads)
       const int kn = k + kG < kg1 ? k + kG : k;
 #pragma unroll
       for (int e = 0; e < 3 * kG; ++e) nx[e] = cb[3 * kn + e];
-#pragma unroll
-      for (int g = 0; g < kG; ++g) visit(c[3 * g], c[3 * g + 1], c[3 * g + 2], k + g);
+      group(c, k, kG);
 #pragma unroll
       for (int e = 0; e < 3 * kG; ++e) c[e] = nx[e];
     }
   }
-  for (; k < k1; ++k) visit(cb[3 * k], cb[3 * k + 1], cb[3 * k + 2], k);
+  if (k < k1) {  // ragged tail: one partial group
+    float c[3 * kG];
+#pragma unroll
+    for (int e = 0; e < 3 * kG; ++e) c[e] = cb[3 * min(k + e / 3, k1 - 1) + e % 3];
+    group(c, k, k1 - k);
+  }
+  // exact index inside each query's winning group
+#pragma unroll
+  for (int q = 0; q < kQ; ++q) {
+    const f2 qv = {0.0f, 0.0f};
+    (void)qv;
+    const float x = qx[q >> 1][q & 1], y = qy[q >> 1][q & 1], z = qz[q >> 1][q & 1];
+    int found = gk[q];
+    bool done = false;
+    const int gend = min(gk[q] + kG, k1);
+    for (int kk = gk[q]; kk < gend; ++kk) {
+      const float ddx = cb[3 * kk] - x, ddy = cb[3 * kk + 1] - y, ddz = cb[3 * kk + 2] - z;
+      const float d = __builtin_fmaf(ddz, ddz, __builtin_fmaf(ddx, ddx, ddy * ddy));
+      if (!done && d == best[q]) {
+        found = kk;
+        done = true;
+      }
+    }
+    bi[q] = found;
+  }
   float* __restrict__ dist = dir ? dist2 : dist1;
   int* __restrict__ idx = dir ? idx2 : idx1;
   unsigned long long* __restrict__ key = dir ? key2 : key1;
@@ -429,7 +467,22 @@ __global__ void __launch_bounds__(64 * kCWaves)
     while (need) {
       const int l = __ffsll((long long)need) - 1;
       need &= need - 1;
-      if (rlf(lb, l) <= wmax) wmax = visit(g0 + l);
+      if (rlf(lb, l) > wmax) continue;
+      // finer test, per query: does the tile's box come within ANY query's own
+      // current best?  (the wave box against the wave's worst best passes whole
+      // tiles that none of the wave's queries can use -- Gaussian clouds put
+      // dense and sparse queries in one wave)
+      const int t = g0 + l;
+      const float4 blo = cbox[2 * t], bhi = cbox[2 * t + 1];
+      bool use = false;
+#pragma unroll
+      for (int j = 0; j < kCQ; ++j) {
+        const float dx = fmaxf(0.0f, fmaxf(blo.x - qx[j], qx[j] - bhi.x));
+        const float dy = fmaxf(0.0f, fmaxf(blo.y - qy[j], qy[j] - bhi.y));
+        const float dz = fmaxf(0.0f, fmaxf(blo.z - qz[j], qz[j] - bhi.z));
+        use = use || (qi[j] >= 0 && (dx * dx + dy * dy + dz * dz) * (1.0f - 1e-5f) <= best[j]);
+      }
+      if (__ballot(use)) wmax = visit(t);
     }
   }
   float* __restrict__ dist = (dir ? dist2 : dist1) + (size_t)bb * nq;
@@ -460,12 +513,13 @@ using namespace pcfm;
 
 namespace {
 // Culled search from this many pairs per batch element.  Brute force runs at
-// the VALU issue rate (~9 lane-operations per pair); the culled search scores
-// a pair at ~14 (index tie-break, lane broadcasts) and, on the randn clouds of
-// the benchmark, still visits ~30 % of the candidates at N = 20000 (a wave's
-// worst query sets its radius) but ~8 % at N = 100000: measured on MI355X,
-// C2 (8 x 20000^2) brute 1.16 ms vs culled 1.79 ms, C5 (4 x 100000^2) brute
-// 12.6 ms vs culled 5.9 ms.  PCFM_CHAMFER_CULL_PAIRS overrides the threshold
+// the VALU issue rate (~7 lane-operations per pair); the culled search scores
+// a pair at ~14 (index tie-break, lane broadcasts) and visits a fraction of
+// the candidates that depends on the cloud.  Measured on MI355X (round 2, with
+// the per-query tile test): C2 (8 x 20000^2, randn) brute 0.90 ms vs culled
+// 1.06 ms; C5 (4 x 100000^2) culled 2.25 ms (randn) / 1.51 ms (uniform) vs
+// ~11 ms brute; the reference's published 32 x 2000 x 1000: brute 0.08 ms vs
+// culled 0.38 ms.  PCFM_CHAMFER_CULL_PAIRS overrides the threshold
 // (tests force both paths on the same inputs).
 long long cull_pairs() {
   static const long long v = [] {
