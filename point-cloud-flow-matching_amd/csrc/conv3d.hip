@@ -484,13 +484,14 @@ __global__ void __launch_bounds__(512)
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's stage-s reads done
     __builtin_amdgcn_s_barrier();
 #ifndef PCFM_CONV_DMA_LATE
-#define PCFM_CONV_DMA_LATE 3  // MFMAs per LDS-DMA piece; 0: the burst after the barrier
+#define PCFM_CONV_DMA_LATE 4  // MFMAs per LDS-DMA piece; 0: the burst after the barrier
 #endif
 #if PCFM_CONV_DMA_LATE > 0
     // LDS-DMA issue (~60-185 cycles per piece) between the MFMAs instead of in
     // a burst after the barrier, where both waves of a SIMD issue theirs at the
     // same time and the MFMA pipe idles: 0.711 -> 0.694 ms (C128 R32 fwd),
-    // 0.368 -> 0.357 ms (C256 R16), tools/conv_ab.py on MI355X
+    // 0.368 -> 0.357 ms (C256 R16), tools/conv_ab.py on MI355X; 4 MFMAs per
+    // piece (over-asking the 16 left after the fragment reads): 0.680 / 0.348 ms
     glds_frags<KT>(lds, (s + 1) % kGStages, wr, wc, r, h, Fn);
     glds_mfma<KT>(Fc, acc);
     // unconditional (same basic block as the MFMAs, so the scheduler can place
