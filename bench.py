@@ -239,9 +239,13 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     ddp = world > 1
+    # one process per GPU; PCFM_DIST_BACKEND=gloo rehearses the N > 1 path with
+    # several ranks sharing the GPUs there are (dev knob; the product path is RCCL)
+    backend = os.environ.get("PCFM_DIST_BACKEND", "nccl")
+    local = local % max(1, torch.cuda.device_count())
     if ddp:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", init_method="env://")
+        dist.init_process_group(backend, init_method="env://")
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 

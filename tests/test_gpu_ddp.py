@@ -1,0 +1,36 @@
+"""GPU: the N > 1 train step (DDP, one process per rank) with this build's
+fused kernels -- shared segment plans, the fused parameter update, the
+deterministic scatters -- rehearsed with two ranks on the box's GPU over gloo
+(the product path is RCCL with one GPU per rank; the driver runs that at
+N = 2..8).  After two steps every rank must hold the same parameters
+(bit-identical: DDP broadcast them at wrap time and the all-reduced gradients
+are the same on all ranks) while the ranks' losses differ (different data).
+BatchNorm running statistics stay per rank (broadcast_buffers=False) and the
+EMA shadows start from each rank's own initialisation -- both as the
+reference (train.py:182, 232, 242-244)."""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_ddp_two_ranks_stay_in_sync(tmp_path):
+    out = tmp_path / "ddp.json"
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", "29533",
+           os.path.join(REPO, "tests", "helpers", "ddp_rank.py"), str(out)]
+    subprocess.run(cmd, check=True, timeout=240, env=env, cwd=REPO)
+    d = json.load(open(out))
+    assert d["world"] == 2 and d["backend"] == "gloo"
+    s0, s1 = np.array(d["sums"][0]), np.array(d["sums"][1])
+    assert np.all(np.isfinite(s0))
+    np.testing.assert_array_equal(s0, s1)
+    l0, l1 = d["losses"]
+    assert np.all(np.isfinite(l0)) and l0 != l1
