@@ -377,6 +377,9 @@ __global__ void __launch_bounds__(256)
 //   crowded tile write partial tiles that seg_part_sum_kernel adds in unit
 //   order.  Waves never wait for each other and nothing is atomic.
 // --------------------------------------------------------------------------
+#ifndef PCFM_SEG_XCD
+#define PCFM_SEG_XCD 1
+#endif
 #ifndef PCFM_KTV
 #define PCFM_KTV 16
 #endif
@@ -496,17 +499,35 @@ __global__ void __launch_bounds__(kUnitWaves * 64)
                            int slots, float* __restrict__ out, float* __restrict__ partial) {
   __shared__ float lds[kUnitWaves][kTV * 65];
   constexpr int NR = seg_ranges<TAPS>();
+#if PCFM_SEG_XCD
+  // XCD-contiguous deal: consecutive blocks in dispatch order go round-robin
+  // to the 8 XCDs; give each XCD a contiguous run of (unit block, channel
+  // group, batch) so a row's re-reads by the other stencil columns hit its L2
+  int bx, by, bz;
+  {
+    const int gx = (int)gridDim.x, gy = (int)gridDim.y;
+    const int tot = gx * gy * (int)gridDim.z;
+    int id = (int)(blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z));
+    const int q = tot / 8, rr = tot % 8, xcd = id % 8;
+    id = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + id / 8;
+    bx = id % gx;
+    by = (id / gx) % gy;
+    bz = id / (gx * gy);
+  }
+  const int b = bz, c0 = by * 64;
+#else
+  const int bx = blockIdx.x;
   const int b = blockIdx.z, c0 = blockIdx.y * 64;
+#endif
   // readfirstlane: the wave index is uniform, so the whole walk stays scalar
   // (no exec-mask branches, no vmcnt(0) stalls between the row loads)
   const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  // natural block order: the 4 units of a block are consecutive tiles and the
-  // tile 32 units back (stencil columns dx = 1) ran 8 blocks earlier on the
-  // same XCD, so column re-reads mostly hit L2 (an XCD-contiguous deal
-  // measured 1.5-1.9x slower)
+  // (XCD-contiguous deal vs dispatch order, tools/scatter_ab.py on MI355X:
+  // devox backward 0.183 -> 0.175 ms C128 R32, 0.235 -> 0.215 C256 R16,
+  // 0.224 -> 0.207 C256 R8; the voxelize forward unchanged)
   const int nu = nunits[b];
-  const int u = blockIdx.x * kUnitWaves + w;
+  const int u = bx * kUnitWaves + w;
   if (u >= nu) return;  // wave-uniform; no block barrier below
   const int4 un = units[(size_t)b * umax + u];
   const int tile = un.x, part = un.y, parts = un.z, T = un.w;
