@@ -406,8 +406,8 @@ size_t pcfm_bn_workspace_bytes(int b, int c, int s);
  * r = (1 - momentum) * r + momentum * stat (unbiased variance for running_var). */
 int pcfm_bn_act_fwd(const float* x, const float* gamma, const float* beta, int b, int c, int s,
                     float eps, float slope, float momentum, float* running_mean,
-                    float* running_var, float* y, float* mean, float* invstd, void* ws,
-                    size_t ws_bytes, void* stream);
+                    float* running_var, long long* num_batches_tracked, float* y, float* mean,
+                    float* invstd, void* ws, size_t ws_bytes, void* stream);
 
 /* Backward of pcfm_bn_act_fwd given dz = dL/dy: dx [b][c][s] and
  * dgamma / dbeta [c] (all fully written); if dbias_in is non-NULL it receives
@@ -423,8 +423,8 @@ int pcfm_bn_act_bwd(const float* dz, const float* x, const float* gamma, const f
  * as fp32.  Workspace: pcfm_bn_workspace_bytes(b, c, s). */
 int pcfm_bn_act_fwd_split(const float* x, const float* gamma, const float* beta, int b, int c,
                           int s, float eps, float slope, float momentum, float* running_mean,
-                          float* running_var, void* ys, float* mean, float* invstd, void* ws,
-                          size_t ws_bytes, void* stream);
+                          float* running_var, long long* num_batches_tracked, void* ys,
+                          float* mean, float* invstd, void* ws, size_t ws_bytes, void* stream);
 
 /* pcfm_bn_act_bwd for a voxel convolution's output x [b][c][s] (c, s multiples
  * of 64) whose dx only feeds that convolution's backward: dx is written

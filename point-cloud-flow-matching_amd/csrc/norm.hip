@@ -124,6 +124,7 @@ struct BnFwdFin {
   float eps, momentum;
   float* rmean;
   float* rvar;
+  long long* nbt;  // BatchNorm num_batches_tracked (+1 by channel 0's publisher), or NULL
   __device__ __forceinline__ void get(const float* x, int c, float& m, float& is, float& var,
                                       double& n) const {
     float s = 0.0f, q = 0.0f;
@@ -146,6 +147,7 @@ struct BnFwdFin {
       rmean[c] = (1.0f - momentum) * rmean[c] + momentum * m;
       rvar[c] = (1.0f - momentum) * rvar[c] + momentum * (float)(var * n / (n - 1.0));
     }
+    if (nbt != nullptr && c == 0) nbt[0] += 1;
   }
 };
 __device__ __forceinline__ void bn_bwd_fin(const float* part, int P, int c, float& sg,
@@ -763,8 +765,9 @@ extern "C" size_t pcfm_bn_workspace_bytes(int b, int c, int s) {
 
 extern "C" int pcfm_bn_act_fwd(const float* x, const float* gamma, const float* beta, int b, int c,
                                int s, float eps, float slope, float momentum, float* running_mean,
-                               float* running_var, float* y, float* mean, float* invstd, void* ws,
-                               size_t ws_bytes, void* stream) {
+                               float* running_var, long long* num_batches_tracked, float* y,
+                               float* mean, float* invstd, void* ws, size_t ws_bytes,
+                               void* stream) {
   PCFM_CHECK_ARG(bn_ok(b, c, s), "bn_act_fwd: bad shape b=%d c=%d s=%d (s %% 4 == 0 needed)", b,
                  c, s);
   PCFM_CHECK_ARG(ws_bytes >= pcfm_bn_workspace_bytes(b, c, s), "bn_act_fwd: workspace too small");
@@ -773,7 +776,9 @@ extern "C" int pcfm_bn_act_fwd(const float* x, const float* gamma, const float* 
   hipStream_t st = (hipStream_t)stream;
   float* part = (float*)ws;
   hipLaunchKernelGGL(bn_stats_kernel, dim3(c, bn_parts(b)), dim3(256), 0, st, x, b, c, s, part);
-  const BnFwdFin fin{part, b, s, bn_parts(b), eps, momentum, running_mean, running_var};
+  const BnFwdFin fin{part,         b,           s,
+                     bn_parts(b),  eps,         momentum,
+                     running_mean, running_var, num_batches_tracked};
   hipLaunchKernelGGL(bn_act_apply_kernel, dim3(bn_apply_blocks(s), b * c), dim3(256), 0, st, x,
                      fin, mean, invstd, gamma, beta, c, s / 4, slope, y);
   return check_launch("bn_act_fwd");
@@ -803,9 +808,9 @@ extern "C" int pcfm_bn_act_bwd(const float* dz, const float* x, const float* gam
 
 extern "C" int pcfm_bn_act_fwd_split(const float* x, const float* gamma, const float* beta, int b,
                                      int c, int s, float eps, float slope, float momentum,
-                                     float* running_mean, float* running_var, void* ys,
-                                     float* mean, float* invstd, void* ws, size_t ws_bytes,
-                                     void* stream) {
+                                     float* running_mean, float* running_var,
+                                     long long* num_batches_tracked, void* ys, float* mean,
+                                     float* invstd, void* ws, size_t ws_bytes, void* stream) {
   PCFM_CHECK_ARG(bn_ok(b, c, s) && c % 64 == 0 && s % 64 == 0 && (long long)b < 65536,
                  "bn_act_fwd_split: bad shape b=%d c=%d s=%d (c, s multiples of 64)", b, c, s);
   PCFM_CHECK_ARG(ws_bytes >= pcfm_bn_workspace_bytes(b, c, s), "bn_act_fwd_split: workspace too small");
@@ -814,7 +819,9 @@ extern "C" int pcfm_bn_act_fwd_split(const float* x, const float* gamma, const f
   hipStream_t st = (hipStream_t)stream;
   float* part = (float*)ws;
   hipLaunchKernelGGL(bn_stats_kernel, dim3(c, bn_parts(b)), dim3(256), 0, st, x, b, c, s, part);
-  const BnFwdFin fin{part, b, s, bn_parts(b), eps, momentum, running_mean, running_var};
+  const BnFwdFin fin{part,         b,           s,
+                     bn_parts(b),  eps,         momentum,
+                     running_mean, running_var, num_batches_tracked};
   uint16_t* yh = (uint16_t*)ys;
   hipLaunchKernelGGL(bn_act_apply_split_kernel, dim3(s / 64, c / 64, b), dim3(256), 0, st, x,
                      fin, mean, invstd, gamma, beta, c, s, slope, yh,

@@ -17,10 +17,10 @@ __all__ = ["bn_act", "conv_bn_act", "gn_film_residual"]
 
 class _BNAct(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, running_mean, running_var, eps, momentum, slope):
+    def forward(ctx, x, weight, bias, running_mean, running_var, nbt, eps, momentum, slope):
         from pcfm import ops
         y, mean, invstd = ops.bn_act_forward(x, weight, bias, eps, slope, momentum, running_mean,
-                                             running_var)
+                                             running_var, nbt)
         ctx.save_for_backward(x, weight, bias, mean, invstd)
         ctx.slope = slope
         return y
@@ -30,7 +30,7 @@ class _BNAct(torch.autograd.Function):
         from pcfm import ops
         x, weight, bias, mean, invstd = ctx.saved_tensors
         dx, dgamma, dbeta, _ = ops.bn_act_backward(dy, x, weight, bias, mean, invstd, ctx.slope)
-        return dx, dgamma, dbeta, None, None, None, None, None
+        return dx, dgamma, dbeta, None, None, None, None, None, None
 
 
 def _fusable(x: torch.Tensor, bn) -> bool:
@@ -47,10 +47,9 @@ def _fusable(x: torch.Tensor, bn) -> bool:
 
 def bn_act(x: torch.Tensor, bn, slope: float) -> torch.Tensor:
     """act(bn(x)) with act(v) = v if v > 0 else slope * v (slope 0: ReLU)."""
-    if _fusable(x, bn):
-        bn.num_batches_tracked.add_(1)
+    if _fusable(x, bn):  # num_batches_tracked += 1 inside the kernel (no extra launch)
         return _BNAct.apply(x.contiguous(), bn.weight, bn.bias, bn.running_mean, bn.running_var,
-                            float(bn.eps), float(bn.momentum), float(slope))
+                            _nbt(bn), float(bn.eps), float(bn.momentum), float(slope))
     y = bn(x)
     return F.relu(y, inplace=True) if slope == 0 else F.leaky_relu(y, slope, inplace=True)
 
@@ -60,10 +59,11 @@ class _PwBnAct(torch.autograd.Function):
     conv's bias gradient comes out of the BN backward pass (sum of dBN/dy)."""
 
     @staticmethod
-    def forward(ctx, x, w, b, gamma, beta, rmean, rvar, eps, momentum, slope):
+    def forward(ctx, x, w, b, gamma, beta, rmean, rvar, nbt, eps, momentum, slope):
         from pcfm import ops
         y = ops.pointwise_forward(x, w, b)
-        z, mean, invstd = ops.bn_act_forward(y, gamma, beta, eps, slope, momentum, rmean, rvar)
+        z, mean, invstd = ops.bn_act_forward(y, gamma, beta, eps, slope, momentum, rmean, rvar,
+                                             nbt)
         ctx.save_for_backward(x, w, y, gamma, beta, mean, invstd)
         ctx.slope, ctx.has_bias = slope, b is not None
         return z
@@ -76,7 +76,7 @@ class _PwBnAct(torch.autograd.Function):
                                                     want_dbias_in=ctx.has_bias)
         dx = ops.pointwise_backward_data(dy, w) if ctx.needs_input_grad[0] else None
         dw = ops.pointwise_backward_weight(x, dy).view_as(w) if ctx.needs_input_grad[1] else None
-        return dx, dw, db, dgamma, dbeta, None, None, None, None, None
+        return dx, dw, db, dgamma, dbeta, None, None, None, None, None, None
 
 
 class _Conv3dBnAct(torch.autograd.Function):
@@ -84,14 +84,15 @@ class _Conv3dBnAct(torch.autograd.Function):
     kept for the weight gradient, the conv bias gradient from the BN backward."""
 
     @staticmethod
-    def forward(ctx, x, w, b, gamma, beta, rmean, rvar, eps, momentum, slope):
+    def forward(ctx, x, w, b, gamma, beta, rmean, rvar, nbt, eps, momentum, slope):
         from pcfm import ops
         bsz, cin, r = x.shape[0], x.shape[1], x.shape[2]
         cout = w.shape[0]
         xs = ops.conv3d_split(x)
         y = ops.conv3d_igemm_split(xs, ops.conv3d_prep_weight(w, False), b, bsz, cin, cout, r,
                                    "conv3d_fwd")
-        z, mean, invstd = ops.bn_act_forward(y, gamma, beta, eps, slope, momentum, rmean, rvar)
+        z, mean, invstd = ops.bn_act_forward(y, gamma, beta, eps, slope, momentum, rmean, rvar,
+                                             nbt)
         ctx.save_for_backward(xs, w, y, gamma, beta, mean, invstd)
         ctx.slope, ctx.has_bias, ctx.dims = slope, b is not None, (bsz, cin, cout, r)
         return z
@@ -111,7 +112,7 @@ class _Conv3dBnAct(torch.autograd.Function):
                                         r, "conv3d_bwd_data")
         if ctx.needs_input_grad[1]:
             dw = ops.conv3d_wgrad_split(xs, gys, bsz, cin, cout, r)
-        return dx, dw, db, dgamma, dbeta, None, None, None, None, None
+        return dx, dw, db, dgamma, dbeta, None, None, None, None, None, None
 
 
 class _Conv3dBnActPair(torch.autograd.Function):
@@ -121,18 +122,18 @@ class _Conv3dBnActPair(torch.autograd.Function):
     grad (bn_act_backward_split): no fp32 pass over either."""
 
     @staticmethod
-    def forward(ctx, x, w1, b1, g1, bt1, rm1, rv1, w2, b2, g2, bt2, rm2, rv2, eps1, mom1,
-                slope1, eps2, mom2, slope2):
+    def forward(ctx, x, w1, b1, g1, bt1, rm1, rv1, nbt1, w2, b2, g2, bt2, rm2, rv2, nbt2, eps1,
+                mom1, slope1, eps2, mom2, slope2):
         from pcfm import ops
         bsz, cin, r = x.shape[0], x.shape[1], x.shape[2]
         cmid, cout = w1.shape[0], w2.shape[0]
         xs = ops.conv3d_split(x)
         y1 = ops.conv3d_igemm_split(xs, ops.conv3d_prep_weight(w1, False), b1, bsz, cin, cmid,
                                     r, "conv3d_fwd")
-        z1s, m1, is1 = ops.bn_act_forward_split(y1, g1, bt1, eps1, slope1, mom1, rm1, rv1)
+        z1s, m1, is1 = ops.bn_act_forward_split(y1, g1, bt1, eps1, slope1, mom1, rm1, rv1, nbt1)
         y2 = ops.conv3d_igemm_split(z1s, ops.conv3d_prep_weight(w2, False), b2, bsz, cmid, cout,
                                     r, "conv3d_fwd")
-        z2, m2, is2 = ops.bn_act_forward(y2, g2, bt2, eps2, slope2, mom2, rm2, rv2)
+        z2, m2, is2 = ops.bn_act_forward(y2, g2, bt2, eps2, slope2, mom2, rm2, rv2, nbt2)
         ctx.save_for_backward(xs, w1, y1, g1, bt1, m1, is1, z1s, w2, y2, g2, bt2, m2, is2)
         ctx.slopes = (slope1, slope2)
         ctx.has_bias = (b1 is not None, b2 is not None)
@@ -160,8 +161,8 @@ class _Conv3dBnActPair(torch.autograd.Function):
             dx = ops.conv3d_igemm_split(gys1, ops.conv3d_prep_weight(w1, True), None, bsz, cmid,
                                         cin, r, "conv3d_bwd_data")
         dw1 = ops.conv3d_wgrad_split(xs, gys1, bsz, cin, cmid, r)
-        return (dx, dw1, db1, dg1, dbt1, None, None, dw2, db2, dg2, dbt2, None, None,
-                None, None, None, None, None, None)
+        return (dx, dw1, db1, dg1, dbt1, None, None, None, dw2, db2, dg2, dbt2, None, None,
+                None, None, None, None, None, None, None)
 
 
 def conv_bn_act_pair(conv1, bn1, slope1: float, conv2, bn2, slope2: float,
@@ -184,13 +185,11 @@ def conv_bn_act_pair(conv1, bn1, slope1: float, conv2, bn2, slope2: float,
     if not ok:
         x = conv_bn_act(conv1, bn1, x, slope1)
         return conv_bn_act(conv2, bn2, x, slope2)
-    bn1.num_batches_tracked.add_(1)
-    bn2.num_batches_tracked.add_(1)
     return _Conv3dBnActPair.apply(
         x.contiguous(), conv1.weight, conv1.bias, bn1.weight, bn1.bias, bn1.running_mean,
-        bn1.running_var, conv2.weight, conv2.bias, bn2.weight, bn2.bias, bn2.running_mean,
-        bn2.running_var, float(bn1.eps), float(bn1.momentum), float(slope1), float(bn2.eps),
-        float(bn2.momentum), float(slope2))
+        bn1.running_var, _nbt(bn1), conv2.weight, conv2.bias, bn2.weight, bn2.bias,
+        bn2.running_mean, bn2.running_var, _nbt(bn2), float(bn1.eps), float(bn1.momentum),
+        float(slope1), float(bn2.eps), float(bn2.momentum), float(slope2))
 
 
 def conv_bn_act(conv, bn, x: torch.Tensor, slope: float) -> torch.Tensor:
@@ -202,11 +201,20 @@ def conv_bn_act(conv, bn, x: torch.Tensor, slope: float) -> torch.Tensor:
         if out_shape_ok:
             from modules.shared_mlp import PointwiseConv1d
             fn = _PwBnAct if isinstance(conv, PointwiseConv1d) else _Conv3dBnAct
-            bn.num_batches_tracked.add_(1)
             return fn.apply(x.contiguous(), conv.weight, conv.bias, bn.weight, bn.bias,
-                            bn.running_mean, bn.running_var, float(bn.eps), float(bn.momentum),
-                            float(slope))
+                            bn.running_mean, bn.running_var, _nbt(bn), float(bn.eps),
+                            float(bn.momentum), float(slope))
     return bn_act(conv(x), bn, slope)
+
+
+def _nbt(bn):
+    """bn.num_batches_tracked for the fused kernels to increment (channel 0's
+    statistics publisher adds 1, as torch's batch_norm path does with a separate
+    add_ launch); None when the module has no int64 counter on the device."""
+    t = getattr(bn, "num_batches_tracked", None)
+    if t is None or t.dtype != torch.int64 or t.numel() != 1 or not t.is_cuda:
+        return None
+    return t
 
 
 def _fusable_pre(bn) -> bool:

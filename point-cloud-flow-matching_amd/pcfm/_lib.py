@@ -90,12 +90,12 @@ SIGNATURES = {
                                    _P, _P, _P, _P, _P, _P, _P, _P, _P, _Z, _P]),
     "pcfm_head_silu_bwd": (_I, [_P, _P, _P, _I, _I, _I, _P, _P, _P, _P, _Z, _P]),
     "pcfm_bn_workspace_bytes": (_Z, [_I, _I, _I]),
-    "pcfm_bn_act_fwd": (_I, [_P, _P, _P, _I, _I, _I, _F, _F, _F, _P, _P, _P, _P, _P, _P, _Z,
-                             _P]),
+    "pcfm_bn_act_fwd": (_I, [_P, _P, _P, _I, _I, _I, _F, _F, _F, _P, _P, _P, _P, _P, _P, _P,
+                             _Z, _P]),
     "pcfm_bn_act_bwd": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _F, _P, _P, _P, _P, _P, _Z,
                              _P]),
     "pcfm_bn_act_fwd_split": (_I, [_P, _P, _P, _I, _I, _I, _F, _F, _F, _P, _P, _P, _P, _P, _P,
-                                   _Z, _P]),
+                                   _P, _Z, _P]),
     "pcfm_bn_act_bwd_split_workspace_bytes": (_Z, [_I, _I, _I]),
     "pcfm_bn_act_bwd_split": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _F, _P, _P, _P, _P, _P,
                                    _Z, _P]),

@@ -984,9 +984,22 @@ def head_silu_bwd(da16, uprev, gprev, n: int):
 # --------------------------------------------------------------------------
 # BatchNorm (batch statistics) + ReLU / LeakyReLU (include/pcfm.h)
 # --------------------------------------------------------------------------
+def _counter(t, like: torch.Tensor):
+    """A BatchNorm num_batches_tracked buffer the kernel may increment: int64, one
+    element, on the input's device (None passes through)."""
+    if t is None:
+        return None
+    if t.dtype != torch.int64 or t.numel() != 1 or t.device != like.device:
+        raise RuntimeError("num_batches_tracked: expected a one-element int64 tensor on the "
+                           "input's device")
+    return t
+
+
 def bn_act_forward(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, eps: float,
-                   slope: float, momentum: float, running_mean, running_var):
-    """x (B, C, ...) fp32 contiguous -> (y, mean, invstd); running stats updated in place."""
+                   slope: float, momentum: float, running_mean, running_var,
+                   num_batches_tracked=None):
+    """x (B, C, ...) fp32 contiguous -> (y, mean, invstd); running stats (and the int64
+    num_batches_tracked counter, +1) updated in place."""
     _check(x, "input", "f")
     b, c = x.shape[0], x.shape[1]
     s = x.numel() // max(1, b * c)
@@ -995,13 +1008,15 @@ def bn_act_forward(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, ep
     ws = _workspace(_lib.query("pcfm_bn_workspace_bytes", b, c, s), x)
     with _timed("bn_act_fwd", 4 * 3 * x.numel(), x):
         _lib.call("pcfm_bn_act_fwd", _ptr(x), _ptr(weight), _ptr(bias), b, c, s, float(eps),
-                  float(slope), float(momentum), _p(running_mean), _p(running_var), _ptr(y),
+                  float(slope), float(momentum), _p(running_mean), _p(running_var),
+                  _p(_counter(num_batches_tracked, x)), _ptr(y),
                   _ptr(stats[0]), _ptr(stats[1]), _ptr(ws), ws.numel(), _stream(x))
     return y, stats[0], stats[1]
 
 
 def bn_act_forward_split(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, eps: float,
-                         slope: float, momentum: float, running_mean, running_var):
+                         slope: float, momentum: float, running_mean, running_var,
+                         num_batches_tracked=None):
     """bn_act_forward for a voxel conv output x (B, C, R, R, R) whose activation only
     feeds the next voxel conv: -> (split(act(bn(x))) as conv3d_split lays it out,
     mean, invstd); running stats updated in place."""
@@ -1017,7 +1032,8 @@ def bn_act_forward_split(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tens
     with _timed("bn_act_fwd", 4 * 3 * x.numel(), x):
         _lib.call("pcfm_bn_act_fwd_split", _ptr(x), _ptr(weight), _ptr(bias), b, c, s,
                   float(eps), float(slope), float(momentum), _p(running_mean), _p(running_var),
-                  _ptr(ys), _ptr(stats[0]), _ptr(stats[1]), _ptr(ws), ws.numel(), _stream(x))
+                  _p(_counter(num_batches_tracked, x)), _ptr(ys), _ptr(stats[0]), _ptr(stats[1]),
+                  _ptr(ws), ws.numel(), _stream(x))
     return ys, stats[0], stats[1]
 
 

@@ -136,6 +136,8 @@ def test_conv_bn_act_fused_matches_modules(ops, kind):
     assert rel(bn2.bias.grad, bn.bias.grad) < 1e-3
     torch.testing.assert_close(bn2.running_mean, bn.running_mean, rtol=1e-4, atol=1e-5)
     torch.testing.assert_close(bn2.running_var, bn.running_var, rtol=1e-4, atol=1e-5)
+    # the fused kernel increments the counter itself (no separate add_ launch)
+    assert int(bn2.num_batches_tracked) == int(bn.num_batches_tracked) == 1
 
 
 @pytest.mark.parametrize("b,c,n,groups", [(8, 256, 20000, 32), (2, 128, 1000, 32), (3, 64, 36, 8)])
@@ -217,3 +219,4 @@ def test_conv_bn_act_pair_matches_two_nodes(ops, b, c, r):
             assert torch.equal(p_ref.grad, p.grad), name
         for (name, b_ref), bb in zip(m_ref.named_buffers(), m.buffers()):
             assert torch.equal(b_ref, bb), name
+    assert int(mods[1].num_batches_tracked) == int(mods[3].num_batches_tracked) == 1
