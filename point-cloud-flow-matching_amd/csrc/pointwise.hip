@@ -275,6 +275,154 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))
   }
 }
 
+// Streaming form for M <= 128, K <= 256, both multiples of 32 (SharedMLP 128 -> 128 layers and
+// their backward-data, stage-2 proj backward-data): a skinny GEMM that is
+// HBM-bound (x in, y out once), so no point tile is staged through LDS.  The
+// whole weight image (hi + lo, <= 132 KiB) is loaded into LDS once per
+// persistent block; then every wave streams its own 32-point tiles with no
+// barrier: the B operand comes straight from global memory into registers
+// (lane l: point p0 + (l & 31), channels 16 kk + 8 (l >> 5) + 0..7 -- per load
+// instruction 32 consecutive points of one channel row, 128 B) and is split to
+// bf16 hi / lo in registers; the next 32-channel chunk's loads (and across tile
+// boundaries the next tile's first chunk) are in flight while the current
+// chunk's 24 MFMAs run.  LDS rows of Kpad + 8 bf16 keep the ds_read_b128
+// fragment reads conflict-free.  grid = min(tiles / 8, CUs x blocks per CU),
+// 512 threads.
+constexpr int kSW = 8;  // waves per streaming block
+__device__ __forceinline__ bf16x8 split8(const float (&v)[8], bf16x8& lo) {
+  bf16x8 hi;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    hi[j] = (__bf16)v[j];
+    lo[j] = (__bf16)(v[j] - (float)hi[j]);
+  }
+  return hi;
+}
+
+__device__ __forceinline__ const float* uniform_ptr(const float* p) {
+  const unsigned long long u = (unsigned long long)p;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)u);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(u >> 32));
+  return (const float*)(((unsigned long long)hi << 32) | lo);
+}
+
+// the 16 B-operand values of one 32-channel chunk for lane (n, h): channels
+// c0 + 16 kk + 8 h + j (kk < 2, j < 8) of point p (K % 32 == 0: whole chunks);
+// one uniform row pointer + one 32-bit lane offset, so the 16 loads differ by
+// uniform multiples of N.  Points >= N read row N - 1 and are zeroed.
+__device__ __forceinline__ void pw_stream_load(const Parts& x, int b, int c0, int N, int p, int h,
+                                               float (&v)[16]) {
+  const bool pok = p < N;
+  // 32 channels in one part (parts are 32-aligned); the row pointer is wave-uniform
+  const float* __restrict__ xr = uniform_ptr(x.row(b, c0, N));
+  const int lo = 8 * h * N + (pok ? p : N - 1);  // pw_ok: C * N < 2^31
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float val = xr[lo + (16 * kk + j) * N];
+      v[8 * kk + j] = pok ? val : 0.0f;
+    }
+}
+
+template <int NCH>  // Kpad / 32
+__global__ void __launch_bounds__(kSW * 64)
+    pw_stream128_kernel(const Parts x, const uint16_t* __restrict__ wh,
+                        const uint16_t* __restrict__ wl, const float* __restrict__ bias,
+                        int bias_bstride, const Parts y, int K, int M, int N, int B) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t sa[];  // [2][128][Kpad + 8]
+  constexpr int Kpad = 32 * NCH, ldr = Kpad + 8, cpr = Kpad / 8;
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  for (int e = t; e < 2 * 128 * cpr; e += kSW * 64) {  // weight image -> LDS, 16-B pieces
+    const int img = e / (128 * cpr), rem = e - img * 128 * cpr;
+    const int row = rem / cpr, pc = rem - row * cpr;
+    const uint16_t* src = (img ? wl : wh) + (size_t)row * Kpad + pc * 8;
+    *reinterpret_cast<uint4*>(sa + img * 128 * ldr + row * ldr + pc * 8) =
+        *reinterpret_cast<const uint4*>(src);
+  }
+  __syncthreads();
+
+  const int n = lane & 31, h = lane >> 5;
+  const int ntn = (N + 31) / 32, tiles = B * ntn;
+  const int wstride = (int)gridDim.x * kSW;
+  int tl = __builtin_amdgcn_readfirstlane((int)blockIdx.x * kSW + w);
+  if (tl >= tiles) return;  // wave-uniform; no barrier below
+  const uint16_t* sah = sa;
+  const uint16_t* sal = sa + 128 * ldr;
+  float nx[16];
+  {
+    const int b = tl / ntn;
+    pw_stream_load(x, b, 0, N, (tl - b * ntn) * 32 + n, h, nx);
+  }
+  while (true) {
+    const int b = __builtin_amdgcn_readfirstlane(tl / ntn);
+    const int p = (tl - b * ntn) * 32 + n;
+    const int ntl = tl + wstride;  // the next tile's chunk 0 is issued during chunk NCH-1
+    const int nb = __builtin_amdgcn_readfirstlane(ntl / ntn);
+    const int np = (ntl - nb * ntn) * 32 + n;
+    f32x16 acc[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][e] = 0.0f;
+#pragma unroll 1
+    for (int ck = 0; ck < NCH; ++ck) {
+      float cur[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) cur[q] = nx[q];
+      if (ck + 1 < NCH) {
+        pw_stream_load(x, b, 32 * (ck + 1), N, p, h, nx);
+      } else if (ntl < tiles) {
+        pw_stream_load(x, nb, 0, N, np, h, nx);
+      }
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        bf16x8 bh, bl;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          bh[j] = (__bf16)cur[8 * kk + j];
+          bl[j] = (__bf16)(cur[8 * kk + j] - (float)bh[j]);
+        }
+        const int ko = ck * 32 + kk * 16 + 8 * h;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int o = (32 * i + n) * ldr + ko;
+          const bf16x8 ah = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(sah + o));
+          const bf16x8 al = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(sal + o));
+          acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc[i], 0, 0, 0);
+          acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc[i], 0, 0, 0);
+          acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc[i], 0, 0, 0);
+        }
+      }
+    }
+    // epilogue: rows 32 i + (e & 3) + 8 (e >> 2) + 4 h, point p
+    const int bo = b * bias_bstride;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int mg = 32 * i;
+      if (mg < M) {
+        // a 32-row group lies in one output part
+        float* __restrict__ yr = const_cast<float*>(uniform_ptr(y.row(b, mg, N)));
+        float* __restrict__ yl = yr + 4 * h * N + p;  // + uniform row offsets below
+        // M % 32 == 0: whole row groups.  One lane pointer + immediate offsets (a
+        // per-element index is loop-invariant: the compiler would hoist 64
+        // addresses out of the tile loop)
+        float bv[16];
+        const float* bl = bias != nullptr ? uniform_ptr(bias + bo + mg) + 4 * h : nullptr;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) bv[e] = bl != nullptr ? bl[(e & 3) + 8 * (e >> 2)] : 0.0f;
+        if (p < N) {
+#pragma unroll
+          for (int e = 0; e < 16; ++e) yl[((e & 3) + 8 * (e >> 2)) * N] = acc[i][e] + bv[e];
+        }
+      }
+    }
+    tl = ntl;
+    if (tl >= tiles) break;
+  }
+}
+
 // dW partials: grid = (ceil(Cout/128) * ceil(Cin/128), S); K-steps of 32
 // points (a step never crosses a batch element).  part [S][Cout][Cin].
 __global__ void __launch_bounds__(256)
@@ -591,6 +739,33 @@ static int pw_gemm_launch(const Parts& x, const void* wsplit, const float* bias,
   const size_t total = (size_t)Mpad * Kpad;
   const uint16_t* wh = (const uint16_t*)wsplit;
   const long long big = (long long)ceil_div(n, 128) * (Mpad / 128) * b;
+#ifndef PCFM_PW_NOSTREAM
+  if (Mpad == 128 && Kpad <= 256 && cin % 32 == 0 && cout % 32 == 0) {
+    const uint16_t* wl_img = wh + total;
+    const long long tiles = (long long)b * ceil_div(n, 32);
+    const size_t lds = (size_t)2 * 128 * (Kpad + 8) * sizeof(uint16_t);
+    const int per_cu = lds <= 80 * 1024 ? 2 : 1;
+    const int grid = (int)std::max(1LL, std::min((tiles + kSW - 1) / kSW, (long long)kCUs * per_cu));
+    const void* kfn = nullptr;
+    switch (Kpad / 32) {
+#define PW_STREAM_CASE(NC) \
+  case NC: kfn = (const void*)pw_stream128_kernel<NC>; break;
+      PW_STREAM_CASE(1) PW_STREAM_CASE(2) PW_STREAM_CASE(3) PW_STREAM_CASE(4)
+      PW_STREAM_CASE(5) PW_STREAM_CASE(6) PW_STREAM_CASE(7) PW_STREAM_CASE(8)
+#undef PW_STREAM_CASE
+    }
+    const int e = allow_big_lds(kfn);
+    if (e) return e;
+    void* args[] = {(void*)&x, (void*)&wh, (void*)&wl_img, (void*)&bias, (void*)&bias_bstride,
+                    (void*)&y, (void*)&cin, (void*)&cout, (void*)&n, (void*)&b};
+    const hipError_t le = hipLaunchKernel(kfn, dim3(grid), dim3(kSW * 64), args, lds, st);
+    if (le != hipSuccess) {
+      set_error("pointwise_gemm: launch failed");
+      return (int)le;
+    }
+    return check_launch("pointwise_gemm");
+  }
+#endif
 #ifndef PCFM_PW_NO256
   if (Mpad % 256 == 0 && big / 2 >= 2 * kCUs) {
     hipLaunchKernelGGL(pw_gemm256_kernel, dim3(ceil_div(n, 128), Mpad / 256, b), dim3(512), 0, st,
