@@ -297,14 +297,17 @@ constexpr int kGM = 128, kGN = 256, kGStages = 3;
 
 // K-step geometry of the LDS-DMA kernel: KT = 32 (64-B rows, 48 KiB stages,
 // one block per CU) or KT = 16 (32-B rows, 24 KiB stages, two blocks per CU)
-template <int KT>
+// GN: voxels per block tile (256: 8 waves, one block per CU; 128: 4 waves and
+// two stages, two independent blocks per CU)
+template <int KT, int GN = kGN>
 struct GK {
+  static constexpr int NW = 2 * (GN / 64);     // waves: 2 (m) x GN / 64 (voxels)
   static constexpr int RB = KT * 2;            // bytes per LDS row (hi or lo)
   static constexpr int CPR = RB / 16;          // 16-B chunks per row
   static constexpr int RPP = 1024 / RB;        // rows per 1-KiB LDS-DMA piece
-  static constexpr int A = kGM * RB, B = kGN * RB;  // bytes per image
+  static constexpr int A = kGM * RB, B = GN * RB;  // bytes per image
   static constexpr int STAGE = 2 * A + 2 * B;
-  static constexpr int APW = 2 * A / 1024 / 8, BPW = 2 * B / 1024 / 8;  // pieces per wave
+  static constexpr int APW = 2 * A / 1024 / NW, BPW = 2 * B / 1024 / NW;  // pieces per wave
   static constexpr int API = A / 1024, BPI = B / 1024;                  // pieces per image
   // physical chunk p of row r holds logical chunk p ^ swz(r): conflict-free
   // ds_read_b128 fragment reads
@@ -320,10 +323,10 @@ __device__ __forceinline__ void glds16(const void* g, uint8_t* l) {
 
 // One step's MFMA operands of a wave (64 x 64 of the 128 x 256 tile):
 // F[kk] = {A hi 0, A hi 1, A lo 0, A lo 1, B hi 0, B hi 1, B lo 0, B lo 1}
-template <int KT>
+template <int KT, int GN = kGN>
 __device__ __forceinline__ void glds_frags(const uint8_t* lds, int buf, int wr, int wc, int r,
                                            int h, bf16x8 (&F)[KT / 16][8]) {
-  using G = GK<KT>;
+  using G = GK<KT, GN>;
   const uint8_t* base = lds + buf * G::STAGE;
 #pragma unroll
   for (int kk = 0; kk < KT / 16; ++kk) {
@@ -367,31 +370,31 @@ __device__ __forceinline__ void glds_mfma(const bf16x8 (&F)[KT / 16][8], f32x16 
   }
 }
 
-template <int KT>
-__global__ void __launch_bounds__(512)
+template <int KT, int GN = kGN, int NST = kGStages>
+__global__ void __launch_bounds__(GN * 2)  // GK<KT, GN>::NW = GN / 32 waves
     conv3_igemm_glds_kernel(const uint16_t* __restrict__ xh, const uint16_t* __restrict__ xl,
                             const uint16_t* __restrict__ wh, const uint16_t* __restrict__ wl,
                             const uint16_t* __restrict__ zrow, const float* __restrict__ bias,
                             float* __restrict__ y, int K, int M, int R, int S,
                             float* __restrict__ part) {
-  using G = GK<KT>;
-  __shared__ __attribute__((aligned(16))) uint8_t lds[kGStages * G::STAGE];
+  using G = GK<KT, GN>;
+  __shared__ __attribute__((aligned(16))) uint8_t lds[NST * G::STAGE];
   const int V = R * R * R, R2 = R * R;
   int id = (int)blockIdx.x;
   {
     const int nwg = (int)gridDim.x, q = nwg / 8, rr = nwg % 8, xcd = id % 8;
     id = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + id / 8;
   }
-  const int nmt = M / kGM, nvt = V / kGN;
+  const int nmt = M / kGM, nvt = V / GN;
   const int nb = (int)gridDim.x / (S * nmt * nvt);  // batch elements
   const int m0 = (id % nmt) * kGM;
   id /= nmt;
-  const int v0 = (id % nvt) * kGN;
+  const int v0 = (id % nvt) * GN;
   id /= nvt;
   const int b = id % nb, sp = id / nb;
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int wr = w >> 2, wc = w & 3, r = lane & 31, h = lane >> 5;
+  const int wr = w / (GN / 64), wc = w % (GN / 64), r = lane & 31, h = lane >> 5;
   // split-K (small grids, r = 8): this block's K-steps [k0, k1) of 27 * K / KT
   const int nall = 27 * (K / KT);
   const int k0 = (int)((long long)nall * sp / S), k1 = (int)((long long)nall * (sp + 1) / S);
@@ -430,13 +433,18 @@ __global__ void __launch_bounds__(512)
     const int c0 = (s / 27) * KT, tap = s - (s / 27) * 27;
     uint8_t* base = lds + buf * G::STAGE;
     const size_t aofs = (size_t)tap * M * K + c0;
+#ifndef PCFM_EXP_CNOA
 #pragma unroll
     for (int q = 0; q < G::APW; ++q) {
       const int I = G::APW * w + q;
       glds16(abase[q] + aofs, base + (I / G::API) * G::A + (I % G::API) * 1024);
     }
+#endif
     const int dx = tap / 9 - 1, dy = (tap / 3) % 3 - 1, dz = tap % 3 - 1;
     const long long bofs = (long long)(dx * R2 + dy * R + dz) * K + c0;
+#ifdef PCFM_EXP_CNOB
+    if (aofs == (size_t)-1)
+#endif
 #pragma unroll
     for (int q = 0; q < G::BPW; ++q) {
       const int I = G::BPW * w + q;
@@ -474,13 +482,15 @@ __global__ void __launch_bounds__(512)
   if (nsteps > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::APW + G::BPW) : "memory");
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
-  if (nsteps > 2) issue(2, 2);
-  glds_frags<KT>(lds, 0, wr, wc, r, h, F0);
+  if (NST == 3 && nsteps > 2) issue(2, 2);
+  glds_frags<KT, GN>(lds, 0, wr, wc, r, h, F0);
   // step s with the prefetch of step s+1 (s + 1 < nsteps)
   auto step = [&](int s, bf16x8 (&Fc)[KT / 16][8], bf16x8 (&Fn)[KT / 16][8]) {
-    // stage s+1 landed (own pieces; stage s+2's stay in flight)
-    if (s + 2 < nsteps) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::APW + G::BPW) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // stage s+1 landed (own pieces; with three stages, stage s+2's stay in flight)
+    if (NST == 3 && s + 2 < nsteps)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::APW + G::BPW) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's stage-s reads done
     __builtin_amdgcn_s_barrier();
 #ifndef PCFM_CONV_DMA_LATE
@@ -492,12 +502,19 @@ __global__ void __launch_bounds__(512)
     // same time and the MFMA pipe idles: 0.711 -> 0.694 ms (C128 R32 fwd),
     // 0.368 -> 0.357 ms (C256 R16), tools/conv_ab.py on MI355X; 4 MFMAs per
     // piece (over-asking the 16 left after the fragment reads): 0.680 / 0.348 ms
-    glds_frags<KT>(lds, (s + 1) % kGStages, wr, wc, r, h, Fn);
+    glds_frags<KT, GN>(lds, (s + 1) % NST, wr, wc, r, h, Fn);
+#ifndef PCFM_EXP_CNOMFMA
     glds_mfma<KT>(Fc, acc);
+#else
+    acc[0][0][0] += (float)Fc[0][0][0];
+#endif
     // unconditional (same basic block as the MFMAs, so the scheduler can place
     // the pieces between them): past the last step it reloads the final
     // step's data into the buffer step s just drained (never read again)
-    issue(min(s + 3, nsteps - 1), s % kGStages);
+#ifndef PCFM_EXP_CNODMA
+    // the buffer step s just drained (its fragments were read in step s - 1)
+    issue(min(s + NST, nsteps - 1), s % NST);
+#endif
 #pragma unroll
     for (int g = 0; g < 4 * (KT / 16); ++g) {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
@@ -510,10 +527,11 @@ __global__ void __launch_bounds__(512)
     }
     __builtin_amdgcn_sched_group_barrier(0x008, 8 * (KT / 16), 0);
 #else
+    static_assert(NST == 3, "the burst-issue schedule needs three stages");
 #ifndef PCFM_EXP_NOLOAD
     if (s + 3 < nsteps) issue(s + 3, s % kGStages);
 #endif
-    glds_frags<KT>(lds, (s + 1) % kGStages, wr, wc, r, h, Fn);
+    glds_frags<KT, GN>(lds, (s + 1) % kGStages, wr, wc, r, h, Fn);
     glds_mfma<KT>(Fc, acc);
     // reads of step s+1 interleaved with the first MFMAs of step s (two
     // ds_read_b128 per MFMA gap are free, microarch guide "LDS")
@@ -1458,6 +1476,16 @@ extern "C" int pcfm_conv3d_igemm_cl(const void* xs, const void* wsplit, const fl
 #endif
 #ifndef PCFM_CONV_GK
 #define PCFM_CONV_GK 32  // 16: two blocks per CU, measured 1.15-1.18x slower
+#endif
+#ifdef PCFM_CONV_GN128
+    // 128-voxel tiles, two stages, two independent 4-wave blocks per CU
+    if (S == 1 && PCFM_CONV_GK == 32 && cin % 32 == 0) {
+      const long long blocks128 = (long long)(V / 128) * (cout / kGM) * b;
+      hipLaunchKernelGGL((conv3_igemm_glds_kernel<32, 128, 2>), dim3((unsigned)blocks128),
+                         dim3(256), 0, st, xh, xl, wh, wh + total, zrow, bias, y, cin, cout, r, 1,
+                         part);
+      return check_launch("conv3d_igemm_cl");
+    }
 #endif
     if (PCFM_CONV_GK == 16 || cin % 32 != 0)
       hipLaunchKernelGGL(conv3_igemm_glds_kernel<16>, dim3((unsigned)glds_blocks), dim3(512), 0,
