@@ -384,7 +384,10 @@ __global__ void __launch_bounds__(256)
 #define PCFM_KTV 16
 #endif
 constexpr int kTV = PCFM_KTV;    // voxels per tile
-constexpr int kItems = 256;      // target items per work unit
+#ifndef PCFM_SEG_ITEMS
+#define PCFM_SEG_ITEMS 256
+#endif
+constexpr int kItems = PCFM_SEG_ITEMS;  // target items per work unit
 constexpr int kInFlight = 16;    // feature-row loads issued back to back per wave
 constexpr int kUnitWaves = 4;    // waves (independent units) per block
 

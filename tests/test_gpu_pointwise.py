@@ -22,7 +22,11 @@ def ops():
 
 
 @pytest.mark.parametrize("b,cin,cout,n", [(2, 262, 128, 1000), (1, 896, 256, 777), (3, 256, 64, 129),
-                                          (2, 128, 128, 64), (1, 5, 3, 7), (8, 256, 256, 20000)])
+                                          (2, 128, 128, 64), (1, 5, 3, 7), (8, 256, 256, 20000),
+                                          # streaming form (M <= 128, K <= 256, multiples of 32):
+                                          # ragged point tiles, 8 K-chunks in the backward-data
+                                          (2, 128, 256, 1000), (1, 96, 32, 45),
+                                          (8, 128, 128, 20000)])
 def test_pointwise_vs_fp64(ops, b, cin, cout, n):
     g = torch.Generator(device="cuda").manual_seed(cin * 7 + cout + n)
     x = torch.randn(b, cin, n, device="cuda", generator=g)
