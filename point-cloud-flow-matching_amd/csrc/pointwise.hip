@@ -696,11 +696,20 @@ int pw_wgrad_splits(int B, int cin, int cout, int N) {
     s = std::min(s, std::max(1LL, steps / 16));
     return (int)std::min(s, 256LL);
   }
+#ifndef PCFM_PW_WG_BPC
+#define PCFM_PW_WG_BPC 2  // target blocks per CU
+#endif
+#ifndef PCFM_PW_WG_MINSTEPS
+#define PCFM_PW_WG_MINSTEPS 8  // K-steps per split at least
+#endif
+#ifndef PCFM_PW_WG_CAP
+#define PCFM_PW_WG_CAP 512  // splits at most (128: 72 -> 49 us at C128, tools/pw_ab.py)
+#endif
   const long long tiles = (long long)((cout + 127) / 128) * ((cin + 127) / 128);
   const long long steps = (long long)B * ((N + kKT - 1) / kKT);
-  long long s = std::max(1LL, (2LL * kCUs + tiles - 1) / tiles);
-  s = std::min(s, std::max(1LL, steps / 16));
-  return (int)std::min(s, 128LL);
+  long long s = std::max(1LL, ((long long)PCFM_PW_WG_BPC * kCUs + tiles - 1) / tiles);
+  s = std::min(s, std::max(1LL, steps / PCFM_PW_WG_MINSTEPS));
+  return (int)std::min(s, (long long)PCFM_PW_WG_CAP);
 }
 
 bool pw_ok(int b, int cin, int cout, int n) {

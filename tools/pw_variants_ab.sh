@@ -1,0 +1,9 @@
+set -e
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+: > gpurun_out/pw_ab.jsonl
+for V in main ${VARIANTS}; do
+  if [ $V = main ]; then unset PCFM_LIB; else export PCFM_LIB=$PWD/point-cloud-flow-matching_amd/csrc/build/variants/libpcfm_$V.so; fi
+  timeout -k 10 120 python tools/pw_ab.py $V >> gpurun_out/pw_ab.jsonl
+done
