@@ -15,6 +15,10 @@ namespace pcfm {
 namespace {
 
 inline int pad_to(int x, int m) { return (x + m - 1) / m * m; }
+// rows of the weight image: above 256 a multiple of 256, so the 256-row tile
+// (x read once per 256 output rows) applies -- ContextNet head_pre's backward-data
+// (M = 640 -> 768: x read 3 times instead of 5 by 128-row tiles)
+inline int pw_mpad(int m) { return m > 256 ? pad_to(m, 256) : pad_to(m, 128); }
 
 // A channel-segmented (B, C, N) tensor: channels [off[i], off[i+1]) live in
 // their own (B, off[i+1] - off[i], N) tensor p[i] -- ContextNet's head input
@@ -549,9 +553,13 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
   const int wr = w >> 1, wc = w & 1, r = lane & 31, h = lane >> 5;  // wr 0..3 (co), wc 0..1 (ci)
   const int srow = t >> 1, shalf = (t & 1) * 16;                     // row 0..255, 16-point half
   const int co = co0 + srow, ci = ci0 + srow;
+  // a ragged last input-channel tile (cin % 256 != 0): rows past cin read the
+  // last row and are zeroed
+  const bool ciok = ci < cin;
+  const int cic = ciok ? ci : cin - 1;
   const bool vec = (N & 3) == 0;
-  const float* __restrict__ xrow = x.row(0, ci, N);
-  const size_t xbstride = (size_t)(x.row(1, ci, N) - xrow);
+  const float* __restrict__ xrow = x.row(0, cic, N);
+  const size_t xbstride = (size_t)(x.row(1, cic, N) - xrow);
 
   float ra[16], rb[16];
   uint32_t pmask = 0u;
@@ -590,7 +598,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       ra[q] = (pmask >> q) & 1u ? 0.0f : ra[q];
-      rb[q] = (pmask >> q) & 1u ? 0.0f : rb[q];
+      rb[q] = ((pmask >> q) & 1u) || !ciok ? 0.0f : rb[q];
     }
     uint16_t* ah = lds + srow * kLDR + shalf;
     store_split<16>(ra, ah, ah + A_ELEMS);
@@ -650,7 +658,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
       for (int e = 0; e < 16; ++e) {
         const int o = co0 + wr * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
         const int c = ci0 + wc * 128 + j * 32 + r;
-        pb[(size_t)o * cin + c] = acc[i][j][e];
+        if (c < cin) pb[(size_t)o * cin + c] = acc[i][j][e];
       }
 }
 
@@ -684,13 +692,16 @@ bool pw_wgrad_wide(int cin, int cout) {
 #ifdef PCFM_PW_NO256
   return false;
 #else
+  // (a ragged last input-channel tile is supported and masked, but measured
+  // slower than the 128 x 128 tiles for ContextNet head_pre, cin = 640: 378 vs
+  // 290 us -- one block per CU over a half-empty third tile)
   return cin % 256 == 0 && cout % 256 == 0;
 #endif
 }
 
 int pw_wgrad_splits(int B, int cin, int cout, int N) {
   if (pw_wgrad_wide(cin, cout)) {  // one 512-thread block per CU
-    const long long tiles = (long long)(cout / 256) * (cin / 256);
+    const long long tiles = (long long)(cout / 256) * ((cin + 255) / 256);
     const long long steps = (long long)B * ((N + kKT - 1) / kKT);
     long long s = std::max(1LL, ((long long)kCUs + tiles - 1) / tiles);
     s = std::min(s, std::max(1LL, steps / 16));
@@ -724,8 +735,8 @@ using namespace pcfm;
 
 extern "C" size_t pcfm_pointwise_weight_bytes(int cout, int cin) {
   if (cout <= 0 || cin <= 0) return 0;
-  const size_t a = (size_t)pad_to(cout, 128) * pad_to(cin, kKT);
-  const size_t b = (size_t)pad_to(cin, 128) * pad_to(cout, kKT);
+  const size_t a = (size_t)pw_mpad(cout) * pad_to(cin, kKT);
+  const size_t b = (size_t)pw_mpad(cin) * pad_to(cout, kKT);
   return 2 * std::max(a, b) * sizeof(uint16_t);
 }
 
@@ -733,7 +744,7 @@ extern "C" int pcfm_pointwise_prep_weight(const float* w, int cout, int cin, int
                                           void* wsplit, void* stream) {
   PCFM_CHECK_ARG(cout > 0 && cin > 0, "pointwise_prep_weight: bad size %d x %d", cout, cin);
   const int M = transpose ? cin : cout, K = transpose ? cout : cin;
-  const int Mpad = pad_to(M, 128), Kpad = pad_to(K, kKT);
+  const int Mpad = pw_mpad(M), Kpad = pad_to(K, kKT);
   const size_t total = (size_t)Mpad * Kpad;
   uint16_t* wh = (uint16_t*)wsplit;
   hipLaunchKernelGGL(pw_wsplit_kernel, dim3(ceil_div((long long)total, 256)), dim3(256), 0,
@@ -744,7 +755,7 @@ extern "C" int pcfm_pointwise_prep_weight(const float* w, int cout, int cin, int
 
 static int pw_gemm_launch(const Parts& x, const void* wsplit, const float* bias, int bias_bstride,
                           int b, int cin, int cout, int n, const Parts& y, hipStream_t st) {
-  const int Mpad = pad_to(cout, 128), Kpad = pad_to(cin, kKT);
+  const int Mpad = pw_mpad(cout), Kpad = pad_to(cin, kKT);
   const size_t total = (size_t)Mpad * Kpad;
   const uint16_t* wh = (const uint16_t*)wsplit;
   const long long big = (long long)ceil_div(n, 128) * (Mpad / 128) * b;
@@ -843,7 +854,7 @@ static int pw_wgrad_launch(const Parts& x, const float* grad_y, int b, int cin, 
   const size_t total = (size_t)cout * cin;
   const int S = pw_wgrad_splits(b, cin, cout, n);
   if (pw_wgrad_wide(cin, cout)) {
-    hipLaunchKernelGGL(pw_wgrad256_kernel, dim3((cout / 256) * (cin / 256), S), dim3(512), 0, st,
+    hipLaunchKernelGGL(pw_wgrad256_kernel, dim3((cout / 256) * ((cin + 255) / 256), S), dim3(512), 0, st,
                        x, grad_y, b, cin, cout, n, S, (float*)ws);
   } else {
     const int tiles = ((cout + 127) / 128) * ((cin + 127) / 128);
