@@ -99,8 +99,24 @@ __global__ void __launch_bounds__(256)
   uint8_t* imgA = lds;
   uint8_t* imgB = lds + kRT * 256;
   const int tm = (M + kTile - 1) / kTile;
-  const int m0 = (blockIdx.x % tm) * kTile, n0 = (blockIdx.x / tm) * kTile;
-  const int sp = blockIdx.y;
+#ifndef PCFM_RW_NOXCD
+  // XCD-contiguous deal: consecutive blocks go round-robin to the 8 XCDs, so
+  // give each XCD a contiguous run of (split, tile) items -- the tiles of one
+  // split read the same A / B row chunks and now share that XCD's L2
+  int bx, sp;
+  {
+    const int tiles = (int)gridDim.x;
+    const int tot = tiles * (int)gridDim.y;
+    int id = (int)(blockIdx.x + tiles * blockIdx.y);
+    const int q = tot / 8, rr = tot % 8, xcd = id % 8;
+    id = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + id / 8;
+    bx = id % tiles;
+    sp = id / tiles;
+  }
+#else
+  const int bx = blockIdx.x, sp = blockIdx.y;
+#endif
+  const int m0 = (bx % tm) * kTile, n0 = (bx / tm) * kTile;
   const long long nsteps = (R + kRT - 1) / kRT;
   const long long k0 = nsteps * sp / S, k1 = nsteps * (sp + 1) / S;
   const int t = threadIdx.x, lane = t & 63;
