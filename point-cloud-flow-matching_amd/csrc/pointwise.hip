@@ -15,6 +15,17 @@ namespace pcfm {
 namespace {
 
 inline int pad_to(int x, int m) { return (x + m - 1) / m * m; }
+
+// GEMM output stores are streamed (non-temporal): the outputs (80-330 MB) do
+// not fit L2 and are next read by another kernel.  256 -> 256 at N = 20000:
+// forward 112 -> 106 us, backward-data 134 -> 116 us (tools/pw_ab.py)
+__device__ __forceinline__ void out_store(float* p, float v) {
+#ifndef PCFM_PW_CACHED_STORE
+  __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
+#endif
+}
 // rows of the weight image: above 256 a multiple of 256, so the 256-row tile
 // (x read once per 256 output rows) applies -- ContextNet head_pre's backward-data
 // (M = 640 -> 768: x read 3 times instead of 5 by 128-row tiles)
@@ -157,7 +168,7 @@ __global__ void __launch_bounds__(256)
         const int dm = (e & 3) + 8 * (e >> 2) + 4 * h;
         const int m = mg + dm;
         const int p = p0 + wc * (TN / 2) + j * 32 + r;
-        if (m < M && p < N) yr[(size_t)dm * N + p] = acc[i][j][e] + bv[e];
+        if (m < M && p < N) out_store(yr + (size_t)dm * N + p, acc[i][j][e] + bv[e]);
       }
   }
 }
@@ -274,7 +285,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))
         const int dm = (e & 3) + 8 * (e >> 2) + 4 * h;
         const int m = mg + dm;
         const int p = p0 + wc * 64 + j * 32 + r;
-        if (m < M && p < N) yr[(size_t)dm * N + p] = acc[i][j][e] + bv[e];
+        if (m < M && p < N) out_store(yr + (size_t)dm * N + p, acc[i][j][e] + bv[e]);
       }
   }
 }
@@ -418,7 +429,7 @@ __global__ void __launch_bounds__(kSW * 64)
         for (int e = 0; e < 16; ++e) bv[e] = bl != nullptr ? bl[(e & 3) + 8 * (e >> 2)] : 0.0f;
         if (p < N) {
 #pragma unroll
-          for (int e = 0; e < 16; ++e) yl[((e & 3) + 8 * (e >> 2)) * N] = acc[i][e] + bv[e];
+          for (int e = 0; e < 16; ++e) out_store(yl + ((e & 3) + 8 * (e >> 2)) * N, acc[i][e] + bv[e]);
         }
       }
     }
