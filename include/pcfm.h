@@ -41,7 +41,8 @@ extern "C" {
  * 7: channel-segmented pointwise GEMMs, SE3d folded into the devoxelization;
  * 8: per-batch input bias of the head FiLM kernels; 9: split-K workspace of
  * pcfm_conv3d_igemm_cl; 10: fused AdamW + clip + EMA parameter update; 11: segment
- * plans shared by scatters over the same points). */
+ * plans shared by scatters over the same points; 12: the BatchNorm forward entry
+ * points take the module's num_batches_tracked counter). */
 int pcfm_abi_version(void);
 /* Thread-local text of the last non-zero return code. */
 const char* pcfm_last_error(void);
@@ -403,7 +404,10 @@ size_t pcfm_bn_workspace_bytes(int b, int c, int s);
  * mean / invstd = batch statistics over (b, s) per channel (biased variance,
  * invstd = 1/sqrt(var + eps)), written to mean / invstd [c].  If running_mean
  * and running_var are non-NULL they are updated in place:
- * r = (1 - momentum) * r + momentum * stat (unbiased variance for running_var). */
+ * r = (1 - momentum) * r + momentum * stat (unbiased variance for running_var).
+ * If num_batches_tracked (one int64 on the device) is non-NULL it is incremented
+ * by 1 -- the nn.BatchNorm counter torch's batch_norm path advances with a
+ * separate launch. */
 int pcfm_bn_act_fwd(const float* x, const float* gamma, const float* beta, int b, int c, int s,
                     float eps, float slope, float momentum, float* running_mean,
                     float* running_var, long long* num_batches_tracked, float* y, float* mean,

@@ -116,7 +116,7 @@ SIGNATURES = {
     "pcfm_adamw_ema_step": (_I, [_P, _P, _I, _P, _P, _I, _DP, _DP, _D, _D, _D, _D, _P]),
 }
 
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 _lock = threading.Lock()
 _lib = None
