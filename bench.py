@@ -401,8 +401,9 @@ def main():
             "vs_h100_derived_upper_bound": value / H100_DERIVED_PTS,
             "dtype": "fp32 ContextNet (scatter/gather ops fp32; Conv3d + 1x1 convs as bf16x3 "
                      "split-operand matrix-core products, fp32 accumulate, ~2^-16 per product vs "
-                     "the reference's default cuDNN TF32 2^-11) + bf16 autocast MLP head "
-                     "(reference AMP config)",
+                     "the reference's default cuDNN TF32 2^-11) + bf16 autocast per-point MLP "
+                     "head (reference AMP config; its per-cloud B-row layers -- embeddings, "
+                     "FiLM affines, latent net, encoder head -- in fp32)",
             "data": "synthetic (randn xyz, U[0,1] rgb, U[0,1] cond; no dataset on the box)",
             "config": {"workload": f"{cfg.pf_backbone} flow-matching train step, "
                                    f"B={cfg.batch_size}/GPU, N={cfg.num_points} xyz+rgb, "

@@ -169,8 +169,11 @@ def fused_trunk(trunk, h: torch.Tensor, emb: torch.Tensor, n: int) -> torch.Tens
     runs over the point columns only (K = 70 instead of 326)."""
     dt = torch.bfloat16
     blk = []
+    from pcfm.models import _batch_fp32
+    ctx, fp32 = _batch_fp32(emb)
     for seq, film in zip(trunk.blocks, trunk.films):
-        scale, shift = film.affine(emb).chunk(2, dim=-1)  # autocast: bf16 (B, W) each
+        with ctx:  # per-cloud FiLM vectors: fp32 (PCFM_BATCH_FP32=0: autocast bf16)
+            scale, shift = film.affine(emb.float() if fp32 else emb).chunk(2, dim=-1)
         sp1 = 1.0 + scale
         blk += [film.norm.weight, film.norm.bias, sp1.to(dt).contiguous(),
                 shift.to(dt).contiguous(), seq[1].weight.to(dt), seq[1].bias.to(dt)]
