@@ -11,6 +11,8 @@ it is exactly nn.Linear.forward.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -158,6 +160,9 @@ def fused_trunk_supported(trunk, h: torch.Tensor, emb: torch.Tensor, n: int) -> 
     return len(eps) <= 1
 
 
+_FILM_BATCH = os.environ.get("PCFM_FILM_BATCH", "1") != "0"  # A/B knob (dev)
+
+
 def fused_trunk(trunk, h: torch.Tensor, emb: torch.Tensor, n: int) -> torch.Tensor:
     """trunk._run_trunk(h, emb, n) through _HeadTrunkBF16 (same math, autocast casts).
 
@@ -171,12 +176,35 @@ def fused_trunk(trunk, h: torch.Tensor, emb: torch.Tensor, n: int) -> torch.Tens
     blk = []
     from pcfm.models import _batch_fp32
     ctx, fp32 = _batch_fp32(emb)
-    for seq, film in zip(trunk.blocks, trunk.films):
-        with ctx:  # per-cloud FiLM vectors: fp32 (PCFM_BATCH_FP32=0: autocast bf16)
-            scale, shift = film.affine(emb.float() if fp32 else emb).chunk(2, dim=-1)
-        sp1 = 1.0 + scale
-        blk += [film.norm.weight, film.norm.bias, sp1.to(dt).contiguous(),
-                shift.to(dt).contiguous(), seq[1].weight.to(dt), seq[1].bias.to(dt)]
+    nb = len(trunk.films)
+    if fp32 and nb > 1 and _FILM_BATCH:
+        # all blocks at once: the FiLM affines as one batched fp32 product
+        # (nb*2, B, W) and the blocks' Linear weights / biases cast to bf16 as one
+        # stacked tensor each -- a handful of launches instead of ~6 per block
+        with ctx:
+            aw = torch.stack([f.affine.weight for f in trunk.films])  # (nb, 2W, E)
+            ab = torch.stack([f.affine.bias for f in trunk.films])    # (nb, 2W)
+            w2 = aw.shape[1] // 2
+            wt = aw.view(nb * 2, w2, -1).transpose(1, 2)                # (nb*2, E, W)
+            ss = torch.baddbmm(ab.view(nb * 2, 1, w2), emb.float().expand(nb * 2, -1, -1), wt)
+            ss = ss.view(nb, 2, emb.shape[0], w2)
+            # (nb, B, W) contiguous, so each block's slice is a contiguous (B, W)
+            sp1s = (1.0 + ss[:, 0]).to(dt, memory_format=torch.contiguous_format)
+            shifts = ss[:, 1].to(dt, memory_format=torch.contiguous_format)
+        ws = torch.stack([seq[1].weight for seq in trunk.blocks]).to(dt)
+        bs = torch.stack([seq[1].bias for seq in trunk.blocks]).to(dt)
+        # unbind: one autograd node per stack, whose backward stacks the slices'
+        # gradients in one launch (per-slice indexing would zero-fill and add)
+        per = zip(sp1s.unbind(0), shifts.unbind(0), ws.unbind(0), bs.unbind(0))
+        for film, (sp1, shift, wk, bk) in zip(trunk.films, per):
+            blk += [film.norm.weight, film.norm.bias, sp1, shift, wk, bk]
+    else:
+        for seq, film in zip(trunk.blocks, trunk.films):
+            with ctx:  # per-cloud FiLM vectors: fp32 (PCFM_BATCH_FP32=0: autocast bf16)
+                scale, shift = film.affine(emb.float() if fp32 else emb).chunk(2, dim=-1)
+            sp1 = 1.0 + scale
+            blk += [film.norm.weight, film.norm.bias, sp1.to(dt).contiguous(),
+                    shift.to(dt).contiguous(), seq[1].weight.to(dt), seq[1].bias.to(dt)]
     eps = trunk.films[0].norm.eps if len(trunk.films) else 1e-5
     lin_in, lin_out = trunk.input, trunk.out[1]
     k = h.shape[1]

@@ -5,7 +5,7 @@ cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 : > gpurun_out/ab_env.jsonl
-for rep in 1 2; do
+for rep in ${REPS:-1 2}; do
   for E in base ${ENVS}; do
     if [ $E = base ]; then
       timeout -k 10 200 python bench.py --no-cpu-baseline --no-chamfer --steps 20 > gpurun_out/ab_one.json 2>/dev/null
