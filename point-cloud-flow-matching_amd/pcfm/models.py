@@ -51,6 +51,8 @@ def timestep_embedding(t: torch.Tensor, dim: int, max_period: float = 10000.0) -
 # the ~100 tiny cast launches per train step autocast spends on them.
 # PCFM_BATCH_FP32=0 restores autocast's bf16 for them.
 _BATCH_FP32 = os.environ.get("PCFM_BATCH_FP32", "1") != "0"
+# ContextNet's PV-block FiLM affines as batched products (A/B knob, dev)
+_FILM_GROUPS = os.environ.get("PCFM_FILM_GROUPS", "1") != "0"
 
 
 def _batch_fp32(ref: torch.Tensor):
@@ -323,12 +325,15 @@ class _PVBlock(nn.Module):
         self.film = _FiLM1d(channels, emb_dim, norm_type=norm_type, gn_groups=gn_groups,
                             one_plus=True)
 
-    def forward(self, feat_coords: Tuple[torch.Tensor, torch.Tensor], emb: torch.Tensor):
+    def forward(self, feat_coords: Tuple[torch.Tensor, torch.Tensor], emb: torch.Tensor,
+                gb: Optional[Tuple[torch.Tensor, torch.Tensor]] = None):
+        """gb: this block's (gamma, beta) = film.affine(emb) precomputed by
+        ContextNet with the other blocks' in one batched product."""
         f, c = self.post(self.pvconv(feat_coords))
         film = self.film
         if film.one_plus and isinstance(film.norm, nn.GroupNorm):
             # f + GroupNorm(f) * (1 + gamma) + beta as one fused op (modules/norm_act.py)
-            gamma, beta = film.affine(emb.to(f.dtype)).chunk(2, dim=-1)
+            gamma, beta = gb if gb is not None else film.affine(emb.to(f.dtype)).chunk(2, dim=-1)
             return gn_film_residual(f, film.norm, gamma, beta), c
         return f + film(f, emb), c
 
@@ -346,13 +351,13 @@ class _PVStage(nn.Module):
                      gn_groups=gn_groups, voxel_normalize=voxel_normalize)
             for _ in range(int(num_blocks))])
 
-    def forward(self, feat: torch.Tensor, coords: torch.Tensor, emb: torch.Tensor):
+    def forward(self, feat: torch.Tensor, coords: torch.Tensor, emb: torch.Tensor, gbs=None):
         f, c = self.proj((feat, coords))
-        return self.run_blocks(f, c, emb)
+        return self.run_blocks(f, c, emb, gbs)
 
-    def run_blocks(self, f: torch.Tensor, c: torch.Tensor, emb: torch.Tensor):
-        for blk in self.blocks:
-            f, c = blk((f, c), emb)
+    def run_blocks(self, f: torch.Tensor, c: torch.Tensor, emb: torch.Tensor, gbs=None):
+        for i, blk in enumerate(self.blocks):
+            f, c = blk((f, c), emb, None if gbs is None else gbs[i])
         return f, c
 
 
@@ -486,6 +491,34 @@ class ContextNet(_TimeCondEmbed):
         pre = _PointwiseParts.apply(w[:, e:], bias_b, pts)
         return bn_act(pre, bn, 0.0)
 
+    def _block_films(self, emb32: torch.Tensor):
+        """Every PV block's FiLM (gamma, beta) = affine(emb) (models.py:322-346),
+        the blocks of equal width as one batched product (nb*2, B, C) -- each
+        gamma / beta a contiguous (B, C) slice -- instead of one Linear, two
+        copies and their backward per block.  None per stage when a block's FiLM
+        is not the fused GroupNorm form (the block then runs its own affine)."""
+        if not (emb32.is_cuda and _FILM_GROUPS):
+            return [None] * len(self.stages)
+        films = [(si, bi, blk.film) for si, st in enumerate(self.stages)
+                 for bi, blk in enumerate(st.blocks)]
+        if not all(f.one_plus and isinstance(f.norm, nn.GroupNorm) for _, _, f in films):
+            return [None] * len(self.stages)
+        out = [[None] * len(st.blocks) for st in self.stages]
+        by_c: dict = {}
+        for si, bi, f in films:
+            by_c.setdefault(f.affine.out_features, []).append((si, bi, f))
+        for oc, group in by_c.items():
+            c = oc // 2
+            aw = torch.stack([f.affine.weight for _, _, f in group])  # (g, 2C, E)
+            ab = torch.stack([f.affine.bias for _, _, f in group])    # (g, 2C)
+            ng = len(group)
+            wt = aw.view(ng * 2, c, -1).transpose(1, 2)                 # (2g, E, C)
+            gb = torch.baddbmm(ab.view(ng * 2, 1, c), emb32.expand(ng * 2, -1, -1), wt)
+            parts = gb.unbind(0)  # one autograd node: its backward stacks the grads
+            for j, (si, bi, _) in enumerate(group):
+                out[si][bi] = (parts[2 * j], parts[2 * j + 1])
+        return out
+
     def _head_pre(self, scales: List[torch.Tensor], g: Optional[torch.Tensor]) -> torch.Tensor:
         """head_pre(cat(scales | g broadcast over points)) (models.py:460-466).
 
@@ -522,15 +555,16 @@ class ContextNet(_TimeCondEmbed):
             c = coords.float()
             emb32 = emb.float()
             scales = []
+            gbs = self._block_films(emb32)
             f = self._stem_proj(pts, emb32, c)
             if f is None:  # stem = cat([emb broadcast over the points, xyz, rgb])
                 stem = torch.cat([emb[:, :, None].expand(b, self.emb_dim, n)] + pts, dim=1)
-                f, c = self.stages[0](stem.float(), c, emb32)
+                f, c = self.stages[0](stem.float(), c, emb32, gbs[0])
             else:
-                f, c = self.stages[0].run_blocks(f, c, emb32)
+                f, c = self.stages[0].run_blocks(f, c, emb32, gbs[0])
             scales.append(f)
-            for stage in self.stages[1:]:
-                f, c = stage(f, c, emb32)
+            for stage, gb in zip(self.stages[1:], gbs[1:]):
+                f, c = stage(f, c, emb32, gb)
                 scales.append(f)
             g = self.global_mlp(f.max(dim=-1).values) if self.with_global else None
             pre = self._head_pre(scales, g)
