@@ -233,16 +233,49 @@ def ball_query_ms(dev, b, n, m, radius, u, iters=5):
             "distance_tests_per_s_upper": b * m * n / (ms * 1e-3)}
 
 
+def launch_ranks(args, backend):
+    """`bench.py --gpus N` run directly (no WORLD_SIZE in the env): start N ranks
+    as a `torch.distributed.run` child -- the reference's `torchrun --standalone
+    --nproc_per_node=N` recipe (train.py:810-826) -- and exit with its code.
+    Runs before anything touches the GPU (device_count() does not, on ROCm)."""
+    import socket
+    import subprocess
+    ndev = torch.cuda.device_count()
+    if backend == "nccl" and args.gpus > ndev:
+        log(f"--gpus {args.gpus} but only {ndev} GPU(s) visible: one rank per GPU over RCCL")
+        sys.exit(2)
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1", f"--master-port={port}",
+           os.path.abspath(__file__), *sys.argv[1:]]
+    log("launching:", " ".join(cmd))
+    sys.exit(subprocess.call(cmd, env=dict(os.environ, MASTER_ADDR="127.0.0.1")))
+
+
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    ddp = world > 1
     # one process per GPU; PCFM_DIST_BACKEND=gloo rehearses the N > 1 path with
     # several ranks sharing the GPUs there are (dev knob; the product path is RCCL)
     backend = os.environ.get("PCFM_DIST_BACKEND", "nccl")
-    local = local % max(1, torch.cuda.device_count())
+    if args.gpus < 1:
+        log("--gpus must be >= 1")
+        sys.exit(2)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        launch_ranks(args, backend)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"WORLD_SIZE={world} but --gpus {args.gpus}: launch one rank per GPU")
+        sys.exit(2)
+    ndev = torch.cuda.device_count()
+    if backend == "nccl" and world > ndev:
+        log(f"{world} ranks but only {ndev} GPU(s) visible: one rank per GPU over RCCL")
+        sys.exit(2)
+    ddp = world > 1
+    local = local % max(1, ndev)
     if ddp:
         torch.cuda.set_device(local)
         dist.init_process_group(backend, init_method="env://")

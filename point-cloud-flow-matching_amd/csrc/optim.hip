@@ -63,19 +63,26 @@ __global__ void __launch_bounds__(256)
   double s = 0.0;
   for (int i = threadIdx.x; i < nchunks; i += 256) s += part[i];
   s = block_sum_d(s, sh);
-  // fused AdamW: a step skipped for a non-finite gradient does not count
-  if (isfinite(s))
+  // The inf check is GradScaler's (train.py:652-657 with amp on): only with a
+  // scale does a non-finite gradient skip the update -- and, as in
+  // AdamW(fused=True), the step count.  Without one (amp off) torch's AdamW
+  // steps anyway and the non-finite values reach the parameters.
+  const bool found = scale != nullptr && !isfinite(s);
+  if (!found)
     for (int t = threadIdx.x; t < ntensors; t += 256)
       if (!(tab[t].flags & kSkip)) steps[t] += 1.0f;
   if (threadIdx.x != 0) return;
   // GradScaler._unscale_grads_: inv_scale = scale.double().reciprocal().float()
   const float inv = scale != nullptr ? (float)(1.0 / (double)scale[0]) : 1.0f;
-  const bool found = !isfinite(s);
   // clip_grad_norm_ over the unscaled gradients (g * inv is exact: the scale is
-  // a power of two), fp32 coefficient arithmetic as torch
+  // a power of two), fp32 coefficient arithmetic as torch; clamp(max=1) keeps
+  // a NaN coefficient NaN (fminf would not)
   const float total = (float)(sqrt(s) * (double)inv);
   float coef = 1.0f;
-  if (max_norm > 0.0f) coef = fminf(max_norm / (total + 1e-6f), 1.0f);
+  if (max_norm > 0.0f) {
+    const float c = max_norm / (total + 1e-6f);
+    coef = isnan(c) ? c : fminf(c, 1.0f);
+  }
   state[0] = total;
   state[1] = inv * coef;
   state[2] = found ? 1.0f : 0.0f;

@@ -96,6 +96,11 @@ size_t seg_sort_stable_ws(int B, int n, int V) {
 int seg_sort_stable(const int* key, long long key_bstride, int B, int n, int V, int* start,
                     int* cnt_out, float* vinv, int* rank, void* ws, hipStream_t st) {
   const long long total = (long long)B * n;
+  // composite keys are 32-bit unsigned, values / permutation 32-bit int
+  PCFM_CHECK_ARG((unsigned long long)B * ((unsigned long long)V + 1) <= 0xffffffffull,
+                 "segment sort: B * (V + 1) = %llu exceeds 32-bit keys",
+                 (unsigned long long)B * ((unsigned long long)V + 1));
+  PCFM_CHECK_ARG(total <= 0x7fffffffll, "segment sort: B * n = %lld exceeds int indices", total);
   char* p = (char*)ws;
   auto take = [&p](size_t bytes) {
     char* q = p;

@@ -210,7 +210,11 @@ class ShapeEncoder(nn.Module):
         pooled = max_over_points(h)
         ctx, fp32 = _batch_fp32(pooled)
         with ctx:
-            return self.head(pooled.float() if fp32 else pooled), h
+            z = self.head(pooled.float() if fp32 else pooled)
+        # z leaves in autocast's dtype, as the reference's autocast Linear returns
+        # it: the latent FM draws, interpolants and targets (train.py:636-641) and
+        # the point flow's condition then carry the reference's bf16 rounding
+        return (z.to(torch.bfloat16) if fp32 else z), h
 
 
 class ConditionalLatentVelocityNet(_TimeCondEmbed):
@@ -237,10 +241,11 @@ class ConditionalLatentVelocityNet(_TimeCondEmbed):
 
     def forward(self, y, t, cond, cond_drop_p: float = 0.0):
         ctx, fp32 = _batch_fp32(y)
-        if fp32:  # the whole net acts on B rows
+        if fp32:  # the whole net acts on B rows; its output in autocast's dtype
             with ctx:
-                return self._forward(y.float(), t, None if cond is None else cond.float(),
-                                     cond_drop_p)
+                v = self._forward(y.float(), t, None if cond is None else cond.float(),
+                                  cond_drop_p)
+            return v.to(torch.bfloat16)
         return self._forward(y, t, cond, cond_drop_p)
 
     def _forward(self, y, t, cond, cond_drop_p: float = 0.0):

@@ -119,6 +119,67 @@ class FusedAdamWEMA:
             elif p.grad is not None:
                 p.grad.zero_()
 
+    # checkpoint layout of torch.optim.AdamW (the reference saves opt.state_dict()
+    # with every checkpoint and restores it on resume, train.py:501, :701)
+    def _moments(self, i: int):
+        off = int(self._tab[i]["m"] - self.exp_avg.data_ptr()) // 4
+        p = self.params[i]
+        n = p.numel()
+        return (self.exp_avg[off:off + n].view_as(p), self.exp_avg_sq[off:off + n].view_as(p))
+
+    def state_dict(self) -> Dict:
+        """{'state': {index: {'step', 'exp_avg', 'exp_avg_sq'}}, 'param_groups':
+        [...]} as torch.optim.AdamW.state_dict() lays it out: parameters numbered
+        in group order, an entry only for parameters that have taken a step,
+        `step` a float32 scalar tensor on the CPU."""
+        steps = self.steps.cpu()
+        state = {}
+        for i in range(len(self.params)):
+            if float(steps[i]) > 0:
+                m, v = self._moments(i)
+                state[i] = {"step": steps[i].clone(), "exp_avg": m.clone(),
+                            "exp_avg_sq": v.clone()}
+        groups, k = [], 0
+        for g in self.param_groups:
+            n = len(g["params"])
+            groups.append({"lr": g["lr"], "betas": self.betas, "eps": self.eps,
+                           "weight_decay": g["weight_decay"], "amsgrad": False,
+                           "maximize": False, "foreach": None, "capturable": False,
+                           "differentiable": False, "fused": None,
+                           "params": list(range(k, k + n))})
+            k += n
+        return {"state": state, "param_groups": groups}
+
+    def load_state_dict(self, sd: Dict) -> None:
+        """Accepts torch.optim.AdamW's (or this class's) state_dict: moments and
+        step counts per parameter, lr / weight decay per group."""
+        groups = sd["param_groups"]
+        if len(groups) != len(self.param_groups) or any(
+                len(a["params"]) != len(b["params"]) for a, b in zip(groups, self.param_groups)):
+            raise ValueError("FusedAdamWEMA.load_state_dict: parameter groups do not match")
+        if any(g.get("amsgrad") or g.get("maximize") for g in groups):
+            raise ValueError("FusedAdamWEMA.load_state_dict: amsgrad / maximize unsupported")
+        if any(tuple(g.get("betas", self.betas)) != self.betas
+               or float(g.get("eps", self.eps)) != self.eps for g in groups):
+            raise ValueError("FusedAdamWEMA.load_state_dict: betas / eps differ")
+        index = [i for g in groups for i in g["params"]]
+        steps = torch.zeros(len(self.params))
+        with torch.no_grad():
+            self.exp_avg.zero_()
+            self.exp_avg_sq.zero_()
+            for pos, key in enumerate(index):
+                st = sd["state"].get(key)
+                if st is None:
+                    continue
+                m, v = self._moments(pos)
+                m.copy_(st["exp_avg"])
+                v.copy_(st["exp_avg_sq"])
+                steps[pos] = float(st["step"])
+            self.steps.copy_(steps)
+        for mine, g in zip(self.param_groups, groups):
+            mine["lr"] = float(g["lr"])
+            mine["weight_decay"] = float(g["weight_decay"])
+
     @property
     def last_grad_norm(self) -> torch.Tensor:
         """clip_grad_norm_'s return value of the last step (device scalar)."""

@@ -412,6 +412,26 @@ class Trainer:
         randn | rgb rand), t_pts (B,), drop_u (B,) CFG-drop uniforms, eps_z
         (B, latent) randn, t_z (B,) -- scaled by the configured stds here as the
         reference scales its own draws (train.py:271-276, :595, :617, :637)."""
+        out = self.forward_backward(batch, epoch, draws)
+        self._update_params()
+
+        self.ema_pf.update(self.pf)
+        self.ema_lf.update(self.lf)
+
+        if self.cfg.use_cosine_lr:
+            cfg = self.cfg
+            for group, base in zip(self.opt.param_groups, (cfg.lr_enc, cfg.lr_pf, cfg.lr_lf)):
+                group["lr"] = cosine_lr(self.global_step, self.total_steps, base, cfg.min_lr,
+                                        cfg.warmup_steps)
+        self.global_step += 1
+        return out
+
+    def forward_backward(self, batch: Dict[str, torch.Tensor], epoch: int,
+                         draws: Optional[Dict[str, torch.Tensor]] = None
+                         ) -> Dict[str, torch.Tensor]:
+        """The step up to and including the scaled backward (train.py:553-652):
+        afterwards every parameter's .grad holds the loss-scaled gradient -- under
+        DDP the all-reduced mean over the ranks -- and nothing is updated yet."""
         cfg = self.cfg
         dev = self.device
         dr = None if draws is None else {k: v.to(dev) for k, v in draws.items()}
@@ -481,14 +501,4 @@ class Trainer:
 
         loss = cfg.lambda_point * loss_point + cfg.lambda_latent * loss_latent
         self.scaler.scale(loss).backward()
-        self._update_params()
-
-        self.ema_pf.update(self.pf)
-        self.ema_lf.update(self.lf)
-
-        if cfg.use_cosine_lr:
-            for group, base in zip(self.opt.param_groups, (cfg.lr_enc, cfg.lr_pf, cfg.lr_lf)):
-                group["lr"] = cosine_lr(self.global_step, self.total_steps, base, cfg.min_lr,
-                                        cfg.warmup_steps)
-        self.global_step += 1
         return {"loss_point": loss_point.detach(), "loss_latent": loss_latent.detach()}

@@ -34,3 +34,26 @@ def test_ddp_two_ranks_stay_in_sync(tmp_path):
     np.testing.assert_array_equal(s0, s1)
     l0, l1 = d["losses"]
     assert np.all(np.isfinite(l0)) and l0 != l1
+
+
+def test_ddp_grad_is_mean_of_shard_grads(tmp_path, report):
+    """SURVEY §8(e) on the HIP path: two ranks (gloo, sharing cuda:0), each with
+    its own B=8 shard; each rank's losses equal the one-process forward on its
+    shard bit for bit, and the all-reduced gradient equals the mean of the two
+    one-process per-shard gradients (tests/helpers/ddp_grad_rank.py)."""
+    out = tmp_path / "grad.json"
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", "29534",
+           os.path.join(REPO, "tests", "helpers", "ddp_grad_rank.py"), str(out)]
+    subprocess.run(cmd, check=True, timeout=300, env=env, cwd=REPO)
+    res = [json.load(open(f"{out}.{r}")) for r in range(2)]
+    report("ddp_grad_mean", res)
+    for r, d in enumerate(res):
+        assert d["world"] == 2 and d["backend"] == "gloo"
+        assert d["losses"] == d["ref_losses"][r], (d["losses"], d["ref_losses"])
+        # 1e-6 of each gradient's max |.| (the all-reduce's mean of two fp32 terms;
+        # a division by 2 is exact, so in practice the gradients are bit-equal)
+        assert d["max_rel"] <= 1e-6, d
+        assert d["grad_sums_equal_across_ranks"]
+    assert res[0]["losses"] != res[1]["losses"]

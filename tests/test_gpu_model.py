@@ -113,7 +113,9 @@ def test_hybrid_gpu_matches_reference(golden, report, mode, perturbed):
         assert e_v < 1e-5 and e_loss < 1e-5 and e_g < 1e-3 and e_se < 2e-3, (e_v, e_loss, e_g,
                                                                              e_se, worst)
     else:
-        assert e_v < 1e-4 and e_loss < 1e-4 and e_g < 1e-2 and e_se < 3e-2, (e_v, e_loss, e_g,
+        # bf16x3 products (~2^-16 each): v / loss measured 2.4e-6 / 2.6e-6 on
+        # MI355X, held to north_star's 1e-5
+        assert e_v < 1e-5 and e_loss < 1e-5 and e_g < 1e-2 and e_se < 3e-2, (e_v, e_loss, e_g,
                                                                              e_se, worst)
 
 

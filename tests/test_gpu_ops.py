@@ -368,3 +368,26 @@ def test_emd_known_answer(golden):
     loss.backward()
     np.testing.assert_allclose(np_(p1.grad), g["gt_grad1"] / 2, rtol=1e-3, atol=1e-5)
     np.testing.assert_allclose(np_(p2.grad), g["gt_grad2"] / 2, rtol=1e-3, atol=1e-5)
+
+
+def test_chamfer_c2_product_path(tmp_path, report):
+    """The brute-force split-candidate Chamfer kernel the product runs at C2
+    (B=8, N=M=20000), with the session's culling override removed: sampled
+    queries bit-exact against the oracle's full scan (exact hits and duplicate
+    candidates: lowest index on ties), backward within 1e-5
+    (tests/helpers/chamfer_c2_product.py; chamfer3D.cu:12-174)."""
+    import json
+    import os
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k != "PCFM_CHAMFER_CULL_PAIRS"}
+    out = tmp_path / "c2.json"
+    subprocess.run([sys.executable, os.path.join(repo, "tests", "helpers",
+                                                 "chamfer_c2_product.py"), str(out)],
+                   check=True, timeout=240, env=env, cwd=repo)
+    d = json.load(open(out))
+    report("chamfer_c2_product_path", d)
+    assert d["mismatches"] == {"d1": 0, "i1": 0, "d2": 0, "i2": 0}, d
+    assert d["queries_checked"] == 8 * 2 * 400 and d["exact_hits"] >= 8 * 3000
+    assert d["bwd_close"], d

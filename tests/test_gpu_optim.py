@@ -147,3 +147,118 @@ def test_trainer_fused_step_matches_torch_path():
     bound = max(1e-3 * 3e-4 * 2 * max(1.0, np.abs(pt).max()), 2 * 2 * lr_max)
     assert d.max() <= bound, (d.max(), bound)
     np.testing.assert_allclose(ef, et, rtol=1e-6, atol=1e-6)
+
+
+def test_fused_adamw_without_scaler_steps_through_nan():
+    """amp off (no GradScaler): torch's clip_grad_norm_ + AdamW step anyway and
+    the NaN reaches the parameters; the fused update must not skip."""
+    from pcfm.optim import FusedAdamWEMA
+    g, ps, shadows = _setup(4)
+    ref_ps = [p.clone() for p in ps]
+    fused = FusedAdamWEMA([{"params": ps, "lr": 1e-3, "weight_decay": 1e-4}])
+    ref_opt = torch.optim.AdamW([{"params": ref_ps, "lr": 1e-3}], weight_decay=1e-4,
+                                foreach=True)
+    grads = [torch.randn(p.shape, device=DEV, generator=g) for p in ps]
+    grads[2][1] = float("nan")
+    for p, gr in zip(ps, grads):
+        p.grad = gr.clone()
+    fused.step(1.0, None)
+    for p, gr in zip(ref_ps, grads):
+        p.grad = gr.clone()
+    torch.nn.utils.clip_grad_norm_(ref_ps, 1.0)
+    ref_opt.step()
+    for a, b in zip(ps, ref_ps):
+        assert torch.equal(torch.isnan(a), torch.isnan(b))
+    assert all(torch.isnan(p).all() for p in ps)  # the NaN norm scales every gradient
+    assert float(fused.steps.min()) == 1.0 and float(fused.found_inf) == 0.0
+
+
+def test_fused_adamw_state_dict_round_trips_with_torch():
+    """state_dict / load_state_dict in torch.optim.AdamW's layout (the reference
+    checkpoints opt.state_dict(), train.py:501, :701): torch -> fused and
+    fused -> torch, then one more step on both must agree."""
+    from pcfm.optim import FusedAdamWEMA
+    g, ps, _ = _setup(5)
+    split = [slice(0, 4), slice(4, len(ps))]
+    lrs, wd = (3e-4, 1e-3), 1e-4
+    ref_ps = [p.clone() for p in ps]
+    ref_opt = torch.optim.AdamW([{"params": ref_ps[s], "lr": lr} for s, lr in zip(split, lrs)],
+                                weight_decay=wd, foreach=True)
+    for step in range(2):
+        for p in ref_ps:
+            p.grad = None if (step == 1 and p is ref_ps[6]) else torch.randn(
+                p.shape, device=DEV, generator=g)
+        ref_opt.step()
+    fused = FusedAdamWEMA([{"params": ps[s], "lr": 0.5, "weight_decay": 0.5} for s in split])
+    with torch.no_grad():
+        for a, b in zip(ps, ref_ps):
+            a.copy_(b)
+    fused.load_state_dict(ref_opt.state_dict())
+    assert [g_["lr"] for g_ in fused.param_groups] == list(lrs)
+    sd = fused.state_dict()
+    for k, st in ref_opt.state_dict()["state"].items():
+        assert float(sd["state"][k]["step"]) == float(st["step"])
+        assert torch.equal(sd["state"][k]["exp_avg"], st["exp_avg"])
+        assert torch.equal(sd["state"][k]["exp_avg_sq"], st["exp_avg_sq"])
+    grads = [torch.randn(p.shape, device=DEV, generator=g) for p in ps]
+    for a, b, gr in zip(ps, ref_ps, grads):
+        a.grad, b.grad = gr.clone(), gr.clone()
+    fused.step(0.0, None)
+    ref_opt.step()
+    for a, b in zip(ps, ref_ps):
+        torch.testing.assert_close(a, b, rtol=2e-6, atol=1e-8)
+    # fused -> a fresh torch AdamW
+    ref2 = [p.detach().clone() for p in ps]
+    opt2 = torch.optim.AdamW([{"params": ref2[s], "lr": 9.0} for s in split], weight_decay=wd,
+                             foreach=True)
+    opt2.load_state_dict(fused.state_dict())
+    for a, b in zip(ps, ref2):
+        gr = torch.randn(a.shape, device=DEV, generator=g)
+        a.grad, b.grad = gr.clone(), gr.clone()
+    fused.step(0.0, None)
+    opt2.step()
+    for a, b in zip(ps, ref2):
+        torch.testing.assert_close(a, b, rtol=2e-6, atol=1e-8)
+
+
+def test_trainer_fused_first_step_elementwise():
+    """One Trainer step, fused vs torch path, compared element by element
+    (ADVICE r2): the moments at 1e-5, and the parameters within 1e-6 relative +
+    1e-3 lr except where the unscaled, clipped gradient is below 1e-6 -- there
+    AdamW's first step m / (sqrt(v) + eps) = g / (|g| + eps) depends on eps and
+    on the gradient's last bits, so the step itself (up to lr) is rounding."""
+    from pcfm.train import TrainConfig, Trainer, synthetic_batch
+    cfg = dict(batch_size=2, num_points=1024, steps_per_epoch=4, epochs=1, tunableop=False,
+               miopen_find=False, device_rng=False)
+    res = {}
+    for fused in (True, False):
+        tr = Trainer(TrainConfig(fused_step=fused, **cfg), DEV)
+        tr.train_mode()
+        batch = synthetic_batch(tr.cfg, DEV, generator=torch.Generator(device=DEV).manual_seed(3))
+        torch.manual_seed(5)
+        p0 = [p.detach().clone() for p in tr._clip_params]
+        tr.forward_backward(batch, epoch=201)
+        inv = 1.0 / tr.scaler.get_scale()
+        gr = [None if p.grad is None else p.grad.detach().clone() * inv for p in tr._clip_params]
+        tr._update_params()
+        sd = tr.opt.state_dict()["state"]
+        res[fused] = (p0, gr, [p.detach().clone() for p in tr._clip_params], sd,
+                      float(tr.last_grad_norm))
+    p0f, gf, pf, sdf, nf = res[True]
+    p0t, gt, pt, sdt, nt = res[False]
+    assert all(torch.equal(a, b) for a, b in zip(p0f, p0t))
+    assert abs(nf - nt) <= 1e-5 * nt
+    coef = min(1.0, 1.0 / (nt + 1e-6))
+    lr = 3e-4  # the groups' initial lr (the schedule is applied after the step)
+    for i, (g1, g2) in enumerate(zip(gf, gt)):
+        if g1 is None:
+            assert g2 is None and i not in sdf and i not in sdt
+            continue
+        torch.testing.assert_close(g1, g2, rtol=0, atol=0)  # same forward / backward bits
+        torch.testing.assert_close(sdf[i]["exp_avg"], sdt[i]["exp_avg"], rtol=1e-5, atol=1e-12)
+        torch.testing.assert_close(sdf[i]["exp_avg_sq"], sdt[i]["exp_avg_sq"], rtol=1e-5,
+                                   atol=1e-18)
+        live = (g1 * coef).abs() >= 1e-6
+        d = (pf[i] - pt[i]).abs()
+        bound = 1e-6 * pt[i].abs() + 1e-3 * lr
+        assert bool((d[live] <= bound[live]).all()), (i, float(d[live].max()))

@@ -16,6 +16,8 @@ random draws (tests/train_replay.py).
   * the reference's post-epoch Heun sampling with the EMA weights
     (train.py:282-429) replayed through pcfm.sample.heun: 1e-5 exact-fp32,
     1e-4 bf16x3.
+  * dopri5 through pcfm.sample on the same EMA flow against the reference's
+    vendored torchdiffeq 0.2.2 (tests/golden/dopri5_torchdiffeq.npz).
   * the production step (bf16 autocast on the head as the reference trains on
     GPU, train.py:580-645): reported and bounded at 2e-2 -- bf16 rounding.
 """
@@ -52,6 +54,19 @@ def test_exact_fp32_step_matches_reference(golden, report):
     report("sampling_golden_exact_fp32", smp)
     for k, v in smp.items():
         assert v < 1e-5, (k, smp)
+    # dopri5 (BASELINE configs[3]) against the reference's vendored torchdiffeq
+    # on the same EMA flow: NFE and step sequence equal at rtol = atol = 1e-3,
+    # y(1) within 1e-5.  At 1e-5 the fp32 error estimate carries the slopes'
+    # rounding (test_sample_cpu.py), so there y(1) is held to the tolerance the
+    # solver was asked for and the NFE to within one step.
+    with exact_fp32():
+        d5 = train_replay.replay_dopri5(golden("dopri5_torchdiffeq.npz"),
+                                        golden("train_step_c1.npz"), tr)
+    report("dopri5_golden_exact_fp32", d5)
+    r = d5["hybrid_c1_3"]
+    assert r["nfe"] == r["nfe_ref"] and r["times"] < 1e-6 and r["y1"] < 1e-5, d5
+    r = d5["hybrid_c1_5"]
+    assert abs(r["nfe"] - r["nfe_ref"]) <= 6 and r["y1"] < 1e-5, d5
 
 
 def test_bf16x3_step_deviation(golden, report):

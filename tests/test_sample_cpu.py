@@ -67,3 +67,84 @@ def test_generate_end_to_end_cpu(oracle_backend):
     x2, nfe2 = sample.generate(pf, lf, 2, 200, point_dim=6, latent_dim=8, cond=cond, steps=2,
                                method="dopri5_fixed")
     assert x2.shape == (2, 200, 6) and nfe2 == 1 + 2 * 6
+
+
+# ---------------------------------------------------------------------------
+# dopri5 against the reference's vendored torchdiffeq 0.2.2 (the golden's own
+# outputs: tests/golden/make_dopri5_golden.py)
+# ---------------------------------------------------------------------------
+def _golden_case(golden, name):
+    import numpy as np
+    g = golden("dopri5_torchdiffeq.npz")
+    return (torch.from_numpy(g[f"{name}_y0"]), g[f"{name}_y1"], g[f"{name}_times"],
+            int(g[f"{name}_nfe"]), tuple(float(v) for v in g[f"{name}_tol"]), np)
+
+
+def _field(name):
+    import sys
+    import os
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+    import make_dopri5_golden as M
+    if name == "decay_f64":
+        return lambda y, t: -(1.0 + t[:, None]) * y
+    dtype = torch.float64 if "_f64_" in name else torch.float32
+    return M.tanh_field(dtype)[0]
+
+
+@pytest.mark.parametrize("name", ["decay_f64", "tanh_f64_3", "tanh_f64_5", "tanh_f32_3",
+                                  "tanh_f32_5"])
+def test_dopri5_matches_vendored_torchdiffeq(golden, name):
+    """Same NFE, the same evaluation times (the accepted / rejected step
+    sequence) and y(1) within 1e-5 of the vendored solver's (in practice
+    bit-equal: the same tensor operations in the same order)."""
+    y0, y1_ref, times_ref, nfe_ref, (rtol, atol), np = _golden_case(golden, name)
+    times = []
+    y1, nfe = sample.dopri5(_field(name), y0, rtol=rtol, atol=atol, trace=times)
+    assert nfe == nfe_ref
+    np.testing.assert_array_equal(np.array(times), times_ref)
+    y1 = y1.numpy()
+    assert np.abs(y1 - y1_ref).max() <= 1e-5 * np.abs(y1_ref).max()
+    np.testing.assert_array_equal(y1, y1_ref)
+
+
+def test_dopri5_decay_closed_form(golden):
+    y0, y1_ref, _, _, _, np = _golden_case(golden, "decay_f64")
+    exact = y0.numpy() * math.exp(-1.5)
+    assert np.abs(y1_ref - exact).max() < 1e-5
+
+
+@pytest.fixture(scope="module")
+def c1_ema_flow():
+    """The C1 hybrid point flow with the EMA weights after replaying the
+    reference's two recorded steps on the product CPU backend."""
+    import os
+    import sys
+    import numpy as np
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, here)
+    from train_replay import replay
+    g = np.load(os.path.join(here, "golden", "train_step_c1.npz"), allow_pickle=False)
+    _, _, tr = replay(g, "cpu")
+    tr.ema_pf.copy_to(tr.pf)
+    tr.pf.eval()
+    return tr.pf
+
+
+def test_dopri5_hybrid_flow_matches_vendored_torchdiffeq(golden, c1_ema_flow):
+    """The C1 hybrid flow through dopri5 (BASELINE configs[3]'s sampler) at
+    rtol = atol = 1e-3: NFE and evaluation times equal to torchdiffeq's, y(1)
+    within 1e-5.  (The golden's 1e-5 case runs on the GPU only,
+    test_gpu_sample.py: at ~3.7 s per CPU velocity its 38 evaluations do not
+    fit the CPU suite.  At that tolerance an fp32 state's error estimate,
+    ~1e-5 |y|, is a difference of stage slopes that carries their rounding, so
+    velocities that differ in their last bits -- the CPU GEMMs' thread count --
+    move the accepted step sizes by ~1e-4 relative; same-thread-count runs
+    reproduce the golden bit for bit.)"""
+    x0, y1_ref, times_ref, nfe_ref, (rtol, atol), np = _golden_case(golden, "hybrid_c1_3")
+    cond = torch.from_numpy(golden("train_step_c1.npz")["recon_cond"])
+    times = []
+    y1, nfe = sample.dopri5(lambda x, t: c1_ema_flow.guided_velocity(x, t, cond), x0,
+                            rtol=rtol, atol=atol, trace=times)
+    assert nfe == nfe_ref
+    np.testing.assert_allclose(np.array(times), times_ref, rtol=1e-6, atol=0)
+    assert np.abs(y1.numpy() - y1_ref).max() <= 1e-5 * np.abs(y1_ref).max()

@@ -201,3 +201,30 @@ def replay_sampling(g, tr, amp: bool = False):
     out["samples_v"] = max(rel(a, b) for a, b in zip(vs, g["samples_pf_v"]))
     out["samples_xyz"] = rel(x[..., :3].float().cpu().numpy(), g["samples_final_xyz"])
     return out
+
+
+def replay_dopri5(gd, g, tr, names=("hybrid_c1_3", "hybrid_c1_5")):
+    """The golden's dopri5 cases of the C1 hybrid flow (tests/golden/
+    dopri5_torchdiffeq.npz, made by the reference's vendored torchdiffeq 0.2.2)
+    through pcfm.sample.dopri5 on the Trainer after replay() + replay_sampling()
+    (EMA weights, eval mode).  Returns {case: {nfe, nfe_ref, times (max abs
+    difference of the evaluation times, when the counts agree), y1 (max |dy| /
+    max |y_ref|)}}."""
+    from pcfm.sample import dopri5
+    dev = tr.device
+    cond = torch.from_numpy(g["recon_cond"]).to(dev)
+    out = {}
+    for name in names:
+        rtol, atol = (float(v) for v in gd[f"{name}_tol"])
+        times = []
+        y1, nfe = dopri5(lambda x, t: tr.pf.guided_velocity(x, t, cond),
+                         torch.from_numpy(gd[f"{name}_y0"]).to(dev), rtol=rtol, atol=atol,
+                         trace=times)
+        ref = gd[f"{name}_y1"]
+        t_ref = gd[f"{name}_times"]
+        out[name] = {"nfe": nfe, "nfe_ref": int(gd[f"{name}_nfe"]),
+                     "times": float(np.abs(np.array(times) - t_ref).max())
+                     if len(times) == len(t_ref) else None,
+                     "y1": float(np.abs(y1.float().cpu().numpy() - ref).max()
+                                 / np.abs(ref).max())}
+    return out
