@@ -42,7 +42,8 @@ extern "C" {
  * 8: per-batch input bias of the head FiLM kernels; 9: split-K workspace of
  * pcfm_conv3d_igemm_cl; 10: fused AdamW + clip + EMA parameter update; 11: segment
  * plans shared by scatters over the same points; 12: the BatchNorm forward entry
- * points take the module's num_batches_tracked counter). */
+ * points take the module's num_batches_tracked counter; 13: occupancy-masked
+ * voxel convolution entry points). */
 int pcfm_abi_version(void);
 /* Thread-local text of the last non-zero return code. */
 const char* pcfm_last_error(void);
@@ -251,6 +252,32 @@ int pcfm_conv3d_igemm_cl(const void* xs, const void* wsplit, const float* bias, 
  * same workspace query (pcfm_conv3d_wgrad_workspace_bytes). */
 int pcfm_conv3d_wgrad_cl(const void* xs, const void* gys, int b, int cin, int cout, int r,
                          float* grad_w, void* ws, size_t ws_bytes, void* stream);
+
+/* Empty-voxel skipping for PVConv's first convolution (pvconv.py:20-27: its
+ * input is the voxelization, exactly 0 in every voxel no point falls into, and
+ * its input gradient is read back only at occupied voxels, vox.cu:86-110).
+ * pcfm_conv3d_occupancy: from the voxelization's counts cnt i32 [b][r^3]
+ * (> 0 = occupied) writes masks (pcfm_conv3d_occupancy_bytes(b, r); 0 =
+ * unsupported: r^3 % 256 != 0): per 256-voxel tile the taps whose shifted tile
+ * holds an occupied voxel (bits 0-26) and whether the tile holds one (bit 31);
+ * then per 64-voxel chunk the (dx, dy) pairs whose shifted rows hold one. */
+size_t pcfm_conv3d_occupancy_bytes(int b, int r);
+int pcfm_conv3d_occupancy(const int* cnt, int b, int r, unsigned* masks, void* stream);
+/* pcfm_conv3d_igemm_cl skipping exact-zero work: mode 1 (forward over a
+ * voxelized input x: taps that read only empty voxels are skipped, bit-identical
+ * to pcfm_conv3d_igemm_cl), mode 2 (backward-data into a voxelized grid: only
+ * tiles holding an occupied voxel are computed, the others are written 0 --
+ * equal to pcfm_conv3d_igemm_cl at every occupied voxel). */
+int pcfm_conv3d_igemm_cl_occ(const void* xs, const void* wsplit, const float* bias, int b,
+                             int cin, int cout, int r, const unsigned* masks, int mode, float* y,
+                             void* ws, size_t ws_bytes, void* stream);
+/* pcfm_conv3d_wgrad_cl with x a voxelized grid: steps whose X rows are all
+ * empty voxels are skipped (bit-identical to pcfm_conv3d_wgrad_cl); workspace
+ * pcfm_conv3d_wgrad_occ_workspace_bytes (adds the per-split chunk lists). */
+size_t pcfm_conv3d_wgrad_occ_workspace_bytes(int b, int cin, int cout, int r);
+int pcfm_conv3d_wgrad_cl_occ(const void* xs, const void* gys, int b, int cin, int cout, int r,
+                             const unsigned* masks, float* grad_w, void* ws, size_t ws_bytes,
+                             void* stream);
 
 /* Scratch bytes for pcfm_conv3d_wgrad (0 = unsupported shape: cin % 128 is
  * needed in addition to pcfm_conv3d_supported). */

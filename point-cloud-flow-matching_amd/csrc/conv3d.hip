@@ -49,6 +49,52 @@ __global__ void __launch_bounds__(256)
 }
 
 // ---------------------------------------------------------------------------
+// Occupancy of a voxelized grid (PVConv's first convolution reads the
+// voxelization's output, exactly zero in every voxel no point falls into, and
+// its input gradient is read back only at occupied voxels): from the
+// voxelization's counts cnt [b][V] (> 0 = occupied),
+//   tmask [b][V / 256]: bit t < 27 = tap t of the 256-voxel tile's forward
+//     GEMM reads an occupied voxel (v + off(t) in the volume); bit 31 = the
+//     tile holds an occupied voxel;
+//   cmask [b][V / 64]: bit p < 9 = some voxel of the 64-voxel chunk shifted by
+//     (dx, dy, dz), p = 3 (dx + 1) + dy + 1, dz = -1..1, is occupied, i.e. the
+//     weight gradient's (pair, chunk) step has a nonzero X operand.
+// grid = (V / 256, b), 256 threads (a thread = a voxel, a wave = a chunk).
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256)
+    conv3_occupancy_kernel(const int* __restrict__ cnt, int R, uint32_t* __restrict__ tmask,
+                           uint32_t* __restrict__ cmask) {
+  __shared__ uint32_t sm;
+  const int V = R * R * R, R2 = R * R;
+  const int b = blockIdx.y, t = threadIdx.x;
+  const int v = blockIdx.x * 256 + t;
+  const int x = v / R2, y = (v / R) % R, z = v % R;
+  const int* __restrict__ c = cnt + (size_t)b * V;
+  uint32_t taps = 0, pairs = 0;
+#pragma unroll
+  for (int tap = 0; tap < 27; ++tap) {
+    const int dx = tap / 9 - 1, dy = (tap / 3) % 3 - 1, dz = tap % 3 - 1;
+    const int xx = x + dx, yy = y + dy, zz = z + dz;
+    if ((unsigned)xx < (unsigned)R && (unsigned)yy < (unsigned)R && (unsigned)zz < (unsigned)R &&
+        c[xx * R2 + yy * R + zz] > 0) {
+      taps |= 1u << tap;
+      pairs |= 1u << (tap / 3);
+    }
+  }
+  if (c[v] > 0) taps |= 1u << 31;
+  if (t == 0) sm = 0;
+  __syncthreads();
+  // chunk (wave) OR of the pair bits, block OR of the tap bits
+  uint32_t w = pairs;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) w |= __shfl_xor(w, o);
+  if ((t & 63) == 0) cmask[(size_t)b * (V / 64) + v / 64] = w;
+  atomicOr(&sm, taps);
+  __syncthreads();
+  if (t == 0) tmask[(size_t)b * (V / 256) + blockIdx.x] = sm;
+}
+
+// ---------------------------------------------------------------------------
 // Channels-last split of the GEMM's B operand, done once per convolution
 // instead of once per tap: X fp32 [B][C][V] -> hi, lo bf16 [B][V][C].
 // grid = (V / 64, C / 64, B), 256 threads; a 64 x 64 LDS transpose tile.
@@ -376,7 +422,8 @@ __global__ void __launch_bounds__(GN * 2)  // GK<KT, GN>::NW = GN / 32 waves
                             const uint16_t* __restrict__ wh, const uint16_t* __restrict__ wl,
                             const uint16_t* __restrict__ zrow, const float* __restrict__ bias,
                             float* __restrict__ y, int K, int M, int R, int S,
-                            float* __restrict__ part) {
+                            float* __restrict__ part, const uint32_t* __restrict__ tmask,
+                            int mmode) {
   using G = GK<KT, GN>;
   __shared__ __attribute__((aligned(16))) uint8_t lds[NST * G::STAGE];
   const int V = R * R * R, R2 = R * R;
@@ -395,10 +442,31 @@ __global__ void __launch_bounds__(GN * 2)  // GK<KT, GN>::NW = GN / 32 waves
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   const int wr = w / (GN / 64), wc = w % (GN / 64), r = lane & 31, h = lane >> 5;
-  // split-K (small grids, r = 8): this block's K-steps [k0, k1) of 27 * K / KT
-  const int nall = 27 * (K / KT);
+  // Empty-voxel skipping (S == 1; conv3_occupancy_kernel's tile masks):
+  // mmode 1 (forward of a conv over a voxelized grid): only the taps whose
+  // shifted tile holds an occupied voxel -- every other tap's B rows are exact
+  // zeros, so skipping it leaves the accumulators' bits unchanged; mmode 2
+  // (backward-data into a voxelized grid): only tiles that hold an occupied
+  // voxel (the gradient is read back there only); the others are written 0.
+  const uint32_t kAll = 0x7FFFFFFu;
+  uint32_t mask = kAll;
+  if (mmode != 0) {
+    const uint32_t mm = __builtin_amdgcn_readfirstlane(tmask[(size_t)b * (V >> 8) + (v0 >> 8)]);
+    mask = mmode == 1 ? (mm & kAll) : ((mm >> 31) ? kAll : 0u);
+  }
+  const int na = __builtin_popcount(mask);
+  // split-K (small grids, r = 8): this block's K-steps [k0, k1) of na * K / KT
+  const int nall = na * (K / KT);
   const int k0 = (int)((long long)nall * sp / S), k1 = (int)((long long)nall * (sp + 1) / S);
   const int nsteps = k1 - k0;
+  // K-step order: channel chunk major, the active taps of a chunk in tap order.
+  // (ichunk, itap) is the step last issued (iseq); issue() advances one step
+  // at a time in scalar registers (masks apply only with S == 1, so k0 = 0
+  // unless every tap is active)
+  const int first = mask != 0u ? __builtin_ctz(mask) : 0;
+  int iseq = 0;
+  int ichunk = na > 0 ? k0 / na : 0;
+  int itap = mask == kAll ? k0 % 27 : first;
   const size_t bV = (size_t)b * V;
   const int prow = lane / G::CPR, pch = lane % G::CPR;  // this lane's place in a piece
 
@@ -429,8 +497,15 @@ __global__ void __launch_bounds__(GN * 2)  // GK<KT, GN>::NW = GN / 32 waves
   auto issue = [&](int sl, int buf) {
     // channel-chunk-major: the 27 taps of one chunk are consecutive, so the
     // neighbour rows they re-read stay in L2 (tap-major measured slower)
-    const int s = k0 + sl;
-    const int c0 = (s / 27) * KT, tap = s - (s / 27) * 27;
+    {
+      const bool adv = sl != iseq;
+      const uint32_t rest = mask & ~((2u << itap) - 1u);
+      const int nt = rest != 0u ? __builtin_ctz(rest) : first;
+      ichunk += (adv && rest == 0u) ? 1 : 0;
+      itap = adv ? nt : itap;
+      iseq = sl;
+    }
+    const int c0 = ichunk * KT, tap = itap;
     uint8_t* base = lds + buf * G::STAGE;
     const size_t aofs = (size_t)tap * M * K + c0;
 #ifndef PCFM_EXP_CNOA
@@ -469,6 +544,7 @@ __global__ void __launch_bounds__(GN * 2)  // GK<KT, GN>::NW = GN / 32 waves
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
 
+  if (nsteps > 0) {  // an all-skipped tile writes bias (forward) / 0 (backward-data)
 #ifndef PCFM_CONV_GLDS_NOPF
   // Fragment registers double-buffered across steps: after the barrier of
   // step s the waves read step s+1's fragments while step s's 24 MFMAs run,
@@ -611,6 +687,7 @@ __global__ void __launch_bounds__(GN * 2)  // GK<KT, GN>::NW = GN / 32 waves
     }
   }
 #endif
+  }
   float* __restrict__ yb = S == 1 ? y + (size_t)b * M * V : part + ((size_t)sp * nb + b) * M * V;
   float biasv[2][16];
 #pragma unroll
@@ -1047,10 +1124,32 @@ __device__ __forceinline__ bf16x8 mask_k8(bf16x8 v, uint32_t m0, uint32_t m12, u
   return __builtin_bit_cast(bf16x8, u);
 }
 
+// Chunk lists of the masked weight gradient: for each (pair, split sp), the
+// 64-voxel chunks c = sp, sp + S, sp + 2S, ... whose X operand for that pair is
+// nonzero (conv3_occupancy_kernel's cmask), in increasing order -- exactly the
+// chunks the unmasked kernel visits, minus those whose products are all exact
+// zeros.  grid = (9, S), 64 threads; list row stride `cap`.
+__global__ void __launch_bounds__(64)
+    conv3_wgrad_lists_kernel(const uint32_t* __restrict__ cmask, int nchunk, int S, int cap,
+                             int* __restrict__ lists, int* __restrict__ counts) {
+  const int pair = blockIdx.x, sp = blockIdx.y, lane = threadIdx.x;
+  int* __restrict__ out = lists + (size_t)(pair * S + sp) * cap;
+  int n = 0;
+  for (int j0 = 0; sp + (long long)j0 * S < nchunk; j0 += 64) {
+    const long long c = sp + (long long)(j0 + lane) * S;
+    const bool act = c < nchunk && ((cmask[c] >> pair) & 1u);
+    const unsigned long long bal = __ballot(act);
+    if (act) out[n + __popcll(bal & ((1ull << lane) - 1ull))] = (int)c;
+    n += __popcll(bal);
+  }
+  if (lane == 0) counts[pair * S + sp] = n;
+}
+
 __global__ void __launch_bounds__(kW3Threads)
     conv3_wgrad3_kernel(const uint16_t* __restrict__ xh, const uint16_t* __restrict__ xl,
                         const uint16_t* __restrict__ gh, const uint16_t* __restrict__ gl,
-                        int B, int cin, int cout, int R, int S, float* __restrict__ part) {
+                        int B, int cin, int cout, int R, int S, float* __restrict__ part,
+                        const int* __restrict__ lists, const int* __restrict__ counts, int cap) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int V = R * R * R, R2 = R * R;
   const int nco = cout / kMT;
@@ -1065,8 +1164,12 @@ __global__ void __launch_bounds__(kW3Threads)
   id /= S;
   const int co0 = (id % nco) * kMT;
   const int ci0 = (id / nco) * kMT;
-  const long long nsteps = (long long)B * V / kWV;
-  const long long k0 = nsteps * sp / S, k1 = nsteps * (sp + 1) / S;
+  // split sp takes the 64-voxel chunks sp, sp + S, ... (of all B * V / 64), or
+  // with lists those of them whose X operand is nonzero for this pair
+  const int cpb = V / kWV, nchunk = B * cpb;
+  const int* __restrict__ lst = lists != nullptr ? lists + (size_t)(pair * S + sp) * cap : nullptr;
+  const int nst = lists != nullptr ? counts[pair * S + sp]
+                                   : (sp < nchunk ? (nchunk - sp + S - 1) / S : 0);
   const int dx = pair / 3 - 1, dy_ = pair % 3 - 1;
   const int off = dx * R2 + dy_ * R;
 
@@ -1111,20 +1214,20 @@ __global__ void __launch_bounds__(kW3Threads)
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
 
-  // (batch, first voxel) of the current step, advanced incrementally (V % 64 == 0)
-  int cb = (int)(k0 * kWV / V), cv0 = (int)(k0 * kWV - (long long)cb * V);
+  auto chunk_of = [&](int st) { return lst != nullptr ? lst[st] : sp + st * S; };
   const int lgR = 31 - __builtin_clz(R);  // R is a power of two here
-  if (k0 < k1) issue(cb, cv0, lds);
+  int cnext = nst > 0 ? chunk_of(0) : 0;
+  if (nst > 0) issue(cnext / cpb, (cnext % cpb) * kWV, lds);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  const int nst = (int)(k1 - k0);
   for (int st = 0; st < nst; ++st) {
     __builtin_amdgcn_s_barrier();  // step st landed everywhere; step st-1 reads done
     const uint8_t* cur = lds + (st & 1) * kW3Buf;
-    const int v0 = cv0;
-    cv0 += kWV;
-    if (cv0 == V) cv0 = 0, ++cb;
+    const int v0 = (cnext % cpb) * kWV;
 #ifndef PCFM_EXP_WG_NOLOAD
-    if (st + 1 < nst) issue(cb, cv0, lds + ((st + 1) & 1) * kW3Buf);
+    if (st + 1 < nst) {
+      cnext = chunk_of(st + 1);
+      issue(cnext / cpb, (cnext % cpb) * kWV, lds + ((st + 1) & 1) * kW3Buf);
+    }
 #endif
     const uint8_t* iAh = cur;
     const uint8_t* iAl = cur + kW3AImg;
@@ -1445,9 +1548,9 @@ extern "C" size_t pcfm_conv3d_igemm_cl_workspace_bytes(int b, int cin, int cout,
   return S == 1 ? 1 : (size_t)S * b * cout * r * r * r * sizeof(float);
 }
 
-extern "C" int pcfm_conv3d_igemm_cl(const void* xs, const void* wsplit, const float* bias, int b,
-                                    int cin, int cout, int r, float* y, void* ws,
-                                    size_t ws_bytes, void* stream) {
+static int igemm_cl(const void* xs, const void* wsplit, const float* bias, int b, int cin,
+                    int cout, int r, float* y, void* ws, size_t ws_bytes, void* stream,
+                    const uint32_t* tmask, int mmode) {
   PCFM_CHECK_ARG(conv3_shape_ok(b, cin, cout, r),
                  "conv3d_igemm_cl: unsupported shape b=%d cin=%d cout=%d r=%d", b, cin, cout, r);
   if (b == 0) return PCFM_OK;
@@ -1487,16 +1590,21 @@ extern "C" int pcfm_conv3d_igemm_cl(const void* xs, const void* wsplit, const fl
       const long long blocks128 = (long long)(V / 128) * (cout / kGM) * b;
       hipLaunchKernelGGL((conv3_igemm_glds_kernel<32, 128, 2>), dim3((unsigned)blocks128),
                          dim3(256), 0, st, xh, xl, wh, wh + total, zrow, bias, y, cin, cout, r, 1,
-                         part);
+                         part, tmask, mmode);
       return check_launch("conv3d_igemm_cl");
     }
 #endif
+    // tile masks apply to unsplit launches only (a split's K range is a fixed
+    // share of all 27 taps)
+    const int mm = S == 1 && tmask != nullptr ? mmode : 0;
     if (PCFM_CONV_GK == 16 || cin % 32 != 0)
       hipLaunchKernelGGL(conv3_igemm_glds_kernel<16>, dim3((unsigned)glds_blocks), dim3(512), 0,
-                         st, xh, xl, wh, wh + total, zrow, bias, y, cin, cout, r, S, part);
+                         st, xh, xl, wh, wh + total, zrow, bias, y, cin, cout, r, S, part, tmask,
+                         mm);
     else
       hipLaunchKernelGGL(conv3_igemm_glds_kernel<32>, dim3((unsigned)glds_blocks), dim3(512), 0,
-                         st, xh, xl, wh, wh + total, zrow, bias, y, cin, cout, r, S, part);
+                         st, xh, xl, wh, wh + total, zrow, bias, y, cin, cout, r, S, part, tmask,
+                         mm);
     if (S > 1) {
       const long long total4 = (long long)b * cout * V / 4;
       hipLaunchKernelGGL(conv3_ksum_kernel, dim3((unsigned)ceil_div(total4, 256)), dim3(256), 0,
@@ -1526,9 +1634,47 @@ extern "C" int pcfm_conv3d_igemm_cl(const void* xs, const void* wsplit, const fl
   return check_launch("conv3d_igemm_cl");
 }
 
-extern "C" int pcfm_conv3d_wgrad_cl(const void* xs, const void* gys, int b, int cin, int cout,
-                                    int r, float* grad_w, void* ws, size_t ws_bytes,
-                                    void* stream) {
+extern "C" int pcfm_conv3d_igemm_cl(const void* xs, const void* wsplit, const float* bias, int b,
+                                    int cin, int cout, int r, float* y, void* ws,
+                                    size_t ws_bytes, void* stream) {
+  return igemm_cl(xs, wsplit, bias, b, cin, cout, r, y, ws, ws_bytes, stream, nullptr, 0);
+}
+
+extern "C" int pcfm_conv3d_igemm_cl_occ(const void* xs, const void* wsplit, const float* bias,
+                                        int b, int cin, int cout, int r, const unsigned* tmask,
+                                        int mode, float* y, void* ws, size_t ws_bytes,
+                                        void* stream) {
+  PCFM_CHECK_ARG(tmask != nullptr && (mode == 1 || mode == 2) && (r * r * r) % 256 == 0,
+                 "conv3d_igemm_cl_occ: need a tile mask, mode 1 or 2 and r^3 %% 256 == 0 "
+                 "(mode=%d r=%d)", mode, r);
+  return igemm_cl(xs, wsplit, bias, b, cin, cout, r, y, ws, ws_bytes, stream,
+                  (const uint32_t*)tmask, mode);
+}
+
+extern "C" size_t pcfm_conv3d_occupancy_bytes(int b, int r) {
+  const long long v = (long long)r * r * r;
+  if (b <= 0 || r <= 0 || v % 256 != 0) return 0;
+  return (size_t)b * (v / 256 + v / 64) * sizeof(uint32_t);
+}
+
+extern "C" int pcfm_conv3d_occupancy(const int* cnt, int b, int r, unsigned* masks,
+                                     void* stream) {
+  PCFM_CHECK_ARG(pcfm_conv3d_occupancy_bytes(b, r) > 0,
+                 "conv3d_occupancy: bad shape b=%d r=%d (r^3 %% 256 == 0)", b, r);
+  const int V = r * r * r;
+  hipLaunchKernelGGL(conv3_occupancy_kernel, dim3(V / 256, b), dim3(256), 0, (hipStream_t)stream,
+                     cnt, r, (uint32_t*)masks, (uint32_t*)masks + (size_t)b * (V / 256));
+  return check_launch("conv3d_occupancy");
+}
+
+static int wgrad_cap(int b, int r, int S) {
+  const long long nchunk = (long long)b * r * r * r / kWV;
+  return (int)((nchunk + S - 1) / S);
+}
+
+static int wgrad_cl(const void* xs, const void* gys, int b, int cin, int cout, int r,
+                    const uint32_t* cmask, float* grad_w, void* ws, size_t ws_bytes,
+                    void* stream) {
   PCFM_CHECK_ARG(b > 0 && conv3_shape_ok(b, cin, cout, r) && cin % kMT == 0,
                  "conv3d_wgrad_cl: unsupported shape b=%d cin=%d cout=%d r=%d", b, cin, cout, r);
   const size_t need = wgrad_partial_bytes(b, cin, cout, r);
@@ -1542,9 +1688,21 @@ extern "C" int pcfm_conv3d_wgrad_cl(const void* xs, const void* gys, int b, int 
   if (conv3_wgrad3_ok(r)) {
     const int e = allow_big_lds((const void*)conv3_wgrad3_kernel);
     if (e) return e;
+    int* lists = nullptr;
+    int* counts = nullptr;
+    const int cap = wgrad_cap(b, r, S);
+    if (cmask != nullptr) {
+      const size_t lb = (size_t)9 * S * cap * sizeof(int), cb = (size_t)9 * S * sizeof(int);
+      PCFM_CHECK_ARG(ws_bytes >= need + lb + cb,
+                     "conv3d_wgrad_cl_occ: workspace %zu < %zu bytes", ws_bytes, need + lb + cb);
+      lists = (int*)((char*)ws + need);
+      counts = (int*)((char*)ws + need + lb);
+      hipLaunchKernelGGL(conv3_wgrad_lists_kernel, dim3(9, S), dim3(64), 0, st, cmask,
+                         b * (V / kWV), S, cap, lists, counts);
+    }
     hipLaunchKernelGGL(conv3_wgrad3_kernel, dim3(tiles / 3 * S), dim3(kW3Threads), 2 * kW3Buf, st,
                        xh, xh + (size_t)b * V * cin, gh, gh + (size_t)b * V * cout, b, cin, cout, r,
-                       S, (float*)ws);
+                       S, (float*)ws, lists, counts, cap);
   } else {
     hipLaunchKernelGGL(conv3_wgrad_cl_kernel, dim3(tiles * S), dim3(256), 0, st, xh,
                        xh + (size_t)b * V * cin, gh, gh + (size_t)b * V * cout, b, cin, cout, r, S,
@@ -1553,4 +1711,28 @@ extern "C" int pcfm_conv3d_wgrad_cl(const void* xs, const void* gys, int b, int 
   hipLaunchKernelGGL(conv3_wgrad_reduce_kernel, dim3(ceil_div((long long)cout * cin, 64)),
                      dim3(256), 0, st, (const float*)ws, cout, cin, S, grad_w);
   return check_launch("conv3d_wgrad_cl");
+}
+
+extern "C" int pcfm_conv3d_wgrad_cl(const void* xs, const void* gys, int b, int cin, int cout,
+                                    int r, float* grad_w, void* ws, size_t ws_bytes,
+                                    void* stream) {
+  return wgrad_cl(xs, gys, b, cin, cout, r, nullptr, grad_w, ws, ws_bytes, stream);
+}
+
+extern "C" size_t pcfm_conv3d_wgrad_occ_workspace_bytes(int b, int cin, int cout, int r) {
+  if (b <= 0 || !conv3_shape_ok(b, cin, cout, r) || cin % kMT != 0) return 0;
+  const int S = conv3_wgrad_splits(b, cin, cout, r);
+  return wgrad_partial_bytes(b, cin, cout, r) +
+         (size_t)9 * S * (wgrad_cap(b, r, S) + 1) * sizeof(int);
+}
+
+extern "C" int pcfm_conv3d_wgrad_cl_occ(const void* xs, const void* gys, int b, int cin,
+                                        int cout, int r, const unsigned* masks, float* grad_w,
+                                        void* ws, size_t ws_bytes, void* stream) {
+  PCFM_CHECK_ARG(masks != nullptr && (r * r * r) % 256 == 0,
+                 "conv3d_wgrad_cl_occ: need the occupancy masks and r^3 %% 256 == 0 (r=%d)", r);
+  const int V = r * r * r;
+  // the chunk masks follow the tile masks in pcfm_conv3d_occupancy's buffer
+  const uint32_t* cmask = (const uint32_t*)masks + (size_t)b * (V / 256);
+  return wgrad_cl(xs, gys, b, cin, cout, r, cmask, grad_w, ws, ws_bytes, stream);
 }

@@ -119,22 +119,30 @@ class _Conv3dBnActPair(torch.autograd.Function):
     """PVConv's two voxel layers act2(BN2(Conv2(act1(BN1(Conv1(x)))))) in one
     autograd node, so the inner activation lives only as Conv2's channels-last
     split input (bn_act_forward_split) and its gradient only as Conv1's split
-    grad (bn_act_backward_split): no fp32 pass over either."""
+    grad (bn_act_backward_split): no fp32 pass over either.
+
+    `occ` (PVConv, x = the voxelization's grid: pcfm.plans.conv_occupancy)
+    skips Conv1's exact-zero work -- forward taps and weight-gradient steps
+    that read only empty voxels (bit-identical) -- and computes Conv1's input
+    gradient only in voxel tiles that hold an occupied voxel (the voxelization's
+    backward reads it there only, vox.cu:86-110); the returned dx is 0 in the
+    other tiles."""
 
     @staticmethod
     def forward(ctx, x, w1, b1, g1, bt1, rm1, rv1, nbt1, w2, b2, g2, bt2, rm2, rv2, nbt2, eps1,
-                mom1, slope1, eps2, mom2, slope2):
+                mom1, slope1, eps2, mom2, slope2, occ=None):
         from pcfm import ops
         bsz, cin, r = x.shape[0], x.shape[1], x.shape[2]
         cmid, cout = w1.shape[0], w2.shape[0]
         xs = ops.conv3d_split(x)
         y1 = ops.conv3d_igemm_split(xs, ops.conv3d_prep_weight(w1, False), b1, bsz, cin, cmid,
-                                    r, "conv3d_fwd")
+                                    r, "conv3d_fwd", occ=occ, occ_mode=1)
         z1s, m1, is1 = ops.bn_act_forward_split(y1, g1, bt1, eps1, slope1, mom1, rm1, rv1, nbt1)
         y2 = ops.conv3d_igemm_split(z1s, ops.conv3d_prep_weight(w2, False), b2, bsz, cmid, cout,
                                     r, "conv3d_fwd")
         z2, m2, is2 = ops.bn_act_forward(y2, g2, bt2, eps2, slope2, mom2, rm2, rv2, nbt2)
         ctx.save_for_backward(xs, w1, y1, g1, bt1, m1, is1, z1s, w2, y2, g2, bt2, m2, is2)
+        ctx.occ = occ
         ctx.slopes = (slope1, slope2)
         ctx.has_bias = (b1 is not None, b2 is not None)
         ctx.dims = (bsz, cin, cmid, cout, r)
@@ -157,19 +165,21 @@ class _Conv3dBnActPair(torch.autograd.Function):
                                                          want_dbias_in=ctx.has_bias[0])
         del dz1
         dx = None
+        occ = ctx.occ
         if ctx.needs_input_grad[0]:
             dx = ops.conv3d_igemm_split(gys1, ops.conv3d_prep_weight(w1, True), None, bsz, cmid,
-                                        cin, r, "conv3d_bwd_data")
-        dw1 = ops.conv3d_wgrad_split(xs, gys1, bsz, cin, cmid, r)
+                                        cin, r, "conv3d_bwd_data", occ=occ, occ_mode=2)
+        dw1 = ops.conv3d_wgrad_split(xs, gys1, bsz, cin, cmid, r, occ=occ)
         return (dx, dw1, db1, dg1, dbt1, None, None, None, dw2, db2, dg2, dbt2, None, None,
-                None, None, None, None, None, None, None)
+                None, None, None, None, None, None, None, None)
 
 
 def conv_bn_act_pair(conv1, bn1, slope1: float, conv2, bn2, slope2: float,
-                     x: torch.Tensor) -> torch.Tensor:
+                     x: torch.Tensor, occ=None) -> torch.Tensor:
     """act2(bn2(conv2(act1(bn1(conv1(x)))))) for two VoxelConv3d layers: one
     autograd node on the GPU path when both layers qualify, else two
-    conv_bn_act calls."""
+    conv_bn_act calls.  `occ`: occupancy masks when x is a voxelized grid
+    (_Conv3dBnActPair)."""
     from modules.shared_mlp import PointwiseConv1d
     ok = (not isinstance(conv1, PointwiseConv1d) and not isinstance(conv2, PointwiseConv1d)
           and _fusable_pre(bn1) and _fusable_pre(bn2) and hasattr(conv1, "x3_ok")
@@ -189,7 +199,7 @@ def conv_bn_act_pair(conv1, bn1, slope1: float, conv2, bn2, slope2: float,
         x.contiguous(), conv1.weight, conv1.bias, bn1.weight, bn1.bias, bn1.running_mean,
         bn1.running_var, _nbt(bn1), conv2.weight, conv2.bias, bn2.weight, bn2.bias,
         bn2.running_mean, bn2.running_var, _nbt(bn2), float(bn1.eps), float(bn1.momentum),
-        float(slope1), float(bn2.eps), float(bn2.momentum), float(slope2))
+        float(slope1), float(bn2.eps), float(bn2.momentum), float(slope2), occ)
 
 
 def conv_bn_act(conv, bn, x: torch.Tensor, slope: float) -> torch.Tensor:

@@ -123,8 +123,14 @@ class PVConv(nn.Module):
         else:
             grid, grid_coords = self.voxelization(features, coords)
         layers = self.voxel_layers  # Conv3d, BN3d, LeakyReLU, Conv3d, BN3d, LeakyReLU[, SE3d]
+        occ = None
+        if grid.is_cuda:
+            # the first conv's input is the voxelization: exact zeros off the
+            # occupied voxels, and its gradient is read back only on them
+            from pcfm import plans
+            occ = plans.conv_occupancy(self.voxelization._coords(coords)[1], self.resolution)
         grid = conv_bn_act_pair(layers[0], layers[1], layers[2].negative_slope,
-                                layers[3], layers[4], layers[5].negative_slope, grid)
+                                layers[3], layers[4], layers[5].negative_slope, grid, occ=occ)
         pf = self.point_features(features)
         if (len(layers) > 6 and _se_devox_ok(layers[6], grid, pf)
                 and (self.training or not torch.is_grad_enabled())):

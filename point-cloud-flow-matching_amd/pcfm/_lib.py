@@ -58,6 +58,11 @@ SIGNATURES = {
     "pcfm_conv3d_igemm_cl_workspace_bytes": (_Z, [_I, _I, _I, _I]),
     "pcfm_conv3d_igemm_cl": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P, _Z, _P]),
     "pcfm_conv3d_wgrad_cl": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, _Z, _P]),
+    "pcfm_conv3d_occupancy_bytes": (_Z, [_I, _I]),
+    "pcfm_conv3d_occupancy": (_I, [_P, _I, _I, _P, _P]),
+    "pcfm_conv3d_igemm_cl_occ": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _I, _P, _P, _Z, _P]),
+    "pcfm_conv3d_wgrad_occ_workspace_bytes": (_Z, [_I, _I, _I, _I]),
+    "pcfm_conv3d_wgrad_cl_occ": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, _P, _Z, _P]),
     "pcfm_conv3d_wgrad_workspace_bytes": (_Z, [_I, _I, _I, _I]),
     "pcfm_conv3d_wgrad": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, _Z, _P]),
     "pcfm_pointwise_weight_bytes": (_Z, [_I, _I]),
@@ -116,7 +121,7 @@ SIGNATURES = {
     "pcfm_adamw_ema_step": (_I, [_P, _P, _I, _P, _P, _I, _DP, _DP, _D, _D, _D, _D, _P]),
 }
 
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 _lock = threading.Lock()
 _lib = None

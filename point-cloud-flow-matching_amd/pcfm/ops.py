@@ -686,27 +686,53 @@ def conv3d_split_supported(x: torch.Tensor) -> bool:
     return _lib.query("pcfm_conv3d_split_bytes", x.shape[0], x.shape[1], x.shape[2]) > 0
 
 
+def conv3d_occupancy(cnt: torch.Tensor, r: int):
+    """Occupancy masks of a voxelized grid from the voxelization's counts cnt
+    (b, r^3) int32 (pcfm_conv3d_occupancy), or None where r^3 % 256 != 0."""
+    _check(cnt, "cnt", "i")
+    b = cnt.shape[0]
+    n = _lib.query("pcfm_conv3d_occupancy_bytes", b, int(r))
+    if n == 0:
+        return None
+    masks = torch.empty(n // 4, dtype=torch.int32, device=cnt.device)
+    _lib.call("pcfm_conv3d_occupancy", _ptr(cnt), b, int(r), _ptr(masks), _stream(cnt))
+    return masks
+
+
 def conv3d_igemm_split(xs: torch.Tensor, img: torch.Tensor, bias, b: int, cin: int, cout: int,
-                       r: int, op: str) -> torch.Tensor:
+                       r: int, op: str, occ=None, occ_mode: int = 0) -> torch.Tensor:
     """y (b, cout, r, r, r) from a split input (forward, or backward-data with the
-    transposed weight image)."""
+    transposed weight image).  occ (conv3d_occupancy of the voxelized input /
+    gradient target) with occ_mode 1 (forward) / 2 (backward-data) skips the
+    exact-zero / unread work (pcfm_conv3d_igemm_cl_occ)."""
     y = torch.empty((b, cout, r, r, r), dtype=torch.float32, device=xs.device)
     bias_p = _ptr(bias.contiguous()) if bias is not None else None
     ws = _workspace(_lib.query("pcfm_conv3d_igemm_cl_workspace_bytes", b, cin, cout, r), xs)
     with _timed(op, 54 * b * r ** 3 * cin * cout, xs, "mfma"):
-        _lib.call("pcfm_conv3d_igemm_cl", _ptr(xs), _ptr(img), bias_p, b, cin, cout, r, _ptr(y),
-                  _ptr(ws), ws.numel(), _stream(xs))
+        if occ is not None and occ_mode:
+            _lib.call("pcfm_conv3d_igemm_cl_occ", _ptr(xs), _ptr(img), bias_p, b, cin, cout, r,
+                      _ptr(occ), int(occ_mode), _ptr(y), _ptr(ws), ws.numel(), _stream(xs))
+        else:
+            _lib.call("pcfm_conv3d_igemm_cl", _ptr(xs), _ptr(img), bias_p, b, cin, cout, r,
+                      _ptr(y), _ptr(ws), ws.numel(), _stream(xs))
     return y
 
 
 def conv3d_wgrad_split(xs: torch.Tensor, gys: torch.Tensor, b: int, cin: int, cout: int,
-                       r: int) -> torch.Tensor:
-    """dW (cout, cin, 3, 3, 3) from split(x) and split(grad_y)."""
-    ws = _workspace(_lib.query("pcfm_conv3d_wgrad_workspace_bytes", b, cin, cout, r), xs)
+                       r: int, occ=None) -> torch.Tensor:
+    """dW (cout, cin, 3, 3, 3) from split(x) and split(grad_y); occ (the
+    occupancy masks of a voxelized x) skips the steps whose X rows are empty."""
+    q = "pcfm_conv3d_wgrad_occ_workspace_bytes" if occ is not None else \
+        "pcfm_conv3d_wgrad_workspace_bytes"
+    ws = _workspace(_lib.query(q, b, cin, cout, r), xs)
     dw = torch.empty((cout, cin, 3, 3, 3), dtype=torch.float32, device=xs.device)
     with _timed("conv3d_wgrad", 54 * b * r ** 3 * cin * cout, xs, "mfma"):
-        _lib.call("pcfm_conv3d_wgrad_cl", _ptr(xs), _ptr(gys), b, cin, cout, r, _ptr(dw),
-                  _ptr(ws), ws.numel(), _stream(xs))
+        if occ is not None:
+            _lib.call("pcfm_conv3d_wgrad_cl_occ", _ptr(xs), _ptr(gys), b, cin, cout, r, _ptr(occ),
+                      _ptr(dw), _ptr(ws), ws.numel(), _stream(xs))
+        else:
+            _lib.call("pcfm_conv3d_wgrad_cl", _ptr(xs), _ptr(gys), b, cin, cout, r, _ptr(dw),
+                      _ptr(ws), ws.numel(), _stream(xs))
     return dw
 
 

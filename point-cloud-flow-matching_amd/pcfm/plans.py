@@ -8,7 +8,9 @@ the coordinates is computed once per stage instead of once per block:
   * the voxelization plan (stable sort of the points by voxel, work units;
     also the backward's ind / cnt),
   * the devoxelization's corner indices / weights (inds, wgts) and
-  * the devoxelization-backward plan (sort by base cell, sorted tap weights).
+  * the devoxelization-backward plan (sort by base cell, sorted tap weights),
+  * the occupancy masks of the voxelized grid (which voxel tiles / taps of
+    PVConv's first convolution touch an occupied voxel).
 Entries are keyed on the identity of the tensor they derive from (plus its
 version counter) and die with it (weakref), so nothing outlives the step.
 Results are bit-identical to recomputing (same kernels, same inputs).
@@ -22,6 +24,8 @@ import weakref
 import torch
 
 ENABLED = os.environ.get("PCFM_SHARE_PLANS", "1") != "0"
+# occupancy-masked first voxel convolution of PVConv (measurement switch)
+OCCUPANCY = os.environ.get("PCFM_CONV_OCC", "1") != "0"
 
 
 class IdentityCache:
@@ -82,6 +86,21 @@ def voxel_plan(vox_coords: torch.Tensor, r: int):
     if hit is not None:
         return hit
     return _cache.put(vox_coords, tag, ops.avg_voxelize_plan(vox_coords, r))
+
+
+def conv_occupancy(vox_coords: torch.Tensor, r: int):
+    """ops.conv3d_occupancy of the voxelization plan's counts (shared per
+    points), or None when off or unsupported (r^3 % 256 != 0)."""
+    from pcfm import ops
+    if not (OCCUPANCY and _on(vox_coords)):
+        return None
+    tag = ("occ", int(r))
+    hit = _cache.get(vox_coords, tag)
+    if hit is not None:
+        return hit[0]
+    occ = ops.conv3d_occupancy(voxel_plan(vox_coords, r).cnt, r)
+    _cache.put(vox_coords, tag, (occ,))
+    return occ
 
 
 def devox_corners(norm_coords: torch.Tensor, r: int):

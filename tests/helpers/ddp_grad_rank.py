@@ -70,8 +70,11 @@ def main():
         per.append(grads(ref))
     torch.cuda.synchronize(dev)
 
-    max_rel, bit_equal, n_grads = 0.0, 0, 0
-    for gd, g0, g1 in zip(g_ddp, per[0], per[1]):
+    names = ([f"enc.{n}" for n, _ in tr.enc.named_parameters()]
+             + [f"pf.{n}" for n, _ in tr.pf.named_parameters()]
+             + [f"lf.{n}" for n, _ in tr.lf.named_parameters()])
+    max_rel, bit_equal, n_grads, differ = 0.0, 0, 0, {}
+    for name, gd, g0, g1 in zip(names, g_ddp, per[0], per[1]):
         if gd is None:
             assert g0 is None and g1 is None
             continue
@@ -79,8 +82,11 @@ def main():
         want = (g0 + g1) / world
         scale = want.abs().max().item()
         err = (gd - want).abs().max().item()
-        max_rel = max(max_rel, err / scale if scale > 0 else err)
+        rel = err / scale if scale > 0 else err
+        max_rel = max(max_rel, rel)
         bit_equal += int(torch.equal(gd, want))
+        if not torch.equal(gd, want):
+            differ[name] = rel
     sums = torch.tensor([g.double().sum().item() for g in g_ddp if g is not None],
                         dtype=torch.float64)
     gathered = [torch.zeros_like(sums) for _ in range(world)]
@@ -88,7 +94,7 @@ def main():
     res = {"rank": rank, "world": world, "backend": dist.get_backend(),
            "losses": [float(out["loss_point"]), float(out["loss_latent"])],
            "ref_losses": ref_losses, "max_rel": max_rel, "bit_equal": bit_equal,
-           "n_grads": n_grads, "grad_sums_equal_across_ranks":
+           "n_grads": n_grads, "differ": differ, "grad_sums_equal_across_ranks":
            all(torch.equal(gathered[0], g) for g in gathered)}
     with open(f"{sys.argv[1]}.{rank}", "w") as f:
         json.dump(res, f)

@@ -167,3 +167,92 @@ def test_stage_blocks_share_plans(ops, monkeypatch):
     assert torch.equal(o1, o0)
     for a, b in zip(g1, g0):
         assert torch.equal(a, b)
+
+
+def _voxelized(ops, b, c, r, n, seed, surface=False):
+    """A voxelized grid of random features over a randn (or spherical-shell)
+    cloud, its counts, and the occupancy masks."""
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    pts = torch.randn(b, 3, n, device="cuda", generator=g)
+    if surface:
+        pts = pts / pts.norm(dim=1, keepdim=True)
+    c0 = pts - pts.mean(2, keepdim=True)
+    unit = c0 / (2 * c0.norm(dim=1, keepdim=True).max(2, keepdim=True).values + 1e-6) + 0.5
+    vox = torch.round(torch.clamp(unit * r, 0, r - 1)).int().contiguous()
+    feats = torch.randn(b, c, n, device="cuda", generator=g)
+    grid, _, cnt = ops.avg_voxelize_forward(feats, vox, r)
+    occ = ops.conv3d_occupancy(cnt, r)
+    return grid.view(b, c, r, r, r), cnt, occ
+
+
+@pytest.mark.parametrize("cin,cout,r,surface", [(128, 128, 32, False), (128, 256, 16, False),
+                                                (64, 128, 32, True)])
+def test_conv_occupancy_skipping_is_exact(ops, cin, cout, r, surface, report):
+    """PVConv's first conv over a voxelized grid with the occupancy masks:
+    forward and weight gradient bit-identical to the unmasked kernels; the
+    backward-data equal at every occupied voxel (0 in tiles without one)."""
+    b = 4
+    grid, cnt, occ = _voxelized(ops, b, cin, r, 6000, r + cin, surface)
+    assert occ is not None
+    xs = ops.conv3d_split(grid.contiguous())
+    g = torch.Generator(device="cuda").manual_seed(5)
+    w = torch.randn(cout, cin, 3, 3, 3, device="cuda", generator=g) * 0.05
+    bias = torch.randn(cout, device="cuda", generator=g)
+    img = ops.conv3d_prep_weight(w, False)
+    y0 = ops.conv3d_igemm_split(xs, img, bias, b, cin, cout, r, "conv3d_fwd")
+    y1 = ops.conv3d_igemm_split(xs, img, bias, b, cin, cout, r, "conv3d_fwd", occ=occ,
+                                occ_mode=1)
+    assert torch.equal(y0, y1)
+    dy = torch.randn(b, cout, r, r, r, device="cuda", generator=g)
+    gys = ops.conv3d_split(dy)
+    imgt = ops.conv3d_prep_weight(w, True)
+    dx0 = ops.conv3d_igemm_split(gys, imgt, None, b, cout, cin, r, "conv3d_bwd_data")
+    dx1 = ops.conv3d_igemm_split(gys, imgt, None, b, cout, cin, r, "conv3d_bwd_data", occ=occ,
+                                 occ_mode=2)
+    occupied = (cnt.view(b, 1, -1) > 0).expand(b, cin, r ** 3)
+    assert torch.equal(dx0.view(b, cin, -1)[occupied], dx1.view(b, cin, -1)[occupied])
+    tiles = (cnt.view(b, -1, 256) > 0).any(-1)                     # (b, tiles)
+    empty = (~tiles)[:, None, :, None].expand(b, cin, tiles.shape[1], 256)
+    assert float(dx1.view(b, cin, -1, 256)[empty].abs().max() if empty.any() else 0.0) == 0.0
+    dw0 = ops.conv3d_wgrad_split(xs, gys, b, cin, cout, r)
+    dw1 = ops.conv3d_wgrad_split(xs, gys, b, cin, cout, r, occ=occ)
+    assert torch.equal(dw0, dw1)
+    # fp64 reference of the weight gradient (the new strided step order)
+    ref = torch.nn.grad.conv3d_weight(grid.double(), w.shape, dy.double(), padding=1)
+    err = ((dw1.double() - ref).abs().max() / ref.pow(2).mean().sqrt()).item()
+    assert err < 1e-4
+    m = occ[: b * (r ** 3 // 256)]
+    active = sum(bin(int(v) & 0x7FFFFFF).count("1") for v in m.tolist()) / (27.0 * m.numel())
+    report(f"conv_occupancy_c{cin}_r{r}{'_surface' if surface else ''}",
+           {"fwd_active_tap_fraction": active,
+            "bwd_active_tile_fraction": float(tiles.float().mean()), "wgrad_rel_err": err})
+
+
+def test_pvconv_occupancy_end_to_end(ops, monkeypatch):
+    """A PVConv layer's output and every gradient are bit-identical with the
+    occupancy skipping on and off (pcfm.plans.OCCUPANCY)."""
+    import modules.pvconv as pv
+    from pcfm import plans
+    torch.manual_seed(0)
+    mod = pv.PVConv(128, 128, 3, 32, with_se=True, normalize=True).cuda().train()
+    feats = torch.randn(2, 128, 8000, device="cuda")
+    coords = torch.randn(2, 3, 8000, device="cuda")
+    state = {k: v.clone() for k, v in mod.state_dict().items()}
+
+    def run():
+        mod.load_state_dict(state)
+        f = feats.clone().requires_grad_(True)
+        out, _ = mod((f, coords.clone()))
+        out.backward(torch.randn(out.shape, device="cuda",
+                                 generator=torch.Generator(device="cuda").manual_seed(1)))
+        grads = [f.grad] + [p.grad.clone() for p in mod.parameters()]
+        mod.zero_grad(set_to_none=True)
+        return out.detach(), grads
+
+    monkeypatch.setattr(plans, "OCCUPANCY", True)
+    o1, g1 = run()
+    monkeypatch.setattr(plans, "OCCUPANCY", False)
+    o0, g0 = run()
+    assert torch.equal(o0, o1)
+    for a, b_ in zip(g0, g1):
+        assert torch.equal(a, b_)
