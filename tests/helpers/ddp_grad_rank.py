@@ -68,6 +68,12 @@ def main():
         o = ref.forward_backward(bs, EPOCH, ds)
         ref_losses.append([float(o["loss_point"]), float(o["loss_latent"])])
         per.append(grads(ref))
+    # the reference once more on shard `rank`: names of gradients that are not
+    # reproducible inside one process (diagnostic)
+    ref.opt.zero_grad(set_to_none=True)
+    bs, ds = shard(cfg, rank, dev)
+    ref.forward_backward(bs, EPOCH, ds)
+    again = grads(ref)
     torch.cuda.synchronize(dev)
 
     names = ([f"enc.{n}" for n, _ in tr.enc.named_parameters()]
@@ -87,6 +93,8 @@ def main():
         bit_equal += int(torch.equal(gd, want))
         if not torch.equal(gd, want):
             differ[name] = rel
+    unrepro = [nm for nm, a, b_ in zip(names, per[rank], again)
+               if a is not None and not torch.equal(a, b_)]
     sums = torch.tensor([g.double().sum().item() for g in g_ddp if g is not None],
                         dtype=torch.float64)
     gathered = [torch.zeros_like(sums) for _ in range(world)]
@@ -94,7 +102,7 @@ def main():
     res = {"rank": rank, "world": world, "backend": dist.get_backend(),
            "losses": [float(out["loss_point"]), float(out["loss_latent"])],
            "ref_losses": ref_losses, "max_rel": max_rel, "bit_equal": bit_equal,
-           "n_grads": n_grads, "differ": differ, "grad_sums_equal_across_ranks":
+           "n_grads": n_grads, "differ": differ, "unreproducible": unrepro, "grad_sums_equal_across_ranks":
            all(torch.equal(gathered[0], g) for g in gathered)}
     with open(f"{sys.argv[1]}.{rank}", "w") as f:
         json.dump(res, f)
