@@ -44,8 +44,9 @@ def main():
     x = torch.randn(b, n, 6, device=dev, generator=g)
     t = torch.rand(b, device=dev, generator=g)
     cond = torch.randn(b, cfg.latent_dim + cfg.cond_dim, device=dev, generator=g)
-    res = [run(tr, x, t, cond, None) for _ in range(3)]
-    for k in (1, 2):
+    runs = int(os.environ.get("RUNS", "3"))
+    res = [run(tr, x, t, cond, None) for _ in range(runs)]
+    for k in range(1, runs):
         diff = [name for (name, a), (_, c) in zip(res[0][1], res[k][1])
                 if a.shape != c.shape or not torch.equal(a, c)]
         print(json.dumps({"run": k, "v_equal": bool(torch.equal(res[0][0], res[k][0])),
