@@ -28,10 +28,11 @@
 namespace pcfm {
 namespace {
 
-// W [Cout][Cin][27] fp32 -> W' [27][M][K] bf16 hi, lo (see header)
+// W [Cout][Cin][27] fp32 -> W' [27][M][K] bf16 hi, lo (see header), rows of K
+// interleaved per 32-channel group (split_off)
 __global__ void __launch_bounds__(256)
     conv3_wsplit_kernel(const float* __restrict__ w, int cout, int cin, int transpose,
-                        uint16_t* __restrict__ wh, uint16_t* __restrict__ wl) {
+                        uint16_t* __restrict__ wh) {
   const size_t total = (size_t)27 * cout * cin;
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= total) return;
@@ -44,8 +45,9 @@ __global__ void __launch_bounds__(256)
                             : w[((size_t)m * cin + k) * 27 + tap];
   uint32_t hi, lo;
   split_bf16(v, hi, lo);
-  wh[i] = (uint16_t)hi;
-  wl[i] = (uint16_t)lo;
+  const size_t o = split_off((size_t)tap * M + m, k, K);  // interleaved image (pcfm_common.hpp)
+  wh[o] = (uint16_t)hi;
+  wh[o + kSplitLo] = (uint16_t)lo;
 }
 
 // ---------------------------------------------------------------------------
@@ -96,12 +98,12 @@ __global__ void __launch_bounds__(256)
 
 // ---------------------------------------------------------------------------
 // Channels-last split of the GEMM's B operand, done once per convolution
-// instead of once per tap: X fp32 [B][C][V] -> hi, lo bf16 [B][V][C].
+// instead of once per tap: X fp32 [B][C][V] -> hi, lo bf16 [B][V][C], rows
+// interleaved per 32-channel group (split_off).
 // grid = (V / 64, C / 64, B), 256 threads; a 64 x 64 LDS transpose tile.
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(256)
-    conv3_split_cl_kernel(const float* __restrict__ x, int C, int V, uint16_t* __restrict__ xh,
-                          uint16_t* __restrict__ xl) {
+    conv3_split_cl_kernel(const float* __restrict__ x, int C, int V, uint16_t* __restrict__ xh) {
   __shared__ float tile[64][65];
   const int v0 = blockIdx.x * 64, c0 = blockIdx.y * 64, b = blockIdx.z;
   const int t = threadIdx.x;
@@ -116,8 +118,8 @@ __global__ void __launch_bounds__(256)
   float f[16];
 #pragma unroll
   for (int q = 0; q < 16; ++q) f[q] = tile[cg + q][v];
-  const size_t o = ((size_t)b * V + v0 + v) * C + c0 + cg;
-  store_split<16>(f, xh + o, xl + o);
+  const size_t o = split_off((size_t)b * V + v0 + v, c0 + cg, C);
+  store_split<16>(f, xh + o, xh + o + kSplitLo);
 }
 
 // ---------------------------------------------------------------------------
@@ -209,8 +211,8 @@ __global__ void __launch_bounds__(256)
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   const int wr = w >> 1, wc = w & 1, r = lane & 31, h = lane >> 5;
-  const uint16_t* __restrict__ xbh = xh + (size_t)b * V * K;
-  const uint16_t* __restrict__ xbl = xl + (size_t)b * V * K;
+  const uint16_t* __restrict__ xbh = xh + (size_t)b * V * 2 * K;
+  const uint16_t* __restrict__ xbl = xl + (size_t)b * V * 2 * K;
   const int nck = K / KT, nall = 27 * nck;
   const int s0 = (int)((long long)nall * sp / S), nsteps = (int)((long long)nall * (sp + 1) / S) - s0;
   // chunk q of this thread: row (t + 256 q) / CPR, 8-channel column (t % CPR) * 8
@@ -231,7 +233,7 @@ __global__ void __launch_bounds__(256)
 #pragma unroll
     for (int q = 0; q < T::QA; ++q) {
       const int row = (t + 256 * q) / T::CPR;
-      const size_t g = ((size_t)tap * M + m0 + row) * K + c0 + col;
+      const size_t g = split_off((size_t)tap * M + m0 + row, c0 + col, K);
       sv_put<T::QA>(rah, q, *reinterpret_cast<const uint4*>(wh + g));
       sv_put<T::QA>(ral, q, *reinterpret_cast<const uint4*>(wl + g));
     }
@@ -241,7 +243,7 @@ __global__ void __launch_bounds__(256)
     for (int q = 0; q < T::QB; ++q) {
       const bool inb = (unsigned)(bx[q] + dx) < (unsigned)R &&
                        (unsigned)(by[q] + dy) < (unsigned)R && (unsigned)(bz[q] + dz) < (unsigned)R;
-      const size_t o = (size_t)(inb ? bv[q] + doff : bv[q]) * K + c0 + col;
+      const size_t o = split_off((size_t)(inb ? bv[q] + doff : bv[q]), c0 + col, K);
       const uint4 hv = *reinterpret_cast<const uint4*>(xbh + o);
       const uint4 lv = *reinterpret_cast<const uint4*>(xbl + o);
       sv_put<T::QB>(rbh, q, inb ? hv : uint4{0u, 0u, 0u, 0u});
@@ -477,7 +479,7 @@ __global__ void __launch_bounds__(GN * 2)  // GK<KT, GN>::NW = GN / 32 waves
   for (int q = 0; q < G::APW; ++q) {
     const int I = G::APW * w + q;
     const int row = (I % G::API) * G::RPP + prow;
-    abase[q] = ((I / G::API) ? wl : wh) + (size_t)(m0 + row) * K + ((pch ^ G::swz(row)) << 3);
+    abase[q] = ((I / G::API) ? wl : wh) + (size_t)(m0 + row) * 2 * K + ((pch ^ G::swz(row)) << 3);
   }
   // B pieces: I = BPW w + q -> image I / BPI (waves 0-3: hi, 4-7: lo)
   const uint16_t* bbase[G::BPW];
@@ -489,7 +491,7 @@ __global__ void __launch_bounds__(GN * 2)  // GK<KT, GN>::NW = GN / 32 waves
     const int row = (I % G::BPI) * G::RPP + prow;
     const int v = v0 + row;
     const int cofs = (pch ^ G::swz(row)) << 3;
-    bbase[q] = ((I / G::BPI) ? xl : xh) + (bV + v) * K + cofs;
+    bbase[q] = ((I / G::BPI) ? xl : xh) + (bV + v) * 2 * K + cofs;
     zbase[q] = zrow + cofs;
     bxyz[q] = (v / R2) | (((v / R) % R) << 10) | ((v % R) << 20);
   }
@@ -506,8 +508,11 @@ __global__ void __launch_bounds__(GN * 2)  // GK<KT, GN>::NW = GN / 32 waves
       iseq = sl;
     }
     const int c0 = ichunk * KT, tap = itap;
+    // the chunk's place in an interleaved row (split_off; a KT-chunk never
+    // straddles a 32-channel group)
+    const int cof = ((c0 >> 5) << 6) + (c0 & 31);
     uint8_t* base = lds + buf * G::STAGE;
-    const size_t aofs = (size_t)tap * M * K + c0;
+    const size_t aofs = (size_t)tap * M * 2 * K + cof;
 #ifndef PCFM_EXP_CNOA
 #pragma unroll
     for (int q = 0; q < G::APW; ++q) {
@@ -516,7 +521,7 @@ __global__ void __launch_bounds__(GN * 2)  // GK<KT, GN>::NW = GN / 32 waves
     }
 #endif
     const int dx = tap / 9 - 1, dy = (tap / 3) % 3 - 1, dz = tap % 3 - 1;
-    const long long bofs = (long long)(dx * R2 + dy * R + dz) * K + c0;
+    const long long bofs = (long long)(dx * R2 + dy * R + dz) * 2 * K + cof;
 #ifdef PCFM_EXP_CNOB
     if (aofs == (size_t)-1)
 #endif
@@ -708,18 +713,6 @@ __global__ void __launch_bounds__(GN * 2)  // GK<KT, GN>::NW = GN / 32 waves
       }
 }
 
-// ---------------------------------------------------------------------------
-// Forward / backward-data, THREE taps per step: the dz = -1, 0, +1 taps of one
-// (dx, dy) read X rows shifted by one voxel, so a step stages the 256-voxel
-// tile's X rows once with a one-row halo each side (258 rows, K = 16 channels)
-// plus the three taps' weight slices, and every wave reads its B operand at row
-// offset 1 + dz.  X traffic per output drops 3x against conv3_igemm_glds_kernel
-// (which is L2-bandwidth bound at these shapes).  32-B LDS rows, 16-B halves
-// swapped on odd 8-row blocks (conflict-free ds_read_b128 of both operands),
-// applied on the source side of the lane-linear LDS-DMA; out-of-volume
-// neighbours are zeroed in registers.  3 stages, counted vmcnt, raw barrier,
-// inline-asm LDS-DMA (hipcc adds no waits for it).
-// ---------------------------------------------------------------------------
 // LDS-DMA as inline asm: hipcc does not see it, so it inserts no vmcnt(0)
 // before the step's LDS reads (it does for __builtin_amdgcn_global_load_lds
 // here, which serialises the prefetch with the compute); completion is waited
@@ -735,190 +728,6 @@ __device__ __forceinline__ void glds16_asm(const void* g, uint32_t lds) {
       : "=&s"(keep)
       : "v"(g), "s"(lds)
       : "memory");
-}
-
-constexpr int kHM = 128, kHN = 256, kHK = 16, kHStages = 3;
-constexpr int kHRow = kHK * 2;                    // bytes per LDS row (hi or lo)
-constexpr int kHAImg = kHM * kHRow;               // 4 KiB: one tap's weight slice
-constexpr int kHBRows = 288;                      // 258 rows used, 32-row pieces
-constexpr int kHBImg = kHBRows * kHRow;           // 9 KiB
-constexpr int kHStage = 6 * kHAImg + 2 * kHBImg;  // 42 KiB
-constexpr int kHAPieces = kHAImg / 1024, kHBPieces = kHBImg / 1024;
-constexpr int kHPieces = 6 * kHAPieces + 2 * kHBPieces;  // 42
-constexpr int kHQ = (kHPieces + 7) / 8;                    // pieces per wave (<=)
-constexpr int kHQmin = kHPieces / 8;                       // pieces per wave (>=)
-
-__device__ __forceinline__ int hswz(int row) { return (row >> 3) & 1; }
-
-__device__ __forceinline__ bf16x8 zero_unless(bool ok, bf16x8 v) {
-  uint4 u = __builtin_bit_cast(uint4, v);
-  u.x = ok ? u.x : 0u;
-  u.y = ok ? u.y : 0u;
-  u.z = ok ? u.z : 0u;
-  u.w = ok ? u.w : 0u;
-  return __builtin_bit_cast(bf16x8, u);
-}
-
-__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2)))
-    conv3_igemm_glds3_kernel(const uint16_t* __restrict__ xh, const uint16_t* __restrict__ xl,
-                             const uint16_t* __restrict__ wh, const uint16_t* __restrict__ wl,
-                             const float* __restrict__ bias, float* __restrict__ y, int K, int M,
-                             int R) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[kHStages * kHStage];
-  const int V = R * R * R, R2 = R * R;
-  int id = (int)blockIdx.x;
-  {
-    const int nwg = (int)gridDim.x, q = nwg / 8, rr = nwg % 8, xcd = id % 8;
-    id = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + id / 8;
-  }
-  const int nmt = M / kHM, nvt = V / kHN;
-  const int m0 = (id % nmt) * kHM;
-  id /= nmt;
-  const int v0 = (id % nvt) * kHN, b = id / nvt;
-  const int t = threadIdx.x, lane = t & 63;
-  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int wr = w >> 2, wc = w & 3, r = lane & 31, h = lane >> 5;
-  const int nsteps = 9 * (K / kHK);
-  const size_t bV = (size_t)b * V;
-
-  // coordinates of this lane's two output voxels (B-operand rows)
-  int vx[2], vy[2], vz[2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int v = v0 + wc * 64 + j * 32 + r;
-    vx[j] = v / R2;
-    vy[j] = (v / R) % R;
-    vz[j] = v % R;
-  }
-  // this lane's place in a 1-KiB piece: row lane / 2, physical half lane & 1
-  const int prow = lane >> 1, phalf = lane & 1;
-
-  auto issue = [&](int s, int buf) {
-    const int c0 = (s / 9) * kHK, pair = s - (s / 9) * 9;
-    const int dx = pair / 3 - 1, dy = pair % 3 - 1;
-    const int off = dx * R2 + dy * R;
-    uint8_t* base = lds + buf * kHStage;
-#pragma unroll
-    for (int q = 0; q < kHQ; ++q) {
-      const int I = w + 8 * q;
-      if (I < 6 * kHAPieces) {  // weights: image a = 2 * dz-index + (hi|lo)
-        const int a = I / kHAPieces, P = I % kHAPieces;
-        const int row = 32 * P + prow;
-        const int tap = pair * 3 + (a >> 1);
-        const uint16_t* src = ((a & 1) ? wl : wh) + ((size_t)tap * M + m0 + row) * K + c0 +
-                              8 * (phalf ^ hswz(row));
-        glds16_asm(src, lds_addr(base + a * kHAImg + P * 1024));
-      } else if (I < kHPieces) {  // X rows v0 + off - 1 + row
-        const int I2 = I - 6 * kHAPieces;
-        const int hl = I2 / kHBPieces, P = I2 % kHBPieces;
-        const int row = 32 * P + prow;
-        int gv = v0 + off - 1 + row;
-        gv = gv < 0 ? 0 : (gv >= V ? V - 1 : gv);  // out-of-volume rows are zeroed at use
-        const uint16_t* src = (hl ? xl : xh) + (bV + gv) * K + c0 + 8 * (phalf ^ hswz(row));
-        glds16_asm(src, lds_addr(base + 6 * kHAImg + hl * kHBImg + P * 1024));
-      }
-    }
-  };
-
-  f32x16 acc[2][2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
-
-  issue(0, 0);
-  if (nsteps > 1) issue(1, 1);
-  for (int s = 0; s < nsteps; ++s) {
-    // stage s landed (this wave's pieces): stage s+1's (>= kHQmin) stay in flight
-    if (s + 1 < nsteps) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kHQmin) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // everyone's stage s landed; stage s-1 reads done
-#ifndef PCFM_EXP_NOLOAD
-    if (s + 2 < nsteps) issue(s + 2, (s + 2) % kHStages);
-#endif
-    const uint8_t* base = lds + (s % kHStages) * kHStage;
-    const int pair = s % 9;
-    const int dx = pair / 3 - 1, dy = pair % 3 - 1;
-    bool okxy[2];
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-      okxy[j] = (unsigned)(vx[j] + dx) < (unsigned)R && (unsigned)(vy[j] + dy) < (unsigned)R;
-    // operands of tap tz+1 are read before tap tz's MFMAs (register double
-    // buffer), so only the first tap of a step waits for LDS latency
-    bf16x8 op[2][8];  // [buffer][ah0 ah1 al0 al1 bh0 bh1 bl0 bl1]
-    auto read_ops = [&](int tz, bf16x8 (&o)[8]) {
-      const int dz = tz - 1;
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int row = wr * 64 + i * 32 + r;
-        const int a = (2 * tz) * kHAImg + row * kHRow + ((h ^ hswz(row)) << 4);
-        o[i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(base + a));
-        o[2 + i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(base + a + kHAImg));
-      }
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int row = wc * 64 + j * 32 + r + 1 + dz;
-        const int a = 6 * kHAImg + row * kHRow + ((h ^ hswz(row)) << 4);
-        const bool ok = okxy[j] && (unsigned)(vz[j] + dz) < (unsigned)R;
-        o[4 + j] = zero_unless(ok, __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(base + a)));
-        o[6 + j] = zero_unless(
-            ok, __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(base + a + kHBImg)));
-      }
-    };
-    read_ops(0, op[0]);
-#pragma unroll
-    for (int tz = 0; tz < 3; ++tz) {
-      if (tz < 2) read_ops(tz + 1, op[(tz + 1) & 1]);
-      const bf16x8(&o)[8] = op[tz & 1];
-#ifdef PCFM_EXP_NOMFMA
-      acc[0][0][tz] += (float)(o[0][0] + o[2][1] + o[1][2] + o[3][3] + o[4][4] + o[6][5] +
-                               o[5][6] + o[7][7]);
-      continue;
-#endif
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(o[i], o[4 + j], acc[i][j], 0, 0, 0);
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(o[i], o[6 + j], acc[i][j], 0, 0, 0);
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(o[2 + i], o[4 + j], acc[i][j], 0, 0, 0);
-#ifndef PCFM_EXP_NOSCHED
-      if (tz < 2) {  // spread the next tap's 8 operand reads over this tap's 12 MFMAs
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-        }
-        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
-      }
-#endif
-    }
-  }
-  float* __restrict__ yb = y + (size_t)b * M * V;
-  float biasv[2][16];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) load_bias16(bias, m0 + wr * 64 + i * 32, h, M, biasv[i]);
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int m = m0 + wr * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
-        const int v = v0 + wc * 64 + j * 32 + r;
-        yb[(size_t)m * V + v] = acc[i][j][e] + biasv[i][e];
-      }
 }
 
 // ---------------------------------------------------------------------------
@@ -974,13 +783,13 @@ __global__ void __launch_bounds__(256)
     for (int q = 0; q < 4; ++q) {
       const int row = (t >> 4) + 16 * q;
       const int v = v0 + row;
-      const size_t ga = (rowA + v) * cout + co0 + ch * 8;
+      const size_t ga = split_off(rowA + v, co0 + ch * 8, cout);
       sv_put<4>(rah, q, *reinterpret_cast<const uint4*>(gh + ga));
       sv_put<4>(ral, q, *reinterpret_cast<const uint4*>(gl + ga));
       const int xq = v / R2, yq = (v / R) % R, zq = v % R;
       const bool inb = (unsigned)(xq + dx) < (unsigned)R && (unsigned)(yq + dy_) < (unsigned)R &&
                        (unsigned)(zq + dz) < (unsigned)R;
-      const size_t gb = (rowA + (inb ? v + off : v)) * cin + ci0 + ch * 8;
+      const size_t gb = split_off(rowA + (inb ? v + off : v), ci0 + ch * 8, cin);
       const uint4 hv = *reinterpret_cast<const uint4*>(xh + gb);
       const uint4 lv = *reinterpret_cast<const uint4*>(xl + gb);
       sv_put<4>(rbh, q, inb ? hv : uint4{0u, 0u, 0u, 0u});
@@ -1191,7 +1000,7 @@ __global__ void __launch_bounds__(kW3Threads)
         const int img = I / kW3APieces, P = I % kW3APieces;
         const int row = 4 * P + (lane >> 4);
         const int ch = (lane & 15) ^ (((row & 3) << 2) | ((row >> 2) & 3));
-        const uint16_t* src = (img ? gl : gh) + (base + v0 + row) * cout + co0 + ch * 8;
+        const uint16_t* src = (img ? gl : gh) + split_off(base + v0 + row, co0 + ch * 8, cout);
         glds16_asm(src, lds_addr(buf + img * kW3AImg + P * 1024));
       } else if (I < kW3Pieces) {
         const int I2 = I - 2 * kW3APieces;
@@ -1200,7 +1009,7 @@ __global__ void __launch_bounds__(kW3Threads)
         const int ch = (lane & 15) ^ (((row & 3) << 2) | ((row >> 2) & 3));
         int gv = v0 + off - 1 + row;
         gv = gv < 0 ? 0 : (gv >= V ? V - 1 : gv);  // out-of-volume rows are masked at use
-        const uint16_t* src = (img ? xl : xh) + (base + gv) * cin + ci0 + ch * 8;
+        const uint16_t* src = (img ? xl : xh) + split_off(base + gv, ci0 + ch * 8, cin);
         glds16_asm(src, lds_addr(buf + 2 * kW3AImg + img * kW3BImg + P * 1024));
       }
     }
@@ -1396,11 +1205,13 @@ extern "C" size_t pcfm_conv3d_weight_bytes(int cout, int cin) {
 
 extern "C" int pcfm_conv3d_prep_weight(const float* w, int cout, int cin, int transpose,
                                        void* wsplit, void* stream) {
-  PCFM_CHECK_ARG(cout > 0 && cin > 0, "conv3d_prep_weight: bad size cout=%d cin=%d", cout, cin);
+  PCFM_CHECK_ARG(cout > 0 && cin > 0 && (transpose ? cout : cin) % 32 == 0,
+                 "conv3d_prep_weight: bad size cout=%d cin=%d (the GEMM's K %% 32 == 0)", cout,
+                 cin);
   const size_t total = (size_t)27 * cout * cin;
   uint16_t* wh = (uint16_t*)wsplit;
   hipLaunchKernelGGL(conv3_wsplit_kernel, dim3(ceil_div((long long)total, 256)), dim3(256), 0,
-                     (hipStream_t)stream, w, cout, cin, transpose ? 1 : 0, wh, wh + total);
+                     (hipStream_t)stream, w, cout, cin, transpose ? 1 : 0, wh);
   return check_launch("conv3d_prep_weight");
 }
 
@@ -1494,7 +1305,7 @@ extern "C" int pcfm_conv3d_split(const float* x, int b, int c, int r, void* xs, 
   const int V = r * r * r;
   uint16_t* xh = (uint16_t*)xs;
   hipLaunchKernelGGL(conv3_split_cl_kernel, dim3(V / 64, c / 64, b), dim3(256), 0,
-                     (hipStream_t)stream, x, c, V, xh, xh + (size_t)b * V * c);
+                     (hipStream_t)stream, x, c, V, xh);
   return check_launch("conv3d_split");
 }
 
@@ -1555,10 +1366,9 @@ static int igemm_cl(const void* xs, const void* wsplit, const float* bias, int b
                  "conv3d_igemm_cl: unsupported shape b=%d cin=%d cout=%d r=%d", b, cin, cout, r);
   if (b == 0) return PCFM_OK;
   const int V = r * r * r;
-  const size_t total = (size_t)27 * cout * cin;
   const uint16_t* wh = (const uint16_t*)wsplit;
   const uint16_t* xh = (const uint16_t*)xs;
-  const uint16_t* xl = xh + (size_t)b * V * cin;
+  const uint16_t* xl = xh + kSplitLo;  // interleaved hi / lo (split_off)
   hipStream_t st = (hipStream_t)stream;
   const long long big_blocks = (long long)(V / 128) * (cout / 128) * b;
 #ifndef PCFM_CONV_NOGLDS
@@ -1574,13 +1384,6 @@ static int igemm_cl(const void* xs, const void* wsplit, const float* bias, int b
       set_error("conv3d_igemm_cl: zero-row allocation failed");
       return (int)hipErrorOutOfMemory;
     }
-#ifdef PCFM_CONV_GLDS3  // three-tap variant: 3x less X traffic, measured equal speed
-    if (S == 1 && cin % kHK == 0) {
-      hipLaunchKernelGGL(conv3_igemm_glds3_kernel, dim3((unsigned)glds_blocks), dim3(512), 0, st,
-                         xh, xl, wh, wh + total, bias, y, cin, cout, r);
-      return check_launch("conv3d_igemm_cl");
-    }
-#endif
 #ifndef PCFM_CONV_GK
 #define PCFM_CONV_GK 32  // 16: two blocks per CU, measured 1.15-1.18x slower
 #endif
@@ -1589,7 +1392,7 @@ static int igemm_cl(const void* xs, const void* wsplit, const float* bias, int b
     if (S == 1 && PCFM_CONV_GK == 32 && cin % 32 == 0) {
       const long long blocks128 = (long long)(V / 128) * (cout / kGM) * b;
       hipLaunchKernelGGL((conv3_igemm_glds_kernel<32, 128, 2>), dim3((unsigned)blocks128),
-                         dim3(256), 0, st, xh, xl, wh, wh + total, zrow, bias, y, cin, cout, r, 1,
+                         dim3(256), 0, st, xh, xl, wh, wh + kSplitLo, zrow, bias, y, cin, cout, r, 1,
                          part, tmask, mmode);
       return check_launch("conv3d_igemm_cl");
     }
@@ -1599,11 +1402,11 @@ static int igemm_cl(const void* xs, const void* wsplit, const float* bias, int b
     const int mm = S == 1 && tmask != nullptr ? mmode : 0;
     if (PCFM_CONV_GK == 16 || cin % 32 != 0)
       hipLaunchKernelGGL(conv3_igemm_glds_kernel<16>, dim3((unsigned)glds_blocks), dim3(512), 0,
-                         st, xh, xl, wh, wh + total, zrow, bias, y, cin, cout, r, S, part, tmask,
+                         st, xh, xl, wh, wh + kSplitLo, zrow, bias, y, cin, cout, r, S, part, tmask,
                          mm);
     else
       hipLaunchKernelGGL(conv3_igemm_glds_kernel<32>, dim3((unsigned)glds_blocks), dim3(512), 0,
-                         st, xh, xl, wh, wh + total, zrow, bias, y, cin, cout, r, S, part, tmask,
+                         st, xh, xl, wh, wh + kSplitLo, zrow, bias, y, cin, cout, r, S, part, tmask,
                          mm);
     if (S > 1) {
       const long long total4 = (long long)b * cout * V / 4;
@@ -1615,7 +1418,7 @@ static int igemm_cl(const void* xs, const void* wsplit, const float* bias, int b
 #endif
   if (big_blocks >= 2 * kCUs) {
     hipLaunchKernelGGL((conv3_igemm_cl_kernel<128, 128, PCFM_CONV_KT>),
-                       dim3((V / 128) * (cout / 128) * b), dim3(256), 0, st, xh, xl, wh, wh + total,
+                       dim3((V / 128) * (cout / 128) * b), dim3(256), 0, st, xh, xl, wh, wh + kSplitLo,
                        bias, y, cin, cout, r, 1, nullptr);
   } else {
     const int S = igemm_splits(b, cin, cout, r);
@@ -1624,7 +1427,7 @@ static int igemm_cl(const void* xs, const void* wsplit, const float* bias, int b
                    "conv3d_igemm_cl: workspace %zu < %zu bytes", ws_bytes, need);
     const int items = (V / 64) * (cout / 64) * b;
     hipLaunchKernelGGL((conv3_igemm_cl_kernel<64, 64, PCFM_CONV_KT>), dim3(items * S), dim3(256),
-                       0, st, xh, xl, wh, wh + total, bias, y, cin, cout, r, S, (float*)ws);
+                       0, st, xh, xl, wh, wh + kSplitLo, bias, y, cin, cout, r, S, (float*)ws);
     if (S > 1) {
       const long long total4 = (long long)b * cout * V / 4;
       hipLaunchKernelGGL(conv3_ksum_kernel, dim3((unsigned)ceil_div(total4, 256)), dim3(256), 0,
@@ -1701,11 +1504,11 @@ static int wgrad_cl(const void* xs, const void* gys, int b, int cin, int cout, i
                          b * (V / kWV), S, cap, lists, counts);
     }
     hipLaunchKernelGGL(conv3_wgrad3_kernel, dim3(tiles / 3 * S), dim3(kW3Threads), 2 * kW3Buf, st,
-                       xh, xh + (size_t)b * V * cin, gh, gh + (size_t)b * V * cout, b, cin, cout, r,
+                       xh, xh + kSplitLo, gh, gh + kSplitLo, b, cin, cout, r,
                        S, (float*)ws, lists, counts, cap);
   } else {
     hipLaunchKernelGGL(conv3_wgrad_cl_kernel, dim3(tiles * S), dim3(256), 0, st, xh,
-                       xh + (size_t)b * V * cin, gh, gh + (size_t)b * V * cout, b, cin, cout, r, S,
+                       xh + kSplitLo, gh, gh + kSplitLo, b, cin, cout, r, S,
                        (float*)ws);
   }
   hipLaunchKernelGGL(conv3_wgrad_reduce_kernel, dim3(ceil_div((long long)cout * cin, 64)),

@@ -402,13 +402,14 @@ __global__ void __launch_bounds__(256)
 typedef __bf16 bn_bf16x2 __attribute__((ext_vector_type(2)));
 
 // A 64 (channel) x 64 (voxel) fp32 LDS tile -> channels-last bf16 hi / lo
-// rows [b][v][c] (conv3_split_cl_kernel's layout and rounding), 256 threads:
+// rows [b][v][c] interleaved per 32 channels (conv3_split_cl_kernel's layout,
+// split_off, and rounding), 256 threads:
 // thread t writes 16 channels of voxel t / 4.
 __device__ __forceinline__ void tile_store_split(const float (&tile)[64][65], int b, int C, int S,
                                                  int v0, int c0, int t, uint16_t* __restrict__ h,
                                                  uint16_t* __restrict__ l) {
   const int v = t >> 2, cg = (t & 3) * 16;
-  const size_t o = ((size_t)b * S + v0 + v) * C + c0 + cg;
+  const size_t o = split_off((size_t)b * S + v0 + v, c0 + cg, C);  // l = h + kSplitLo
   uint32_t* h32 = reinterpret_cast<uint32_t*>(h + o);
   uint32_t* l32 = reinterpret_cast<uint32_t*>(l + o);
 #pragma unroll
@@ -848,7 +849,7 @@ extern "C" int pcfm_bn_act_fwd_split(const float* x, const float* gamma, const f
   uint16_t* yh = (uint16_t*)ys;
   hipLaunchKernelGGL(bn_act_apply_split_kernel, dim3(s / 64, c / 64, b), dim3(256), 0, st, x,
                      fin, mean, invstd, gamma, beta, c, s, slope, yh,
-                     yh + (size_t)b * s * c);
+                     yh + kSplitLo);
   return check_launch("bn_act_fwd_split");
 }
 
@@ -874,7 +875,7 @@ extern "C" int pcfm_bn_act_bwd_split(const float* dz, const float* x, const floa
   uint16_t* dxh = (uint16_t*)dxs;
   hipLaunchKernelGGL(bn_bwd_apply_split_kernel, dim3(s / 64, c / 64, b), dim3(256), 0, st, dz, x,
                      mean, invstd, gamma, beta, (const float*)part, bn_parts(b), dgamma, dbeta, c, s,
-                     (float)(1.0 / ((double)b * s)), slope, dxh, dxh + (size_t)b * s * c, rowpart);
+                     (float)(1.0 / ((double)b * s)), slope, dxh, dxh + kSplitLo, rowpart);
   if (dbias_in != nullptr)
     hipLaunchKernelGGL(bn_bias_finalize_block_kernel, dim3(c), dim3(256), 0, st,
                        (const float*)rowpart, b, c, s / 64, dbias_in);

@@ -37,6 +37,17 @@ constexpr int kLdsBytesMax = 160 * 1024;
 // Raise the dynamic-LDS cap of one kernel to the gfx950 maximum once.
 int allow_big_lds(const void* kernel);
 
+// Split operands (bf16 hi / lo of an fp32 tensor, channels-last rows of C
+// channels, C % 32 == 0) are stored interleaved per 32-channel group: row r
+// holds [hi c0..c31 | lo c0..c31 | hi c32..c63 | lo c32..c63 | ...], so the
+// hi and lo halves of one K-step of 32 channels share one 128-byte line (a
+// step fetches whole lines, not halves of lines it reads the rest of 27 steps
+// later).  Element offset of (row, channel c) in hi; its lo is 32 further.
+__host__ __device__ inline size_t split_off(size_t row, int c, int C) {
+  return row * 2 * (size_t)C + (size_t)(((c >> 5) << 6) + (c & 31));
+}
+constexpr int kSplitLo = 32;  // element offset of lo from hi
+
 // Squared distance contract shared by every nearest-neighbour kernel and the
 // oracle: dx = q - p;  d = fma(dz, dz, fma(dx, dx, dy*dy)).
 // (This is how NVVM contracts the reference's `x*x + y*y + z*z`; pinned here
