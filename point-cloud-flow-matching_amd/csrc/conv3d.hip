@@ -1206,7 +1206,7 @@ extern "C" size_t pcfm_conv3d_weight_bytes(int cout, int cin) {
 extern "C" int pcfm_conv3d_prep_weight(const float* w, int cout, int cin, int transpose,
                                        void* wsplit, void* stream) {
   PCFM_CHECK_ARG(cout > 0 && cin > 0 && (transpose ? cout : cin) % 32 == 0,
-                 "conv3d_prep_weight: bad size cout=%d cin=%d (the GEMM's K %% 32 == 0)", cout,
+                 "conv3d_prep_weight: unsupported size cout=%d cin=%d (the GEMM's K %% 32 == 0)", cout,
                  cin);
   const size_t total = (size_t)27 * cout * cin;
   uint16_t* wh = (uint16_t*)wsplit;
