@@ -731,6 +731,187 @@ __device__ __forceinline__ void glds16_asm(const void* g, uint32_t lds) {
 }
 
 // ---------------------------------------------------------------------------
+// Forward / backward-data, PING-PONG form of the LDS-DMA kernel above (same
+// 128 x 256 tile, 32-channel K-steps, three LDS stages, same A / B pieces).
+// There both waves of a SIMD read fragments, issue LDS-DMA and run MFMAs in
+// the same interval and meet at one barrier per step, so their matrix and
+// memory work add up (measured: no-MFMA 0.36 ms + MFMA-only 0.28 ms ~ 0.67 ms
+// as built).  Here waves 0-3 (group 0, one per SIMD, m rows 0-63) and waves
+// 4-7 (group 1, m rows 64-127) run half a step apart: in every phase one wave
+// of each SIMD issues its 24 MFMAs from registers while its partner reads the
+// next step's fragments and issues its LDS-DMA pieces, and the roles swap at
+// the phase barrier (MI355X_MICROARCH.md "Two waves per SIMD").
+//   phase 2t:   group 0 reads stage t, issues its pieces of step t + 2;
+//               group 1 computes step t - 1
+//   phase 2t+1: group 0 computes step t;
+//               group 1 reads stage t, issues its pieces of step t + 2
+// Stage t's buffer is last read in phase 2t+1, refilled (step t + 3) from
+// phase 2t+2 on; a wave's share of step t lands before the barrier that
+// opens phase 2t (counted vmcnt).  Same accumulation order per output as the
+// LDS-DMA kernel (bit-identical results).
+// ---------------------------------------------------------------------------
+template <int KT>
+__global__ void __launch_bounds__(512)
+    conv3_igemm_pp_kernel(const uint16_t* __restrict__ xh, const uint16_t* __restrict__ xl,
+                          const uint16_t* __restrict__ wh, const uint16_t* __restrict__ wl,
+                          const uint16_t* __restrict__ zrow, const float* __restrict__ bias,
+                          float* __restrict__ y, int K, int M, int R,
+                          const uint32_t* __restrict__ tmask, int mmode) {
+  constexpr int GN = kGN, NST = 3;
+  using G = GK<KT, GN>;
+  static_assert(G::NW == 8 && G::APW + G::BPW == 6, "ping-pong form: 8 waves, 6 pieces each");
+  __shared__ __attribute__((aligned(16))) uint8_t lds[NST * G::STAGE];
+  const int V = R * R * R, R2 = R * R;
+  int id = (int)blockIdx.x;
+  {
+    const int nwg = (int)gridDim.x, q = nwg / 8, rr = nwg % 8, xcd = id % 8;
+    id = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + id / 8;
+  }
+  const int nmt = M / kGM, nvt = V / GN;
+  const int m0 = (id % nmt) * kGM;
+  id /= nmt;
+  const int v0 = (id % nvt) * GN;
+  const int b = id / nvt;
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int grp = w >> 2;                 // 0: waves 0-3, 1: waves 4-7
+  const int wr = grp, wc = w & 3, r = lane & 31, h = lane >> 5;
+  const uint32_t kAll = 0x7FFFFFFu;
+  uint32_t mask = kAll;
+  if (mmode != 0) {
+    const uint32_t mm = __builtin_amdgcn_readfirstlane(tmask[(size_t)b * (V >> 8) + (v0 >> 8)]);
+    mask = mmode == 1 ? (mm & kAll) : ((mm >> 31) ? kAll : 0u);
+  }
+  const int na = __builtin_popcount(mask);
+  const int nsteps = na * (K / KT);
+  const int first = mask != 0u ? __builtin_ctz(mask) : 0;
+  // (ichunk, itap) of the step last issued (iseq); issue() advances one step
+  int iseq = 0, ichunk = 0, itap = first;
+  const size_t bV = (size_t)b * V;
+  const int prow = lane / G::CPR, pch = lane % G::CPR;
+  const uint16_t* abase[G::APW];
+#pragma unroll
+  for (int q = 0; q < G::APW; ++q) {
+    const int I = G::APW * w + q;
+    const int row = (I % G::API) * G::RPP + prow;
+    abase[q] = ((I / G::API) ? wl : wh) + (size_t)(m0 + row) * 2 * K + ((pch ^ G::swz(row)) << 3);
+  }
+  const uint16_t* bbase[G::BPW];
+  const uint16_t* zbase[G::BPW];
+  int bxyz[G::BPW];
+#pragma unroll
+  for (int q = 0; q < G::BPW; ++q) {
+    const int I = G::BPW * w + q;
+    const int row = (I % G::BPI) * G::RPP + prow;
+    const int v = v0 + row;
+    const int cofs = (pch ^ G::swz(row)) << 3;
+    bbase[q] = ((I / G::BPI) ? xl : xh) + (bV + v) * 2 * K + cofs;
+    zbase[q] = zrow + cofs;
+    bxyz[q] = (v / R2) | (((v / R) % R) << 10) | ((v % R) << 20);
+  }
+  // this wave's 6 pieces of step sl (sl = iseq or iseq + 1) into stage buffer buf
+  auto issue = [&](int sl, int buf) {
+    {
+      const bool adv = sl != iseq;
+      const uint32_t rest = mask & ~((2u << itap) - 1u);
+      const int nt = rest != 0u ? __builtin_ctz(rest) : first;
+      ichunk += (adv && rest == 0u) ? 1 : 0;
+      itap = adv ? nt : itap;
+      iseq = sl;
+    }
+    const int c0 = ichunk * KT, tap = itap;
+    const int cof = ((c0 >> 5) << 6) + (c0 & 31);
+    uint8_t* base = lds + buf * G::STAGE;
+    const size_t aofs = (size_t)tap * M * 2 * K + cof;
+#pragma unroll
+    for (int q = 0; q < G::APW; ++q) {
+      const int I = G::APW * w + q;
+      glds16_asm(abase[q] + aofs, lds_addr(base + (I / G::API) * G::A + (I % G::API) * 1024));
+    }
+    const int dx = tap / 9 - 1, dy = (tap / 3) % 3 - 1, dz = tap % 3 - 1;
+    const long long bofs = (long long)(dx * R2 + dy * R + dz) * 2 * K + cof;
+#pragma unroll
+    for (int q = 0; q < G::BPW; ++q) {
+      const int I = G::BPW * w + q;
+      const int x = bxyz[q] & 1023, yy = (bxyz[q] >> 10) & 1023, z = bxyz[q] >> 20;
+      const bool inb = (unsigned)(x + dx) < (unsigned)R && (unsigned)(yy + dy) < (unsigned)R &&
+                       (unsigned)(z + dz) < (unsigned)R;
+      const unsigned long long src = (unsigned long long)(bbase[q] + bofs);
+      const unsigned long long zsrc = (unsigned long long)zbase[q];
+      const unsigned long long msk = 0ull - (unsigned long long)inb;
+      glds16_asm((const void*)((src & msk) | (zsrc & ~msk)),
+                 lds_addr(base + 2 * G::A + (I / G::BPI) * G::B + (I % G::BPI) * 1024));
+    }
+  };
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
+
+  if (nsteps > 0) {
+    bf16x8 F[KT / 16][8];
+    issue(0, 0);
+    if (nsteps > 1) {
+      issue(1, 1);
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // step 0 landed (own pieces)
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    for (int p = 0; p <= 2 * nsteps; ++p) {
+      // group 0: memory on even phases (step p / 2), compute on odd (step (p - 1) / 2)
+      // group 1: memory on odd phases (step (p - 1) / 2), compute on even (step p / 2 - 1)
+      const bool mem = ((p & 1) == grp);
+      const int st = grp == 0 ? (p >> 1) : ((p - 1) >> 1);  // the step of this phase's memory work
+      if (mem) {
+        if (st < nsteps) {
+          __builtin_amdgcn_sched_barrier(0);
+          if (st + 2 < nsteps) issue(st + 2, (st + 2) % NST);
+          glds_frags<KT, GN>(lds, st % NST, wr, wc, r, h, F);
+          __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): fragments in registers
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      } else {
+        const int cs = grp == 0 ? ((p - 1) >> 1) : ((p >> 1) - 1);  // the step computed now
+        if (cs >= 0 && cs < nsteps) {
+          __builtin_amdgcn_sched_barrier(0);
+          glds_mfma<KT>(F, acc);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      // before a phase 2s (group 0 reads stage s = p / 2 + 1... of the next
+      // even phase): every wave's share of that step has landed
+      if ((p & 1) == 1) {
+        const int s = (p + 1) >> 1;  // the stage group 0 reads next
+        if (s + 1 < nsteps) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __builtin_amdgcn_s_barrier();
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  float* __restrict__ yb = y + (size_t)b * M * V;
+  float biasv[2][16];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) load_bias16(bias, m0 + wr * 64 + i * 32, h, M, biasv[i]);
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int m = m0 + wr * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+        const int v = v0 + wc * 64 + j * 32 + r;
+        __builtin_nontemporal_store(acc[i][j][e] + biasv[i][e], yb + (size_t)m * V + v);
+      }
+}
+
+
+// ---------------------------------------------------------------------------
 // Weight gradient over the channels-last split operands (the forward's split
 // input xs and the backward-data pass's split dY): per tap a GEMM reducing over
 // voxels, dW[co][ci] = sum_v dY[v][co] * X[v + off][ci], both operands
@@ -1359,6 +1540,15 @@ extern "C" size_t pcfm_conv3d_igemm_cl_workspace_bytes(int b, int cin, int cout,
   return S == 1 ? 1 : (size_t)S * b * cout * r * r * r * sizeof(float);
 }
 
+// Ping-pong form of the LDS-DMA kernel (PCFM_CONV_PP=0: the one-phase form)
+static bool conv_pp() {
+  static const bool on = [] {
+    const char* e = getenv("PCFM_CONV_PP");
+    return e == nullptr || e[0] != '0';
+  }();
+  return on;
+}
+
 static int igemm_cl(const void* xs, const void* wsplit, const float* bias, int b, int cin,
                     int cout, int r, float* y, void* ws, size_t ws_bytes, void* stream,
                     const uint32_t* tmask, int mmode) {
@@ -1400,6 +1590,11 @@ static int igemm_cl(const void* xs, const void* wsplit, const float* bias, int b
     // tile masks apply to unsplit launches only (a split's K range is a fixed
     // share of all 27 taps)
     const int mm = S == 1 && tmask != nullptr ? mmode : 0;
+    if (S == 1 && PCFM_CONV_GK == 32 && cin % 32 == 0 && conv_pp()) {
+      hipLaunchKernelGGL(conv3_igemm_pp_kernel<32>, dim3((unsigned)glds_blocks), dim3(512), 0, st,
+                         xh, xl, wh, wh + kSplitLo, zrow, bias, y, cin, cout, r, tmask, mm);
+      return check_launch("conv3d_igemm_cl");
+    }
     if (PCFM_CONV_GK == 16 || cin % 32 != 0)
       hipLaunchKernelGGL(conv3_igemm_glds_kernel<16>, dim3((unsigned)glds_blocks), dim3(512), 0,
                          st, xh, xl, wh, wh + kSplitLo, zrow, bias, y, cin, cout, r, S, part, tmask,

@@ -1,0 +1,4 @@
+cd $GRAFT_REPO_ROOT
+bash tools/gpu_r03_j.sh
+echo "j done rc=$?"
+bash tools/gpu_r03_i.sh
