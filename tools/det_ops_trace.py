@@ -80,7 +80,11 @@ def main():
                 first = {"call": i, "op": n0, "other": n1, "why": "sequence differs"}
                 break
             if not eq(i0, i1):
-                first = {"call": i, "op": n0, "why": "inputs differ (an earlier op or a race)"}
+                bad = [(j, list(u.shape), str(u.dtype), float((u.double() - v.double()).abs().max()))
+                       for j, (u, v) in enumerate(zip(i0, i1))
+                       if u.dtype not in (torch.uint8, torch.int64) and not torch.equal(u, v)]
+                first = {"call": i, "op": n0, "why": "inputs differ (an earlier op or a race)",
+                         "inputs": bad, "prev_ops": [runs[0][q][0] for q in range(max(0, i - 4), i)]}
                 break
             if not eq(o0, o1) or not eq(p0, p1):
                 first = {"call": i, "op": n0, "why": "same inputs, different outputs"}
