@@ -58,9 +58,11 @@ def run(path):
 
 def compare(a, b):
     A, B = torch.load(a, weights_only=True), torch.load(b, weights_only=True)
-    res = {k: bool(torch.equal(A[k], B[k])) for k in A}
-    print(json.dumps({"all_equal": all(res.values()), "cases": res}))
-    return all(res.values())
+    res = {k: float((A[k].double() - B[k].double()).abs().max() / A[k].double().pow(2).mean().sqrt())
+           for k in A}
+    print(json.dumps({"all_equal": all(v == 0.0 for v in res.values()),
+                      "max_rel_to_rms": max(res.values()), "cases": res}))
+    return max(res.values()) < 1e-5
 
 
 if __name__ == "__main__":
