@@ -21,7 +21,8 @@ TRACE = []
 
 def _tensors(x):
     if isinstance(x, torch.Tensor):
-        return [x]
+        # expanded stand-ins (stride 0, e.g. shape probes of an empty scalar) hold no data
+        return [] if 0 in x.stride() and x.numel() > 1 else [x]
     if isinstance(x, (list, tuple)):
         return [t for e in x for t in _tensors(e)]
     if hasattr(x, "__dict__") and not isinstance(x, type):
