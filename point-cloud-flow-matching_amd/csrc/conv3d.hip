@@ -1775,11 +1775,13 @@ static bool conv_pp() {
   return on;
 }
 
-// Halo-brick form for r = 32 / 16 (PCFM_CONV_BRICK=0: the LDS-DMA kernel)
+// Halo-brick form for r = 32 / 16 (opt-in, PCFM_CONV_BRICK=1: measured 1.25x
+// slower -- 12 MFMAs per wave between barriers at 16-channel steps; the
+// per-step cost, not the B fetches, sets its pace)
 static bool conv_brick() {
   static const bool on = [] {
     const char* e = getenv("PCFM_CONV_BRICK");
-    return e == nullptr || e[0] != '0';
+    return e != nullptr && e[0] == '1';
   }();
   return on;
 }
