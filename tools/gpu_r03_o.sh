@@ -1,9 +1,9 @@
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-RUNS=10 timeout -k 10 400 python tools/pv_race_probe.py > gpurun_out/pvrace0.jsonl 2> gpurun_out/pvrace0.err &
+FREEZE=0 RUNS=10 timeout -k 10 400 python tools/pv_race_probe.py > gpurun_out/pvrace0.jsonl 2> gpurun_out/pvrace0.err &
 p0=$!
-RUNS=10 timeout -k 10 400 python tools/pv_race_probe.py > gpurun_out/pvrace1.jsonl 2> gpurun_out/pvrace1.err &
+FREEZE=0 RUNS=10 timeout -k 10 400 python tools/pv_race_probe.py > gpurun_out/pvrace1.jsonl 2> gpurun_out/pvrace1.err &
 p1=$!
 wait $p0; r0=$?
 wait $p1; r1=$?

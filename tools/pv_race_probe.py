@@ -46,9 +46,10 @@ def main():
     cfg = TrainConfig(batch_size=b, num_points=n, tunableop=False, miopen_find=False)
     tr = Trainer(cfg, dev)
     tr.train_mode()
-    for m in tr.pf.modules():
-        if isinstance(m, torch.nn.modules.batchnorm._BatchNorm):
-            m.momentum = 0.0
+    if os.environ.get("FREEZE", "1") == "1":
+        for m in tr.pf.modules():
+            if isinstance(m, torch.nn.modules.batchnorm._BatchNorm):
+                m.momentum = 0.0
     g = torch.Generator(device=dev).manual_seed(0)
     x = torch.randn(b, n, 6, device=dev, generator=g)
     t = torch.rand(b, device=dev, generator=g)
