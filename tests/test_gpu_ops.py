@@ -143,6 +143,34 @@ def test_devox_full_size_properties():
     assert torch.allclose(wgts.sum(1), torch.ones_like(wgts[:, 0]), atol=1e-6)
 
 
+@pytest.mark.parametrize("c,r", [(128, 32), (256, 16), (256, 8)])
+def test_devox_c2_matches_grid_sample(c, r):
+    """Outside pin at the C2 stage shapes: the devox kernels against PyTorch's
+    own trilinear interpolation (grid_sample, align_corners=True, fp64) and its
+    autograd adjoint; plus the product's SE-scale + point-branch gather
+    (out = s * devox(grid) + pf)."""
+    from pcfm import ops
+    from golden_util import grid_sample_devox as _grid_sample_devox
+    b, n = 8, 20000
+    g = torch.Generator(device=DEV).manual_seed(r)
+    pts = torch.rand(b, 3, n, device=DEV, generator=g) * (r - 1)
+    pts[:, :, :64] = pts[:, :, :64].round()
+    grid = torch.randn(b, c, r ** 3, device=DEV, generator=g)
+    out, inds, wgts = ops.trilinear_devoxelize_forward(r, True, pts, grid)
+    tg = grid.double().requires_grad_(True)
+    ref = _grid_sample_devox(tg, pts.double(), r)
+    torch.testing.assert_close(out.double(), ref.detach(), rtol=1e-5, atol=1e-5)
+    gy = torch.randn(b, c, n, device=DEV, generator=g)
+    (gref,) = torch.autograd.grad(ref, tg, gy.double())
+    gx = ops.trilinear_devoxelize_backward(gy, inds, wgts, r)
+    torch.testing.assert_close(gx.double(), gref, rtol=1e-5, atol=1e-4)
+    s = torch.rand(b, c, device=DEV, generator=g)
+    pf = torch.randn(b, c, n, device=DEV, generator=g)
+    fused, _, _ = ops.trilinear_devoxelize_scale_add(r, False, pts, grid, s, pf)
+    torch.testing.assert_close(fused.double(), ref.detach() * s.double()[..., None] + pf.double(),
+                               rtol=1e-5, atol=1e-5)
+
+
 def test_voxelize_full_size_properties():
     from pcfm import ops
     b, c, n, r = 8, 128, 20000, 32

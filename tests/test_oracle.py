@@ -152,3 +152,49 @@ def test_grouping_roundtrip():
     gy = rng.random(out.shape, dtype=np.float32)
     gx = O.grouping_bwd(gy, idx, 30)
     np.testing.assert_allclose((out * gy).sum(), (feat * gx).sum(), rtol=1e-5)
+
+
+# --- outside pins: third-party implementations of the same arithmetic --------
+# The reference holds no fixtures for the PVCNN kernels and its CUDA cannot run
+# here, so these pin the oracle against PyTorch's own algorithms instead.
+
+def test_devoxelize_fwd_bwd_match_grid_sample():
+    import torch
+    from golden_util import grid_sample_devox as _grid_sample_devox
+    rng = np.random.default_rng(11)
+    for r, n in ((8, 3000), (5, 500)):
+        grid = rng.standard_normal((2, 6, r ** 3)).astype(np.float32)
+        pts = (rng.random((2, 3, n)) * (r - 1)).astype(np.float32)
+        pts[:, :, :8] = np.round(pts[:, :, :8])       # on-lattice points, incl. the r-1 face
+        pts[:, 0, 8] = r - 1
+        out, inds, wgts = O.trilinear_devoxelize_fwd(pts, grid, r)
+        tg = torch.from_numpy(grid).double().requires_grad_(True)
+        ref = _grid_sample_devox(tg, torch.from_numpy(pts).double(), r)
+        np.testing.assert_allclose(out, ref.detach().numpy(), rtol=1e-5, atol=1e-5)
+        gy = rng.standard_normal(out.shape).astype(np.float32)
+        (gref,) = torch.autograd.grad(ref, tg, torch.from_numpy(gy).double())
+        gx = O.trilinear_devoxelize_bwd(gy, inds, wgts, r)
+        np.testing.assert_allclose(gx, gref.numpy(), rtol=1e-5, atol=1e-4)
+
+
+def test_avg_voxelize_matches_scatter_reduce_mean():
+    import torch
+    rng = np.random.default_rng(12)
+    r, b, c, n = 6, 2, 5, 2000
+    coords = rng.integers(0, r, (b, 3, n)).astype(np.int32)
+    feat = rng.standard_normal((b, c, n)).astype(np.float32)
+    out, ind, cnt = O.avg_voxelize_fwd(feat, coords, r)
+    lin = torch.from_numpy(coords).long()
+    lin = lin[:, 0] * r * r + lin[:, 1] * r + lin[:, 2]                  # vox.cu:24-30
+    np.testing.assert_array_equal(ind, lin.int().numpy())
+    np.testing.assert_array_equal(cnt, torch.stack([torch.bincount(l, minlength=r ** 3)
+                                                    for l in lin]).int().numpy())
+    ref = torch.zeros(b, c, r ** 3, dtype=torch.float64).scatter_reduce(
+        2, lin[:, None].expand(b, c, n), torch.from_numpy(feat).double(), "mean",
+        include_self=False)
+    np.testing.assert_allclose(out, ref.numpy(), rtol=1e-5, atol=1e-6)
+    gy = rng.standard_normal(out.shape).astype(np.float32)
+    gx = O.avg_voxelize_bwd(gy, ind, cnt)
+    c64 = torch.from_numpy(cnt).double().clamp_min(1)
+    gref = torch.gather(torch.from_numpy(gy).double() / c64[:, None], 2, lin[:, None].expand(b, c, n))
+    np.testing.assert_allclose(gx, gref.numpy(), rtol=1e-6, atol=1e-7)
