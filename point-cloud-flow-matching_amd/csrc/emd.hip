@@ -21,7 +21,10 @@
 //     --use_fast_math (__expf, backend.py:20), so EMD parity is tolerance-based.
 #include "pcfm_common.hpp"
 
+#include <hip/hip_cooperative_groups.h>
+
 #include <algorithm>
+#include <cstdlib>
 
 namespace pcfm {
 namespace {
@@ -337,6 +340,224 @@ inline dim3 grid1d(size_t total, int threads = 256) {
   return dim3(ceil_div((long long)std::max<size_t>(total, 1), threads));
 }
 
+// ---------------------------------------------------------------------------
+// Persistent form: the whole auction (10 levels) + the match write in ONE
+// cooperative launch, the levels' phases separated by grid barriers instead of
+// kernel boundaries.  At the metric's sizes (B = 8, N = 2048: 33 M exp per
+// pass, ~1 us of v_exp issue) every pass of the multi-launch form above is
+// launch/drain bound; here a level is 3 barriers.  Same per-element
+// expressions and the same partial-sum order as the multi-launch form, so the
+// two are bit-identical (tests/test_gpu_ops.py::test_emd_persistent_bit_identical).
+//
+// Each finalize is folded into the phase that consumes it:
+//   P1 (rows k, cols l, coef remR)            -> partA;  also level j-1's fin3
+//        for the unit's rows (remL -= sum partC, levL[j-1] = ratL)
+//   P2 (rows l, cols k, coef ratL)            -> partB;  ratL = remL / (1e-9 + sum partA)
+//        computed per column into LDS (row tile 0 also stores it)
+//   P3 (rows k, cols l, coef ratR, rowscale ratL) -> partC;  ratR / remR' from
+//        partB per column into LDS (row tile 0 stores levR[j] and remR')
+// remR is double-buffered (P3 reads the level's remR while remR' is written).
+// ---------------------------------------------------------------------------
+constexpr int kPChunk = 1024;  // columns staged in LDS per chunk
+
+struct EmdPlan {
+  int b, n, m, S;
+  int tilesN, tilesM;  // ceil(n / kThreads), ceil(m / kThreads)
+};
+
+template <typename T>
+struct EmdPState {
+  const T* xyz1;
+  const T* xyz2;
+  T* remL;
+  T* remR[2];
+  T* ratL;
+  T* levL;
+  T* levR;
+  T* part[3];
+  T* match;
+  T multiL, multiR;
+};
+
+// The column coefficient of phase `ph` for column c of batch bb.
+template <typename T>
+__device__ __forceinline__ T p_coef(const EmdPState<T>& s, const EmdPlan& p, int ph, int lvl,
+                                    int bb, int c, bool store) {
+  if (ph == 0) return s.remR[lvl & 1][(size_t)bb * p.m + c];
+  if (ph == 1) {  // fin1: ratioL = remainL / (1e-9 + suml)
+    const size_t bn = (size_t)p.b * p.n, i = (size_t)bb * p.n + c;
+    const T v = s.remL[i] / ((T)1e-9f + sum_parts(s.part[0], p.S, bn, i));
+    if (store) s.ratL[i] = v;
+    return v;
+  }
+  // fin2: ratioR, remainR' (emd_fin2_kernel)
+  const size_t bm = (size_t)p.b * p.m, i = (size_t)bb * p.m + c;
+  const T r = s.remR[lvl & 1][i];
+  T sumr = sum_parts(s.part[1], p.S, bm, i);
+  sumr *= r;
+  const T cons = (T)fminf((float)(r / (sumr + (T)1e-9f)), 1.0f);
+  const T rat = cons * r;
+  if (store) {
+    s.levR[(size_t)lvl * bm + i] = rat;
+    s.remR[(lvl + 1) & 1][i] = (T)fmaxf(0.0f, (float)(r - sumr));
+  }
+  return rat;
+}
+
+template <typename T>
+__device__ void p_pass(const EmdPState<T>& s, const EmdPlan& p, int ph, int lvl, T* lcoef) {
+  const T level = (T)c_levels[lvl];
+  const bool rows_k = ph != 1;
+  const int nr = rows_k ? p.n : p.m, ncol = rows_k ? p.m : p.n;
+  const int tiles = rows_k ? p.tilesN : p.tilesM;
+  const T* rows = rows_k ? s.xyz1 : s.xyz2;
+  const T* cols = rows_k ? s.xyz2 : s.xyz1;
+  T* part = s.part[ph];
+  const int units = tiles * p.S * p.b;
+  for (int u = blockIdx.x; u < units; u += gridDim.x) {
+    const int tile = u % tiles;
+    const int sp = (u / tiles) % p.S;
+    const int bb = u / (tiles * p.S);
+    const int i = tile * kThreads + threadIdx.x;
+    const int ii = i < nr ? i : nr - 1;
+    const T* rp = rows + ((size_t)bb * nr + ii) * 3;
+    const T x1 = rp[0], y1 = rp[1], z1 = rp[2];
+    if (ph == 0 && lvl > 0 && sp == 0 && i < nr) {  // level lvl-1's fin3 for these rows
+      const size_t bn = (size_t)p.b * p.n, k = (size_t)bb * p.n + i;
+      s.remL[k] = (T)fmaxf(0.0f, (float)(s.remL[k] - sum_parts(s.part[2], p.S, bn, k)));
+      s.levL[(size_t)(lvl - 1) * bn + k] = s.ratL[k];
+    }
+    T rl = (T)0;
+    if (ph == 2) rl = s.ratL[(size_t)bb * p.n + ii];
+    const int c0 = (int)(((long long)ncol * sp) / p.S);
+    const int c1 = (int)(((long long)ncol * (sp + 1)) / p.S);
+    const T* __restrict__ cb = cols + (size_t)bb * ncol * 3;
+    T acc = 0;
+    for (int q0 = c0; q0 < c1; q0 += kPChunk) {
+      const int q1 = min(c1, q0 + kPChunk);
+      __syncthreads();  // the previous chunk / unit is done with lcoef
+      for (int c = q0 + (int)threadIdx.x; c < q1; c += kThreads)
+        lcoef[c - q0] = p_coef(s, p, ph, lvl, bb, c, tile == 0);
+      __syncthreads();
+#pragma unroll 4
+      for (int c = q0; c < q1; ++c) {
+        const T d2 = sqdist3(cb[3 * c] - x1, cb[3 * c + 1] - y1, cb[3 * c + 2] - z1);
+        const T e = emd_exp<T>(level * d2);
+        if (ph == 2) {
+          acc = fmaT<T>(e * rl, lcoef[c - q0], acc);
+        } else {
+          acc = fmaT<T>(e, lcoef[c - q0], acc);
+        }
+      }
+    }
+    if (i < nr) part[(size_t)sp * p.b * nr + (size_t)bb * nr + i] = acc;
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(kThreads)
+    emd_persistent_kernel(EmdPState<T> s, EmdPlan p) {
+  __shared__ T lcoef[kPChunk];
+  cooperative_groups::grid_group grid = cooperative_groups::this_grid();
+  const size_t bn = (size_t)p.b * p.n, bm = (size_t)p.b * p.m;
+  const size_t gtid = (size_t)blockIdx.x * kThreads + threadIdx.x;
+  const size_t gstride = (size_t)gridDim.x * kThreads;
+  for (size_t i = gtid; i < (bn > bm ? bn : bm); i += gstride) {  // emd_init_kernel
+    if (i < bn) s.remL[i] = s.multiL;
+    if (i < bm) s.remR[0][i] = s.multiR;
+  }
+  grid.sync();
+  for (int lvl = 0; lvl < kLevels; ++lvl) {
+    for (int ph = 0; ph < 3; ++ph) {
+      p_pass(s, p, ph, lvl, lcoef);
+      grid.sync();
+    }
+  }
+  for (size_t k = gtid; k < bn; k += gstride)  // the last level's fin3 (levL only)
+    s.levL[(size_t)(kLevels - 1) * bn + k] = s.ratL[k];
+  grid.sync();
+  // emd_match_kernel's units: (k tile, l group of kLPer, b)
+  const int lgroups = (p.m + kLPer - 1) / kLPer;
+  const int units = p.tilesN * lgroups * p.b;
+  for (int u = blockIdx.x; u < units; u += gridDim.x) {
+    const int tile = u % p.tilesN;
+    const int lg = (u / p.tilesN) % lgroups;
+    const int bb = u / (p.tilesN * lgroups);
+    const int k = tile * kThreads + threadIdx.x;
+    const int kk = k < p.n ? k : p.n - 1;
+    const T* p1 = s.xyz1 + ((size_t)bb * p.n + kk) * 3;
+    const T x1 = p1[0], y1 = p1[1], z1 = p1[2];
+    T rl[kLevels];
+#pragma unroll
+    for (int j = 0; j < kLevels; ++j) rl[j] = s.levL[(size_t)j * bn + (size_t)bb * p.n + kk];
+    const int l0 = lg * kLPer, l1 = min(p.m, l0 + kLPer);
+    for (int l = l0; l < l1; ++l) {
+      const T* p2 = s.xyz2 + ((size_t)bb * p.m + l) * 3;
+      const T d2 = sqdist3(p2[0] - x1, p2[1] - y1, p2[2] - z1);
+      T acc = 0;
+#pragma unroll
+      for (int j = 0; j < kLevels; ++j) {
+        const T rr = s.levR[(size_t)j * bm + (size_t)bb * p.m + l];
+        const T e = emd_exp<T>((T)c_levels[j] * d2);
+        acc += (e * rl[j]) * rr;
+      }
+      if (k < p.n) s.match[((size_t)bb * p.m + l) * p.n + k] = acc;
+    }
+  }
+}
+
+bool emd_persistent_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("PCFM_EMD_PERSISTENT");  // 0: the multi-launch form
+    return e == nullptr || std::atoi(e) != 0;
+  }();
+  return on;
+}
+
+template <typename T>
+int approxmatch_persistent(const T* xyz1, const T* xyz2, int b, int n, int m, T* match,
+                           EmdWs<T> w, int S, hipStream_t st, bool* launched) {
+  *launched = false;
+  const void* fn = (const void*)emd_persistent_kernel<T>;
+  int dev = 0, per_cu = 0, cus = 0, coop = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kThreads, 0) != hipSuccess ||
+      coop == 0 || per_cu <= 0) {
+    (void)hipGetLastError();
+    return PCFM_OK;  // caller runs the multi-launch form
+  }
+  EmdPlan p{b, n, m, S, ceil_div(n, kThreads), ceil_div(m, kThreads)};
+  const long long want = (long long)std::max(p.tilesN, p.tilesM) * S * b;
+  // at most what is co-resident (a grid barrier needs every block resident)
+  const int blocks = (int)std::max(1LL, std::min(want, (long long)per_cu * cus));
+  EmdPState<T> s;
+  s.xyz1 = xyz1;
+  s.xyz2 = xyz2;
+  s.remL = w.remL;
+  s.remR[0] = w.remR;
+  s.remR[1] = w.ratR;  // the multi-launch form's ratioR buffer: free here (ratR lives in LDS)
+  s.ratL = w.ratL;
+  s.levL = w.levL;
+  s.levR = w.levR;
+  const size_t pstride = (size_t)S * b * std::max(n, m);
+  s.part[0] = w.part;
+  s.part[1] = w.part + pstride;
+  s.part[2] = w.part + 2 * pstride;
+  s.match = match;
+  s.multiL = n >= m ? (T)1 : (T)(m / n);
+  s.multiR = n >= m ? (T)(n / m) : (T)1;
+  void* args[] = {&s, &p};
+  hipError_t e = hipLaunchCooperativeKernel(fn, dim3(blocks), dim3(kThreads), args, 0, st);
+  if (e != hipSuccess) {
+    set_error("approxmatch: hipLaunchCooperativeKernel: %s", hipGetErrorString(e));
+    return (int)e;
+  }
+  *launched = true;
+  return check_launch("approxmatch");
+}
+
 template <typename T>
 int approxmatch(const T* xyz1, const T* xyz2, int b, int n, int m, T* match, void* ws,
                 size_t ws_bytes, hipStream_t st) {
@@ -347,6 +568,11 @@ int approxmatch(const T* xyz1, const T* xyz2, int b, int n, int m, T* match, voi
   if (b == 0 || n == 0 || m == 0) return PCFM_OK;
   EmdWs<T> w = carve<T>(ws, b, n, m);
   const int S = emd_splits(b, n, m);
+  if (emd_persistent_enabled()) {
+    bool launched = false;
+    const int rc = approxmatch_persistent(xyz1, xyz2, b, n, m, match, w, S, st, &launched);
+    if (rc != PCFM_OK || launched) return rc;
+  }
   // multiL/multiR: integer ratio of the cloud sizes (:27-33)
   const T multiL = n >= m ? (T)1 : (T)(m / n);
   const T multiR = n >= m ? (T)(n / m) : (T)1;

@@ -419,3 +419,27 @@ def test_chamfer_c2_product_path(tmp_path, report):
     assert d["mismatches"] == {"d1": 0, "i1": 0, "d2": 0, "i2": 0}, d
     assert d["queries_checked"] == 8 * 2 * 400 and d["exact_hits"] >= 8 * 3000
     assert d["bwd_close"], d
+
+
+def test_emd_persistent_bit_identical(tmp_path, report):
+    """The one-launch cooperative approxmatch (grid barriers between the
+    levels' phases, finalizes folded into the consuming phase) against the
+    multi-launch form: bit-identical matches over f32/f64, n >< m and ragged
+    sizes (tests/helpers/emd_forms.py; emd_kernel.cu:24-156)."""
+    import json
+    import os
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    res = {}
+    for mode in ("0", "1"):
+        env = dict(os.environ, PCFM_EMD_PERSISTENT=mode)
+        subprocess.run([sys.executable, os.path.join(repo, "tests", "helpers", "emd_forms.py"),
+                        str(tmp_path / f"m{mode}.npz"), str(tmp_path / f"t{mode}.json")],
+                       check=True, timeout=120, env=env, cwd=repo)
+        res[mode] = json.load(open(tmp_path / f"t{mode}.json"))
+    a, b = np.load(tmp_path / "m0.npz"), np.load(tmp_path / "m1.npz")
+    for k in a.files:
+        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+    report("emd_persistent", {"multi_launch_ms": res["0"]["approxmatch_ms_b8_n2048"],
+                              "persistent_ms": res["1"]["approxmatch_ms_b8_n2048"]})
