@@ -8,6 +8,7 @@
 // C_out and N: the weight image is zero-padded to the tile grid and partial
 // point / channel tiles are masked.
 #include <algorithm>
+#include <cstdlib>
 
 #include "mfma_x3.hpp"
 
@@ -349,10 +350,14 @@ __global__ void __launch_bounds__(kSW * 64)
   constexpr int Kpad = 32 * NCH, ldr = Kpad + 8, cpr = Kpad / 8;
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  // blockIdx.y: the block's 128-row slice of the output channels (M > 128:
+  // every slice streams all point tiles; slices of a tile share its x reads
+  // in L2 -- blocks (x, y) and (x, y') sit on one XCD when gridDim.x % 8 == 0)
+  const int m0 = (int)blockIdx.y * 128;
   for (int e = t; e < 2 * 128 * cpr; e += kSW * 64) {  // weight image -> LDS, 16-B pieces
     const int img = e / (128 * cpr), rem = e - img * 128 * cpr;
     const int row = rem / cpr, pc = rem - row * cpr;
-    const uint16_t* src = (img ? wl : wh) + (size_t)row * Kpad + pc * 8;
+    const uint16_t* src = (img ? wl : wh) + (size_t)(m0 + row) * Kpad + pc * 8;
     *reinterpret_cast<uint4*>(sa + img * 128 * ldr + row * ldr + pc * 8) =
         *reinterpret_cast<const uint4*>(src);
   }
@@ -415,7 +420,7 @@ __global__ void __launch_bounds__(kSW * 64)
     const int bo = b * bias_bstride;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int mg = 32 * i;
+      const int mg = m0 + 32 * i;
       if (mg < M) {
         // a 32-row group lies in one output part
         float* __restrict__ yr = const_cast<float*>(uniform_ptr(y.row(b, mg, N)));
@@ -771,12 +776,21 @@ static int pw_gemm_launch(const Parts& x, const void* wsplit, const float* bias,
   const uint16_t* wh = (const uint16_t*)wsplit;
   const long long big = (long long)ceil_div(n, 128) * (Mpad / 128) * b;
 #ifndef PCFM_PW_NOSTREAM
-  if (Mpad == 128 && Kpad <= 256 && cin % 32 == 0 && cout % 32 == 0) {
+  // M > 128 in 128-row slices: opt-in (PCFM_PW_STREAM_M=1) until measured
+  static const bool stream_m = [] {
+    const char* e = getenv("PCFM_PW_STREAM_M");
+    return e != nullptr && e[0] == '1';
+  }();
+  if ((Mpad == 128 || (stream_m && Mpad % 128 == 0)) && Kpad <= 256 && cin % 32 == 0 &&
+      cout % 32 == 0) {
     const uint16_t* wl_img = wh + total;
     const long long tiles = (long long)b * ceil_div(n, 32);
     const size_t lds = (size_t)2 * 128 * (Kpad + 8) * sizeof(uint16_t);
     const int per_cu = lds <= 80 * 1024 ? 2 : 1;
-    const int grid = (int)std::max(1LL, std::min((tiles + kSW - 1) / kSW, (long long)kCUs * per_cu));
+    const int slices = Mpad / 128;
+    // the slices share the chip: grid.x a multiple of 8 (XCD pairing, see the kernel)
+    const long long cap = std::max(8LL, ((long long)kCUs * per_cu / slices) & ~7LL);
+    const int grid = (int)std::max(1LL, std::min((tiles + kSW - 1) / kSW, cap));
     const void* kfn = nullptr;
     switch (Kpad / 32) {
 #define PW_STREAM_CASE(NC) \
@@ -789,7 +803,7 @@ static int pw_gemm_launch(const Parts& x, const void* wsplit, const float* bias,
     if (e) return e;
     void* args[] = {(void*)&x, (void*)&wh, (void*)&wl_img, (void*)&bias, (void*)&bias_bstride,
                     (void*)&y, (void*)&cin, (void*)&cout, (void*)&n, (void*)&b};
-    const hipError_t le = hipLaunchKernel(kfn, dim3(grid), dim3(kSW * 64), args, lds, st);
+    const hipError_t le = hipLaunchKernel(kfn, dim3(grid, slices), dim3(kSW * 64), args, lds, st);
     if (le != hipSuccess) {
       set_error("pointwise_gemm: launch failed");
       return (int)le;

@@ -37,10 +37,29 @@ def main():
         feat = torch.randn(b, c, n, device="cuda", generator=g)
         grid = torch.randn(b, c, r ** 3, device="cuda", generator=g)
         _, inds, wgts = ops.trilinear_devoxelize_forward(r, True, nc, grid)
+        vplan = ops.avg_voxelize_plan(vc, r)
+        dplan = ops.trilinear_devoxelize_backward_plan(inds, wgts, r)
         res[f"C{c}R{r}"] = {
             "vox_fwd_ms": timeit(lambda: ops.avg_voxelize_forward(feat, vc, r)),
-            "devox_bwd_ms": timeit(lambda: ops.trilinear_devoxelize_backward(feat, inds, wgts, r))}
+            "devox_bwd_ms": timeit(lambda: ops.trilinear_devoxelize_backward(feat, inds, wgts, r)),
+            "vox_fwd_planned_ms": timeit(lambda: ops.avg_voxelize_forward_planned(feat, vplan)),
+            "devox_bwd_planned_ms": timeit(
+                lambda: ops.trilinear_devoxelize_backward_planned(feat, dplan))}
+        if os.environ.get("SCATTER_SAVE"):  # outputs for a bitwise comparison across variants
+            OUT[f"C{c}R{r}"] = (ops.avg_voxelize_forward_planned(feat, vplan).cpu(),
+                                ops.trilinear_devoxelize_backward_planned(feat, dplan).cpu())
+    if os.environ.get("SCATTER_SAVE"):
+        path = os.environ["SCATTER_SAVE"]
+        if os.path.exists(path):
+            ref = torch.load(path, weights_only=True)
+            res["bit_equal_to_saved"] = all(torch.equal(a, b) for k in OUT
+                                            for a, b in zip(OUT[k], ref[k]))
+        else:
+            torch.save(OUT, path)
     print(json.dumps(res), flush=True)
+
+
+OUT = {}
 
 
 if __name__ == "__main__":
