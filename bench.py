@@ -75,6 +75,10 @@ def measured_traffic(op, batch, points):
 KERNEL_PMC_FILE = os.path.join(REPO, "profiles", "r02_kernel_pmc.json")
 CONV_KERNEL = {"conv3d_fwd": "conv3_igemm_glds_kernel", "conv3d_bwd_data": "conv3_igemm_glds_kernel",
                "conv3d_wgrad": "conv3_wgrad3_kernel"}
+# launches that skip empty-voxel work (PVConv's first conv: chunk lists / tile
+# masks) are timed under "<op>_sparse" with the DENSE algorithmic FLOPs as their
+# amount, so they never stand for a roofline (their rate would overstate it)
+SPARSE_SUFFIX = "_sparse"
 
 
 def committed_mfma_busy(op):
@@ -316,8 +320,9 @@ def main():
         torch.cuda.synchronize(dev)
         ops.timer.enabled = False
         full = ops.timer.summary()
-        if full:
-            roof_ops.add(max(full, key=lambda k: full[k]["ms"]))
+        dense = [k for k in full if not k.endswith(SPARSE_SUFFIX)]
+        if dense:
+            roof_ops.add(max(dense, key=lambda k: full[k]["ms"]))
             hbm = [k for k in full if k in VOXEL_OPS]
             if hbm:
                 roof_ops.add(max(hbm, key=lambda k: full[k]["ms"]))
@@ -352,7 +357,9 @@ def main():
         rate_key = {"hbm": "GBps", "mfma": "TFLOPs_fp32_equiv", "mfma_bf16": "TFLOPs_bf16"}
         kernels = {k: {"launches_per_step": v["launches"] / prof_steps,
                        "ms_per_step": v["ms"] / prof_steps,
-                       rate_key[v["kind"]]:
+                       # sparse launches: the dense op's FLOPs / time (not a rate of work done)
+                       rate_key[v["kind"]] + ("_dense_equivalent" if k.endswith(SPARSE_SUFFIX)
+                                              else ""):
                        (v["amount"] / (v["ms"] * 1e-3) / (1e9 if v["kind"] == "hbm" else 1e12))
                        if v["ms"] > 0 else None}
                    for k, v in full.items()}
@@ -390,7 +397,8 @@ def main():
                     "algorithmic_flops_per_launch": d["amount"] / d["launches"],
                     "avg_launch_ms": d["ms"] / d["launches"]}
 
-        roofline = roof(max(summary, key=lambda k: summary[k]["ms"])) if summary else None
+        dense = [k for k in summary if not k.endswith(SPARSE_SUFFIX)]
+        roofline = roof(max(dense, key=lambda k: summary[k]["ms"])) if dense else None
         hbm_ops = [k for k in summary if k in VOXEL_OPS]
         roofline_scatter = roof(max(hbm_ops, key=lambda k: summary[k]["ms"])) if hbm_ops else None
         log(f"{ms:.2f} ms/step, {value / 1e6:.3f} M points/s; losses {loss_p:.4f} {loss_z:.4f}")

@@ -43,7 +43,7 @@ extern "C" {
  * pcfm_conv3d_igemm_cl; 10: fused AdamW + clip + EMA parameter update; 11: segment
  * plans shared by scatters over the same points; 12: the BatchNorm forward entry
  * points take the module's num_batches_tracked counter; 13: occupancy-masked
- * voxel convolution entry points). */
+ * voxel convolution entry points; 14: voxel-list form of the voxel convolution). */
 int pcfm_abi_version(void);
 /* Thread-local text of the last non-zero return code. */
 const char* pcfm_last_error(void);
@@ -271,6 +271,25 @@ int pcfm_conv3d_occupancy(const int* cnt, int b, int r, unsigned* masks, void* s
 int pcfm_conv3d_igemm_cl_occ(const void* xs, const void* wsplit, const float* bias, int b,
                              int cin, int cout, int r, const unsigned* masks, int mode, float* y,
                              void* ws, size_t ws_bytes, void* stream);
+/* Chunk lists of a voxelized grid (the same counts cnt i32 [b][r^3]; a chunk =
+ * 32 consecutive voxels): list 0 = the chunks holding an occupied voxel, list 1
+ * = the chunks holding a voxel with an occupied voxel in its 3x3x3
+ * neighbourhood; entries are chunk indices (b r^3 + v) / 32, ascending, and
+ * the device-side counts lead the buffer (pcfm_conv3d_vlist_bytes; 0 =
+ * unsupported: r^3 % 256 != 0 or b r^3 >= 2^31). */
+size_t pcfm_conv3d_vlist_bytes(int b, int r);
+int pcfm_conv3d_vlist(const int* cnt, int b, int r, int* lists, void* stream);
+/* pcfm_conv3d_igemm_cl computed in the chunks of list `which` only (its GEMM
+ * tiles are 8 listed chunks, their B rows the chunks' neighbours): which 1
+ * (forward over a voxelized input x: elsewhere the output is exactly the bias,
+ * written as such -- bit-identical to pcfm_conv3d_igemm_cl everywhere), which 0
+ * (backward-data into a voxelized grid, bias NULL: equal to
+ * pcfm_conv3d_igemm_cl at every occupied voxel, 0 in the unlisted chunks).  Shapes without
+ * the list form (split-K grids, r = 8 at the C2 sizes) run the dense GEMM.
+ * Fully writes y; same workspace as pcfm_conv3d_igemm_cl. */
+int pcfm_conv3d_igemm_cl_list(const void* xs, const void* wsplit, const float* bias, int b,
+                              int cin, int cout, int r, const int* cnt, const int* lists,
+                              int which, float* y, void* ws, size_t ws_bytes, void* stream);
 /* pcfm_conv3d_wgrad_cl with x a voxelized grid: steps whose X rows are all
  * empty voxels are skipped (bit-identical to pcfm_conv3d_wgrad_cl); workspace
  * pcfm_conv3d_wgrad_occ_workspace_bytes (adds the per-split chunk lists). */

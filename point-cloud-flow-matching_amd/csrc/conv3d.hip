@@ -21,6 +21,7 @@
 // LDS as bf16 hi/lo rows; D[m][voxel] leaves with lanes along voxels, i.e.
 // coalesced into the NCDHW output.  Out-of-grid neighbours read as 0 (padding).
 #include <algorithm>
+#include <cstdlib>
 #include <mutex>
 
 #include "mfma_x3.hpp"
@@ -94,6 +95,144 @@ __global__ void __launch_bounds__(256)
   atomicOr(&sm, taps);
   __syncthreads();
   if (t == 0) tmask[(size_t)b * (V / 256) + blockIdx.x] = sm;
+}
+
+// ---------------------------------------------------------------------------
+// Chunk lists of a voxelized grid (from the voxelization's counts), for the
+// list form of the LDS-DMA GEMM.  A chunk is 32 consecutive voxels (a z-row at
+// r = 32): list 0 = the chunks holding an occupied voxel (cnt > 0: where
+// PVConv's first convolution's input gradient is read back, vox.cu:86-110),
+// list 1 = the chunks holding a voxel with an occupied voxel in its 3x3x3
+// neighbourhood (outside them that convolution's forward output is exactly
+// its bias: its input is 0 there).  Whole chunks keep the GEMM's B-row fetches
+// and output stores 128-B runs (voxel-granular lists measured slower: short
+// scattered runs).  Entries are global chunk indices (b V + v) / 32, ascending
+// (deterministic).  Buffer: int32 counts[2] | pad to 64 | per-tile counts /
+// offsets [2][tiles] | list 0 [B V / 32] | list 1 [B V / 32].
+// ---------------------------------------------------------------------------
+constexpr int kChunk = 32;
+
+__device__ __forceinline__ void vlist_flags(const int* __restrict__ c, int v, int R, bool& occ,
+                                            bool& act) {
+  const int R2 = R * R;
+  const int x = v / R2, y = (v / R) % R, z = v % R;
+  occ = c[v] > 0;
+  act = false;
+#pragma unroll
+  for (int tap = 0; tap < 27; ++tap) {
+    const int xx = x + tap / 9 - 1, yy = y + (tap / 3) % 3 - 1, zz = z + tap % 3 - 1;
+    act = act || ((unsigned)xx < (unsigned)R && (unsigned)yy < (unsigned)R &&
+                  (unsigned)zz < (unsigned)R && c[xx * R2 + yy * R + zz] > 0);
+  }
+}
+
+// chunk flags of this thread's chunk (32 consecutive lanes = one chunk)
+__device__ __forceinline__ void chunk_flags(const int* __restrict__ cnt, long long g, int R,
+                                            bool& occ, bool& act) {
+  const int V = R * R * R;
+  bool o, a;
+  vlist_flags(cnt + (g / V) * V, (int)(g % V), R, o, a);
+  const int sh = threadIdx.x & 32;
+  occ = ((__ballot(o) >> sh) & 0xFFFFFFFFull) != 0ull;
+  act = ((__ballot(a) >> sh) & 0xFFFFFFFFull) != 0ull;
+}
+
+// grid = B V / 256 tiles (8 chunks each), 256 threads: per-tile chunk counts
+__global__ void __launch_bounds__(256)
+    conv3_vlist_count_kernel(const int* __restrict__ cnt, int R, int tiles,
+                             int* __restrict__ tcount) {
+  __shared__ int ws[2][8];
+  const int t = threadIdx.x;
+  bool occ, act;
+  chunk_flags(cnt, (long long)blockIdx.x * 256 + t, R, occ, act);
+  if ((t & 31) == 0) {
+    ws[0][t >> 5] = occ ? 1 : 0;
+    ws[1][t >> 5] = act ? 1 : 0;
+  }
+  __syncthreads();
+  if (t < 2) {
+    int n = 0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) n += ws[t][q];
+    tcount[t * tiles + blockIdx.x] = n;
+  }
+}
+
+// one block: exclusive scans of the two per-tile count rows (in place) and
+// the totals
+__global__ void __launch_bounds__(1024)
+    conv3_vlist_scan_kernel(int* __restrict__ tcount, int tiles, int* __restrict__ counts) {
+  __shared__ int wsum[16];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  for (int k = 0; k < 2; ++k) {
+    int* row = tcount + (size_t)k * tiles;
+    int carry = 0;
+    for (int t0 = 0; t0 < tiles; t0 += 1024) {
+      const int i = t0 + t;
+      const int c = i < tiles ? row[i] : 0;
+      int x = c;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+      }
+      if (lane == 63) wsum[w] = x;
+      __syncthreads();
+      int ofs = carry, total = 0;
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        ofs += g < w ? wsum[g] : 0;
+        total += wsum[g];
+      }
+      if (i < tiles) row[i] = ofs + x - c;
+      carry += total;
+      __syncthreads();
+    }
+    if (t == 0) counts[k] = carry;
+  }
+}
+
+// grid = tiles, 256 threads: each tile writes its listed chunks at its offsets
+__global__ void __launch_bounds__(256)
+    conv3_vlist_write_kernel(const int* __restrict__ cnt, int R, int tiles,
+                             const int* __restrict__ toff, int* __restrict__ list0,
+                             int* __restrict__ list1) {
+  __shared__ int ws[2][8];
+  const int t = threadIdx.x;
+  bool occ, act;
+  chunk_flags(cnt, (long long)blockIdx.x * 256 + t, R, occ, act);
+  if ((t & 31) == 0) {
+    ws[0][t >> 5] = occ ? 1 : 0;
+    ws[1][t >> 5] = act ? 1 : 0;
+  }
+  __syncthreads();
+  if ((t & 31) == 0) {
+    const int q = t >> 5, chunk = blockIdx.x * 8 + q;
+    int p0 = toff[blockIdx.x], p1 = toff[tiles + blockIdx.x];
+    for (int u = 0; u < q; ++u) {
+      p0 += ws[0][u];
+      p1 += ws[1][u];
+    }
+    if (occ) list0[p0] = chunk;
+    if (act) list1[p1] = chunk;
+  }
+}
+
+// y[b][m][v] = value (bias[m], or 0 without bias) in the chunks NOT in list
+// `which` -- the complement the list form of the GEMM does not write.
+// grid = B V / 256, 256 threads.
+__global__ void __launch_bounds__(256)
+    conv3_fill_unlisted_kernel(const int* __restrict__ cnt, int R, int M, int which,
+                               const float* __restrict__ bias, float* __restrict__ y) {
+  const int V = R * R * R;
+  const long long g = (long long)blockIdx.x * 256 + threadIdx.x;
+  bool occ, act;
+  chunk_flags(cnt, g, R, occ, act);
+  if (which == 0 ? occ : act) return;
+  const int b = (int)(g / V), v = (int)(g % V);
+  float* __restrict__ yb = y + (size_t)b * M * V + v;
+  for (int m = 0; m < M; ++m)
+    __builtin_nontemporal_store(bias != nullptr ? bias[m] : 0.0f, yb + (size_t)m * V);
 }
 
 // ---------------------------------------------------------------------------
@@ -425,19 +564,36 @@ __global__ void __launch_bounds__(GN * 2)  // GK<KT, GN>::NW = GN / 32 waves
                             const uint16_t* __restrict__ zrow, const float* __restrict__ bias,
                             float* __restrict__ y, int K, int M, int R, int S,
                             float* __restrict__ part, const uint32_t* __restrict__ tmask,
-                            int mmode) {
+                            int mmode, const int* __restrict__ vlist = nullptr,
+                            const int* __restrict__ vcount = nullptr) {
   using G = GK<KT, GN>;
   __shared__ __attribute__((aligned(16))) uint8_t lds[NST * G::STAGE];
   const int V = R * R * R, R2 = R * R;
-  int id = (int)blockIdx.x;
+  const int nmt = M / kGM, nvt = V / GN;
+  // Chunk-list form (S == 1, conv3_vlist_*): the block's GN output voxels are
+  // the CPT listed 32-voxel chunks [lt CPT, lt CPT + CPT) -- global chunk
+  // indices (b V + v) / 32 whose result is wanted, ascending -- instead of a
+  // contiguous range; the B rows of every tap are their neighbours (a padding
+  // entry reads zero rows and stores nothing).  Only the first nmt x
+  // ceil(count / CPT) blocks (device-side count) work, dealt to the XCDs as
+  // the dense grid is; the rest leave at once, before any barrier.
+  const bool lmode = vlist != nullptr;
+  constexpr int CPT = GN / kChunk;
+  int lcount = 0;
+  int nwg = (int)gridDim.x, id = (int)blockIdx.x;
+  if (lmode) {
+    lcount = __builtin_amdgcn_readfirstlane(vcount[0]);
+    nwg = nmt * ((lcount + CPT - 1) / CPT);
+    if (id >= nwg) return;
+  }
   {
-    const int nwg = (int)gridDim.x, q = nwg / 8, rr = nwg % 8, xcd = id % 8;
+    const int q = nwg / 8, rr = nwg % 8, xcd = id % 8;
     id = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + id / 8;
   }
-  const int nmt = M / kGM, nvt = V / GN;
   const int nb = (int)gridDim.x / (S * nmt * nvt);  // batch elements
   const int m0 = (id % nmt) * kGM;
   id /= nmt;
+  const int lt = id;  // list tile (list form)
   const int v0 = (id % nvt) * GN;
   id /= nvt;
   const int b = id % nb, sp = id / nb;
@@ -452,7 +608,7 @@ __global__ void __launch_bounds__(GN * 2)  // GK<KT, GN>::NW = GN / 32 waves
   // voxel (the gradient is read back there only); the others are written 0.
   const uint32_t kAll = 0x7FFFFFFu;
   uint32_t mask = kAll;
-  if (mmode != 0) {
+  if (mmode != 0 && !lmode) {
     const uint32_t mm = __builtin_amdgcn_readfirstlane(tmask[(size_t)b * (V >> 8) + (v0 >> 8)]);
     mask = mmode == 1 ? (mm & kAll) : ((mm >> 31) ? kAll : 0u);
   }
@@ -489,11 +645,17 @@ __global__ void __launch_bounds__(GN * 2)  // GK<KT, GN>::NW = GN / 32 waves
   for (int q = 0; q < G::BPW; ++q) {
     const int I = G::BPW * w + q;
     const int row = (I % G::BPI) * G::RPP + prow;
-    const int v = v0 + row;
+    long long gv = (long long)bV + v0 + row;  // global row b V + v, -1: padding
+    if (lmode) {
+      const int e = lt * CPT + row / kChunk;
+      gv = e < lcount ? (long long)vlist[e] * kChunk + row % kChunk : -1;
+    }
+    const int v = gv >= 0 ? (int)(gv % V) : 0;
     const int cofs = (pch ^ G::swz(row)) << 3;
-    bbase[q] = ((I / G::BPI) ? xl : xh) + (bV + v) * 2 * K + cofs;
+    bbase[q] = ((I / G::BPI) ? xl : xh) + (size_t)(gv >= 0 ? gv : 0) * 2 * K + cofs;
     zbase[q] = zrow + cofs;
-    bxyz[q] = (v / R2) | (((v / R) % R) << 10) | ((v % R) << 20);
+    // x = 1023 for padding: every tap's neighbour is out of the volume
+    bxyz[q] = gv >= 0 ? (v / R2) | (((v / R) % R) << 10) | ((v % R) << 20) : 1023;
   }
 
   auto issue = [&](int sl, int buf) {
@@ -697,6 +859,19 @@ __global__ void __launch_bounds__(GN * 2)  // GK<KT, GN>::NW = GN / 32 waves
   float biasv[2][16];
 #pragma unroll
   for (int i = 0; i < 2; ++i) load_bias16(S == 1 ? bias : nullptr, m0 + wr * 64 + i * 32, h, M, biasv[i]);
+  // this lane's output column per j: dense y[b][m][v0 + col], list y[g / V][m][g % V]
+  float* ycol[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int col = wc * 64 + j * 32 + r;
+    if (lmode) {
+      const int e = lt * CPT + col / kChunk;
+      const long long g = e < lcount ? (long long)vlist[e] * kChunk + col % kChunk : -1;
+      ycol[j] = g >= 0 ? y + (size_t)(g / V) * M * V + (size_t)(g % V) : nullptr;
+    } else {
+      ycol[j] = yb + v0 + col;
+    }
+  }
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -704,12 +879,13 @@ __global__ void __launch_bounds__(GN * 2)  // GK<KT, GN>::NW = GN / 32 waves
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
         const int m = m0 + wr * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
-        const int v = v0 + wc * 64 + j * 32 + r;
+        if (ycol[j] != nullptr) {
 #ifndef PCFM_CONV_CACHED_STORE  // streamed: same-box bench 33.70 -> 33.57 ms/step
-        __builtin_nontemporal_store(acc[i][j][e] + biasv[i][e], yb + (size_t)m * V + v);
+          __builtin_nontemporal_store(acc[i][j][e] + biasv[i][e], ycol[j] + (size_t)m * V);
 #else
-        yb[(size_t)m * V + v] = acc[i][j][e] + biasv[i][e];
+          ycol[j][(size_t)m * V] = acc[i][j][e] + biasv[i][e];
 #endif
+        }
       }
 }
 
@@ -1786,9 +1962,21 @@ static bool conv_brick() {
   return on;
 }
 
+static bool list_gn128(long long blocks256) {
+  static const int mode = [] {
+    const char* e = getenv("PCFM_CONV_LIST_GN");
+    // default 256: the 128-entry tiles measured equal (32.24 vs 32.20 ms/step)
+    if (e == nullptr) return 0;
+    if (e[0] == 'a') return 2;  // auto
+    return atoi(e) == 128 ? 1 : 0;
+  }();
+  return mode == 1 || (mode == 2 && blocks256 <= 2LL * kCUs);
+}
+
 static int igemm_cl(const void* xs, const void* wsplit, const float* bias, int b, int cin,
                     int cout, int r, float* y, void* ws, size_t ws_bytes, void* stream,
-                    const uint32_t* tmask, int mmode) {
+                    const uint32_t* tmask, int mmode, const int* vlist = nullptr,
+                    const int* vcount = nullptr) {
   PCFM_CHECK_ARG(conv3_shape_ok(b, cin, cout, r),
                  "conv3d_igemm_cl: unsupported shape b=%d cin=%d cout=%d r=%d", b, cin, cout, r);
   if (b == 0) return PCFM_OK;
@@ -1827,7 +2015,22 @@ static int igemm_cl(const void* xs, const void* wsplit, const float* bias, int b
     // tile masks apply to unsplit launches only (a split's K range is a fixed
     // share of all 27 taps)
     const int mm = S == 1 && tmask != nullptr ? mmode : 0;
-    if (S == 1 && mm == 0 && cin % 16 == 0 && (r == 32 || r == 16) && conv_brick()) {
+    const int* vl = S == 1 ? vlist : nullptr;  // the list form is unsplit
+    const int* vc = S == 1 ? vcount : nullptr;
+    // list form on grids that fill the chip only once with 256-voxel tiles
+    // (r = 16 at B = 8: 256 blocks): 128-entry tiles, two 4-wave blocks per
+    // CU, so a half-empty list still keeps every CU busy (opt-in,
+    // PCFM_CONV_LIST_GN: 256 = never (default), 128 = always, auto)
+    if (vl != nullptr && PCFM_CONV_GK == 32 && cin % 32 == 0 &&
+        list_gn128(glds_blocks)) {
+      const long long blocks128 = (long long)(V / 128) * (cout / kGM) * b;
+      hipLaunchKernelGGL((conv3_igemm_glds_kernel<32, 128, 2>), dim3((unsigned)blocks128),
+                         dim3(256), 0, st, xh, xl, wh, wh + kSplitLo, zrow, bias, y, cin, cout, r, 1,
+                         part, tmask, 0, vl, vc);
+      return check_launch("conv3d_igemm_cl");
+    }
+    if (S == 1 && mm == 0 && vl == nullptr && cin % 16 == 0 && (r == 32 || r == 16) &&
+        conv_brick()) {
       const int e = r == 32 ? allow_big_lds((const void*)conv3_igemm_brick_kernel<32>)
                             : allow_big_lds((const void*)conv3_igemm_brick_kernel<16>);
       if (e) return e;
@@ -1839,7 +2042,7 @@ static int igemm_cl(const void* xs, const void* wsplit, const float* bias, int b
                            BrickGeo<16>::LDS, st, xh, wh, zrow, bias, y, cin, cout);
       return check_launch("conv3d_igemm_cl");
     }
-    if (S == 1 && PCFM_CONV_GK == 32 && cin % 32 == 0 && conv_pp()) {
+    if (S == 1 && PCFM_CONV_GK == 32 && cin % 32 == 0 && vl == nullptr && conv_pp()) {
       hipLaunchKernelGGL(conv3_igemm_pp_kernel<32>, dim3((unsigned)glds_blocks), dim3(512), 0, st,
                          xh, xl, wh, wh + kSplitLo, zrow, bias, y, cin, cout, r, tmask, mm);
       return check_launch("conv3d_igemm_cl");
@@ -1847,11 +2050,11 @@ static int igemm_cl(const void* xs, const void* wsplit, const float* bias, int b
     if (PCFM_CONV_GK == 16 || cin % 32 != 0)
       hipLaunchKernelGGL(conv3_igemm_glds_kernel<16>, dim3((unsigned)glds_blocks), dim3(512), 0,
                          st, xh, xl, wh, wh + kSplitLo, zrow, bias, y, cin, cout, r, S, part, tmask,
-                         mm);
+                         mm, vl, vc);
     else
       hipLaunchKernelGGL(conv3_igemm_glds_kernel<32>, dim3((unsigned)glds_blocks), dim3(512), 0,
                          st, xh, xl, wh, wh + kSplitLo, zrow, bias, y, cin, cout, r, S, part, tmask,
-                         mm);
+                         mm, vl, vc);
     if (S > 1) {
       const long long total4 = (long long)b * cout * V / 4;
       hipLaunchKernelGGL(conv3_ksum_kernel, dim3((unsigned)ceil_div(total4, 256)), dim3(256), 0,
@@ -1912,6 +2115,56 @@ extern "C" int pcfm_conv3d_occupancy(const int* cnt, int b, int r, unsigned* mas
   hipLaunchKernelGGL(conv3_occupancy_kernel, dim3(V / 256, b), dim3(256), 0, (hipStream_t)stream,
                      cnt, r, (uint32_t*)masks, (uint32_t*)masks + (size_t)b * (V / 256));
   return check_launch("conv3d_occupancy");
+}
+
+extern "C" size_t pcfm_conv3d_vlist_bytes(int b, int r) {
+  const long long v = (long long)r * r * r;
+  if (b <= 0 || r <= 0 || v % 256 != 0 || (long long)b * v >= (1LL << 31)) return 0;
+  const long long tiles = (long long)b * v / 256;
+  return (size_t)(64 + 2 * tiles + 2 * (long long)b * v / kChunk) * sizeof(int);
+}
+
+extern "C" int pcfm_conv3d_vlist(const int* cnt, int b, int r, int* lists, void* stream) {
+  PCFM_CHECK_ARG(pcfm_conv3d_vlist_bytes(b, r) > 0,
+                 "conv3d_vlist: bad shape b=%d r=%d (r^3 %% 256 == 0, b r^3 < 2^31)", b, r);
+  const int V = r * r * r, tiles = b * (V / 256);
+  hipStream_t st = (hipStream_t)stream;
+  int* tc = lists + 64;
+  int* l0 = tc + 2 * tiles;
+  hipLaunchKernelGGL(conv3_vlist_count_kernel, dim3(tiles), dim3(256), 0, st, cnt, r, tiles, tc);
+  hipLaunchKernelGGL(conv3_vlist_scan_kernel, dim3(1), dim3(1024), 0, st, tc, tiles, lists);
+  hipLaunchKernelGGL(conv3_vlist_write_kernel, dim3(tiles), dim3(256), 0, st, cnt, r, tiles, tc,
+                     l0, l0 + (size_t)b * V / kChunk);
+  return check_launch("conv3d_vlist");
+}
+
+extern "C" int pcfm_conv3d_igemm_cl_list(const void* xs, const void* wsplit, const float* bias,
+                                         int b, int cin, int cout, int r, const int* cnt,
+                                         const int* lists, int which, float* y, void* ws,
+                                         size_t ws_bytes, void* stream) {
+  PCFM_CHECK_ARG(cnt != nullptr && lists != nullptr && (which == 0 || which == 1) &&
+                     pcfm_conv3d_vlist_bytes(b, r) > 0,
+                 "conv3d_igemm_cl_list: need counts, lists, which 0 / 1 and r^3 %% 256 == 0 "
+                 "(which=%d b=%d r=%d)", which, b, r);
+  PCFM_CHECK_ARG(conv3_shape_ok(b, cin, cout, r),
+                 "conv3d_igemm_cl_list: unsupported shape b=%d cin=%d cout=%d r=%d", b, cin, cout,
+                 r);
+  const int V = r * r * r, tiles = b * (V / 256);
+  const int* l = lists + 64 + 2 * tiles + (size_t)which * b * V / kChunk;
+#ifndef PCFM_CONV_NOGLDS
+  const bool listed = glds_ok(cout, r) && glds_splits(b, cin, cout, r) == 1;
+#else
+  const bool listed = false;
+#endif
+  if (!listed)  // no list form for this shape: the dense GEMM (every voxel)
+    return igemm_cl(xs, wsplit, bias, b, cin, cout, r, y, ws, ws_bytes, stream, nullptr, 0);
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(conv3_fill_unlisted_kernel, dim3(tiles), dim3(256), 0, st, cnt, r, cout,
+                     which, bias, y);
+  const int e = check_launch("conv3d_igemm_cl_list");
+  if (e) return e;
+  return igemm_cl(xs, wsplit, bias, b, cin, cout, r, y, ws, ws_bytes, stream, nullptr, 0, l,
+                  lists + which);
 }
 
 static int wgrad_cap(int b, int r, int S) {

@@ -122,11 +122,13 @@ class _Conv3dBnActPair(torch.autograd.Function):
     grad (bn_act_backward_split): no fp32 pass over either.
 
     `occ` (PVConv, x = the voxelization's grid: pcfm.plans.conv_occupancy)
-    skips Conv1's exact-zero work -- forward taps and weight-gradient steps
-    that read only empty voxels (bit-identical) -- and computes Conv1's input
-    gradient only in voxel tiles that hold an occupied voxel (the voxelization's
-    backward reads it there only, vox.cu:86-110); the returned dx is 0 in the
-    other tiles."""
+    skips Conv1's exact-zero work: its forward is computed at the voxels with
+    an occupied voxel in their 3x3x3 neighbourhood only (elsewhere the output
+    is exactly the bias; with voxel lists, else per tile and tap), its weight
+    gradient skips steps that read only empty voxels (bit-identical), and its
+    input gradient is computed at the occupied voxels only (the voxelization's
+    backward reads it there only, vox.cu:86-110; the returned dx is 0 at the
+    other voxels, or in the other tiles without lists)."""
 
     @staticmethod
     def forward(ctx, x, w1, b1, g1, bt1, rm1, rv1, nbt1, w2, b2, g2, bt2, rm2, rv2, nbt2, eps1,
@@ -135,8 +137,9 @@ class _Conv3dBnActPair(torch.autograd.Function):
         bsz, cin, r = x.shape[0], x.shape[1], x.shape[2]
         cmid, cout = w1.shape[0], w2.shape[0]
         xs = ops.conv3d_split(x)
+        masks, vl, cnt = (occ.masks, occ.lists, occ.cnt) if occ is not None else (None, None, None)
         y1 = ops.conv3d_igemm_split(xs, ops.conv3d_prep_weight(w1, False), b1, bsz, cin, cmid,
-                                    r, "conv3d_fwd", occ=occ, occ_mode=1)
+                                    r, "conv3d_fwd", occ=masks, occ_mode=1, vlists=vl, cnt=cnt)
         z1s, m1, is1 = ops.bn_act_forward_split(y1, g1, bt1, eps1, slope1, mom1, rm1, rv1, nbt1)
         y2 = ops.conv3d_igemm_split(z1s, ops.conv3d_prep_weight(w2, False), b2, bsz, cmid, cout,
                                     r, "conv3d_fwd")
@@ -166,10 +169,12 @@ class _Conv3dBnActPair(torch.autograd.Function):
         del dz1
         dx = None
         occ = ctx.occ
+        masks, vl, cnt = (occ.masks, occ.lists, occ.cnt) if occ is not None else (None, None, None)
         if ctx.needs_input_grad[0]:
             dx = ops.conv3d_igemm_split(gys1, ops.conv3d_prep_weight(w1, True), None, bsz, cmid,
-                                        cin, r, "conv3d_bwd_data", occ=occ, occ_mode=2)
-        dw1 = ops.conv3d_wgrad_split(xs, gys1, bsz, cin, cmid, r, occ=occ)
+                                        cin, r, "conv3d_bwd_data", occ=masks, occ_mode=2,
+                                        vlists=vl, cnt=cnt)
+        dw1 = ops.conv3d_wgrad_split(xs, gys1, bsz, cin, cmid, r, occ=masks)
         return (dx, dw1, db1, dg1, dbt1, None, None, None, dw2, db2, dg2, dbt2, None, None,
                 None, None, None, None, None, None, None, None)
 

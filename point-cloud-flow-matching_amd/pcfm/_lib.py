@@ -61,6 +61,9 @@ SIGNATURES = {
     "pcfm_conv3d_occupancy_bytes": (_Z, [_I, _I]),
     "pcfm_conv3d_occupancy": (_I, [_P, _I, _I, _P, _P]),
     "pcfm_conv3d_igemm_cl_occ": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _I, _P, _P, _Z, _P]),
+    "pcfm_conv3d_vlist_bytes": (_Z, [_I, _I]),
+    "pcfm_conv3d_vlist": (_I, [_P, _I, _I, _P, _P]),
+    "pcfm_conv3d_igemm_cl_list": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P, _I, _P, _P, _Z, _P]),
     "pcfm_conv3d_wgrad_occ_workspace_bytes": (_Z, [_I, _I, _I, _I]),
     "pcfm_conv3d_wgrad_cl_occ": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, _P, _Z, _P]),
     "pcfm_conv3d_wgrad_workspace_bytes": (_Z, [_I, _I, _I, _I]),
@@ -121,7 +124,7 @@ SIGNATURES = {
     "pcfm_adamw_ema_step": (_I, [_P, _P, _I, _P, _P, _I, _DP, _DP, _D, _D, _D, _D, _P]),
 }
 
-ABI_VERSION = 13
+ABI_VERSION = 14
 
 _lock = threading.Lock()
 _lib = None

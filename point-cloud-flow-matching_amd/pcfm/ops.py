@@ -699,17 +699,41 @@ def conv3d_occupancy(cnt: torch.Tensor, r: int):
     return masks
 
 
+def conv3d_vlists(cnt: torch.Tensor, r: int):
+    """Voxel lists of a voxelized grid from the voxelization's counts cnt (b, r^3)
+    int32 (pcfm_conv3d_vlist: occupied voxels, and voxels with an occupied
+    neighbour), or None where r^3 % 256 != 0."""
+    _check(cnt, "cnt", "i")
+    b = cnt.shape[0]
+    n = _lib.query("pcfm_conv3d_vlist_bytes", b, int(r))
+    if n == 0:
+        return None
+    lists = torch.empty(n // 4, dtype=torch.int32, device=cnt.device)
+    _lib.call("pcfm_conv3d_vlist", _ptr(cnt), b, int(r), _ptr(lists), _stream(cnt))
+    return lists
+
+
 def conv3d_igemm_split(xs: torch.Tensor, img: torch.Tensor, bias, b: int, cin: int, cout: int,
-                       r: int, op: str, occ=None, occ_mode: int = 0) -> torch.Tensor:
+                       r: int, op: str, occ=None, occ_mode: int = 0, vlists=None,
+                       cnt=None) -> torch.Tensor:
     """y (b, cout, r, r, r) from a split input (forward, or backward-data with the
     transposed weight image).  occ (conv3d_occupancy of the voxelized input /
     gradient target) with occ_mode 1 (forward) / 2 (backward-data) skips the
-    exact-zero / unread work (pcfm_conv3d_igemm_cl_occ)."""
+    exact-zero / unread work (pcfm_conv3d_igemm_cl_occ); with the grid's voxel
+    lists (conv3d_vlists) and counts the GEMM runs at the listed voxels only
+    (pcfm_conv3d_igemm_cl_list: mode 1 -> the neighbourhood-occupied voxels,
+    bias elsewhere; mode 2 -> the occupied voxels, 0 elsewhere)."""
     y = torch.empty((b, cout, r, r, r), dtype=torch.float32, device=xs.device)
     bias_p = _ptr(bias.contiguous()) if bias is not None else None
     ws = _workspace(_lib.query("pcfm_conv3d_igemm_cl_workspace_bytes", b, cin, cout, r), xs)
+    if occ_mode and (occ is not None or vlists is not None):
+        op = op + "_sparse"  # skips work: timed apart from the dense launches (roofline)
     with _timed(op, 54 * b * r ** 3 * cin * cout, xs, "mfma"):
-        if occ is not None and occ_mode:
+        if vlists is not None and cnt is not None and occ_mode in (1, 2):
+            _lib.call("pcfm_conv3d_igemm_cl_list", _ptr(xs), _ptr(img), bias_p, b, cin, cout, r,
+                      _ptr(cnt), _ptr(vlists), 1 if occ_mode == 1 else 0, _ptr(y), _ptr(ws),
+                      ws.numel(), _stream(xs))
+        elif occ is not None and occ_mode:
             _lib.call("pcfm_conv3d_igemm_cl_occ", _ptr(xs), _ptr(img), bias_p, b, cin, cout, r,
                       _ptr(occ), int(occ_mode), _ptr(y), _ptr(ws), ws.numel(), _stream(xs))
         else:
@@ -726,7 +750,8 @@ def conv3d_wgrad_split(xs: torch.Tensor, gys: torch.Tensor, b: int, cin: int, co
         "pcfm_conv3d_wgrad_workspace_bytes"
     ws = _workspace(_lib.query(q, b, cin, cout, r), xs)
     dw = torch.empty((cout, cin, 3, 3, 3), dtype=torch.float32, device=xs.device)
-    with _timed("conv3d_wgrad", 54 * b * r ** 3 * cin * cout, xs, "mfma"):
+    with _timed("conv3d_wgrad_sparse" if occ is not None else "conv3d_wgrad",
+                54 * b * r ** 3 * cin * cout, xs, "mfma"):
         if occ is not None:
             _lib.call("pcfm_conv3d_wgrad_cl_occ", _ptr(xs), _ptr(gys), b, cin, cout, r, _ptr(occ),
                       _ptr(dw), _ptr(ws), ws.numel(), _stream(xs))

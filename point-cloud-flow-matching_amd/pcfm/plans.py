@@ -20,12 +20,24 @@ from __future__ import annotations
 
 import os
 import weakref
+from typing import NamedTuple, Optional
 
 import torch
 
 ENABLED = os.environ.get("PCFM_SHARE_PLANS", "1") != "0"
 # occupancy-masked first voxel convolution of PVConv (measurement switch)
 OCCUPANCY = os.environ.get("PCFM_CONV_OCC", "1") != "0"
+# ... computed at voxel granularity through voxel lists (measurement switch)
+VOXEL_LISTS = os.environ.get("PCFM_CONV_VLIST", "1") != "0"
+
+
+class Occupancy(NamedTuple):
+    """What PVConv's first convolution may skip, from the voxelization's counts:
+    tile masks (ops.conv3d_occupancy), voxel lists (ops.conv3d_vlists; None when
+    off) and the counts themselves."""
+    masks: torch.Tensor
+    lists: Optional[torch.Tensor]
+    cnt: torch.Tensor
 
 
 class IdentityCache:
@@ -88,9 +100,9 @@ def voxel_plan(vox_coords: torch.Tensor, r: int):
     return _cache.put(vox_coords, tag, ops.avg_voxelize_plan(vox_coords, r))
 
 
-def conv_occupancy(vox_coords: torch.Tensor, r: int):
-    """ops.conv3d_occupancy of the voxelization plan's counts (shared per
-    points), or None when off or unsupported (r^3 % 256 != 0)."""
+def conv_occupancy(vox_coords: torch.Tensor, r: int) -> Optional[Occupancy]:
+    """Occupancy of the voxelization plan's counts (shared per points): tile
+    masks and voxel lists, or None when off or unsupported (r^3 % 256 != 0)."""
     from pcfm import ops
     if not (OCCUPANCY and _on(vox_coords)):
         return None
@@ -98,7 +110,11 @@ def conv_occupancy(vox_coords: torch.Tensor, r: int):
     hit = _cache.get(vox_coords, tag)
     if hit is not None:
         return hit[0]
-    occ = ops.conv3d_occupancy(voxel_plan(vox_coords, r).cnt, r)
+    cnt = voxel_plan(vox_coords, r).cnt
+    masks = ops.conv3d_occupancy(cnt, r)
+    if masks is None:
+        return None
+    occ = Occupancy(masks, ops.conv3d_vlists(cnt, r) if VOXEL_LISTS else None, cnt)
     _cache.put(vox_coords, tag, (occ,))
     return occ
 

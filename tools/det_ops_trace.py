@@ -88,7 +88,15 @@ def main():
                          "inputs": bad, "prev_ops": [runs[0][q][0] for q in range(max(0, i - 4), i)]}
                 break
             if not eq(o0, o1) or not eq(p0, p1):
-                first = {"call": i, "op": n0, "why": "same inputs, different outputs"}
+                det = []
+                for j, (u, v) in enumerate(zip(o0, o1)):
+                    if u.shape == v.shape and not torch.equal(u, v):
+                        d = u != v
+                        det.append({"output": j, "shape": list(u.shape), "dtype": str(u.dtype),
+                                    "n_diff": int(d.sum()), "first_idx": d.nonzero()[:6].tolist(),
+                                    "max_abs": float((u.double() - v.double()).abs().max())})
+                first = {"call": i, "op": n0, "why": "same inputs, different outputs",
+                         "outputs": det, "in_shapes": [list(t.shape) for t in i0]}
                 break
         print(json.dumps({"run": k, "n_calls": len(runs[k]), "first": first}), flush=True)
 
