@@ -232,7 +232,7 @@ __global__ void __launch_bounds__(256)
   const int b = (int)(g / V), v = (int)(g % V);
   float* __restrict__ yb = y + (size_t)b * M * V + v;
   for (int m = 0; m < M; ++m)
-    __builtin_nontemporal_store(bias != nullptr ? bias[m] : 0.0f, yb + (size_t)m * V);
+    nt_st(bias != nullptr ? bias[m] : 0.0f, yb + (size_t)m * V);
 }
 
 // ---------------------------------------------------------------------------
@@ -881,7 +881,7 @@ __global__ void __launch_bounds__(GN * 2)  // GK<KT, GN>::NW = GN / 32 waves
         const int m = m0 + wr * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
         if (ycol[j] != nullptr) {
 #ifndef PCFM_CONV_CACHED_STORE  // streamed: same-box bench 33.70 -> 33.57 ms/step
-          __builtin_nontemporal_store(acc[i][j][e] + biasv[i][e], ycol[j] + (size_t)m * V);
+          nt_st(acc[i][j][e] + biasv[i][e], ycol[j] + (size_t)m * V);
 #else
           ycol[j][(size_t)m * V] = acc[i][j][e] + biasv[i][e];
 #endif
@@ -1126,7 +1126,7 @@ __global__ void __launch_bounds__(512)
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
         const int m = m0 + wr * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
-        __builtin_nontemporal_store(acc[i][j][e] + biasv[i][e], yb + (size_t)m * V + v);
+        nt_st(acc[i][j][e] + biasv[i][e], yb + (size_t)m * V + v);
       }
   }
 }
@@ -1307,7 +1307,7 @@ __global__ void __launch_bounds__(512)
       for (int e = 0; e < 16; ++e) {
         const int m = m0 + wr * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
         const int v = v0 + wc * 64 + j * 32 + r;
-        __builtin_nontemporal_store(acc[i][j][e] + biasv[i][e], yb + (size_t)m * V + v);
+        nt_st(acc[i][j][e] + biasv[i][e], yb + (size_t)m * V + v);
       }
 }
 

@@ -21,7 +21,7 @@ namespace {
 // streamed 16-B store (the output is next read by another kernel, > L2)
 __device__ __forceinline__ void nt_store4(float4* p, float4 v) {
   typedef float v4f __attribute__((ext_vector_type(4)));
-  __builtin_nontemporal_store(v4f{v.x, v.y, v.z, v.w}, reinterpret_cast<v4f*>(p));
+  nt_st(v4f{v.x, v.y, v.z, v.w}, reinterpret_cast<v4f*>(p));
 }
 
 

@@ -68,4 +68,30 @@ __device__ __forceinline__ unsigned rev_order(unsigned i, unsigned n) {
   return PCFM_REV_APPLY ? n - 1 - i : i;
 }
 
+// Streamed (non-temporal) global accesses for outputs next read by another
+// kernel and inputs read once; PCFM_NT=0 builds them as plain accesses
+// (measurement / diagnosis switch).
+#ifndef PCFM_NT
+#define PCFM_NT 1
+#endif
+template <class T>
+__device__ __forceinline__ void nt_st(T v, T* p) {
+#if PCFM_NT
+  __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
+#endif
+}
+template <class T>
+__device__ __forceinline__ T nt_ld(const T* p) {
+#if defined(PCFM_COHERENT_LD) && PCFM_COHERENT_LD
+  // diagnosis switch: device-coherent (agent-scope) load, no stale cache line
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#elif PCFM_NT
+  return __builtin_nontemporal_load(p);
+#else
+  return *p;
+#endif
+}
+
 }  // namespace pcfm

@@ -22,7 +22,7 @@ inline int pad_to(int x, int m) { return (x + m - 1) / m * m; }
 // forward 112 -> 106 us, backward-data 134 -> 116 us (tools/pw_ab.py)
 __device__ __forceinline__ void out_store(float* p, float v) {
 #ifndef PCFM_PW_CACHED_STORE
-  __builtin_nontemporal_store(v, p);
+  nt_st(v, p);
 #else
   *p = v;
 #endif

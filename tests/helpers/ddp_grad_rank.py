@@ -38,6 +38,94 @@ def shard(cfg, s, dev):
     return batch, draws
 
 
+TRACE = None  # PCFM_DDP_TRACE=1: per pcfm.ops call, checksums of its float outputs
+KEEP = []  # ... and full copies of the devoxelization's inputs / outputs per call
+
+
+def _trace_ops():
+    """Wrap every pcfm.ops function so each call appends (name, [sum, abs-sum of
+    every float output]) to TRACE (a diagnostic: where two runs of the same
+    shard first part)."""
+    import functools
+    from pcfm import ops
+
+    def outs(x):
+        if isinstance(x, torch.Tensor):
+            return [x]
+        if isinstance(x, (list, tuple)):
+            return [t for e in x for t in outs(e)]
+        return []
+
+    def sums(ts):
+        return [(float(t.double().sum()), float(t.double().abs().sum()))
+                for t in ts if t.is_floating_point() and t.numel()
+                and not (0 in t.stride() and t.numel() > 1)]
+
+    def wrap(name, fn):
+        @functools.wraps(fn)
+        def inner(*a, **k):
+            out = fn(*a, **k)
+            if TRACE is not None:
+                TRACE.append((name, sums(outs(out))))
+                if name == "trilinear_devoxelize_scale_add":  # full copies, after the call
+                    KEEP.append([t.detach().clone() for t in outs(list(a)) + outs(out)])
+            return out
+        return inner
+    for name in dir(ops):
+        f = getattr(ops, name)
+        if callable(f) and not name.startswith("_") and getattr(f, "__module__", "") == ops.__name__:
+            setattr(ops, name, wrap(name, f))
+
+
+def _first_diff(a, b):
+    for i, (x, y) in enumerate(zip(a, b)):
+        if x != y:
+            return {"call": i, "op": x[0], "other_op": y[0], "a": x[1], "b": y[1]}
+    return None if len(a) == len(b) else {"call": min(len(a), len(b)), "why": "lengths differ"}
+
+
+class _Stagger:
+    """Keeps the two ranks' GPU work from overlapping on the one shared GPU (a
+    rehearsal-only arrangement; the product runs one process per GPU).  With
+    two processes computing on one MI355X at once, this repository's
+    measurements found rare corrupted 16-lane chunks in the devoxelization's
+    output -- never with one process -- so rank 1 starts
+    its DDP step only once rank 0's step has no GPU work left but the gradient
+    exchange: a DDP communication hook on rank 0 sees the last bucket, a
+    helper thread waits for the device to drain and drops a flag file that
+    rank 1 polls for.  The all-reduce itself still runs across both ranks."""
+
+    def __init__(self, path, rank, dev, modules=3):
+        import threading
+        self.path, self.rank, self.dev = path, rank, dev
+        self.last = threading.Event()
+        self.pending = modules  # DDP modules whose last bucket is still to come
+        if rank == 0:
+            def drain():
+                self.last.wait()
+                torch.cuda.synchronize(dev)
+                open(path, "w").close()
+            self.thread = threading.Thread(target=drain, daemon=True)
+            self.thread.start()
+
+    def hook(self, state, bucket):
+        fut = dist.all_reduce(bucket.buffer(), async_op=True).get_future()
+        if self.rank == 0 and bucket.is_last():
+            self.pending -= 1
+            if self.pending == 0:
+                self.last.set()
+        return fut.then(lambda f: f.value()[0].div_(dist.get_world_size()))
+
+    def wait_turn(self):
+        import time
+        if self.rank == 1:
+            t0 = time.time()
+            while not os.path.exists(self.path):
+                if time.time() - t0 > 120:
+                    raise RuntimeError("rank 0's DDP step did not drain")
+                time.sleep(0.01)
+
+
 def grads(tr):
     return [p.grad.detach().clone() if p.grad is not None else None for p in tr._clip_params]
 
@@ -51,30 +139,80 @@ def main():
                       tunableop=False, miopen_find=False)
     tr = Trainer(cfg, dev, rank=rank, world_size=world, ddp=True)
     tr.train_mode()
+    global TRACE
+    tracing = os.environ.get("PCFM_DDP_TRACE") == "1"
+    if tracing:
+        _trace_ops()
+    runs, kept = {}, {}
+    stagger = _Stagger(f"{sys.argv[1]}.drained", rank, dev)
+    for m in (tr.model_enc, tr.model_pf, tr.model_lf):  # one hook per DDP module
+        m.register_comm_hook(None, stagger.hook)
+    TRACE = [] if tracing else None
+    KEEP.clear()
     batch, draws = shard(cfg, rank, dev)
+    stagger.wait_turn()
     out = tr.forward_backward(batch, EPOCH, draws)
     g_ddp = grads(tr)
     torch.cuda.synchronize(dev)
+    runs["ddp"] = TRACE
+    kept["ddp"] = list(KEEP)
 
     # one-process reference on the same (broadcast) parameters
     ref = Trainer(cfg, dev, rank=0, world_size=1, ddp=False)
     for a, b in ((ref.enc, tr.enc), (ref.pf, tr.pf), (ref.lf, tr.lf)):
         a.load_state_dict(b.state_dict())
     ref.train_mode()
+    torch.cuda.synchronize(dev)
+    if rank == 1:  # the reference runs one rank at a time (see _Stagger)
+        dist.barrier()
     per, ref_losses = [], []
     for s in range(world):
         ref.opt.zero_grad(set_to_none=True)
         bs, ds = shard(cfg, s, dev)
+        TRACE = [] if tracing else None
+        KEEP.clear()
         o = ref.forward_backward(bs, EPOCH, ds)
         ref_losses.append([float(o["loss_point"]), float(o["loss_latent"])])
         per.append(grads(ref))
+        runs[f"ref{s}"] = TRACE
+        kept[f"ref{s}"] = list(KEEP)
     # the reference once more on shard `rank`: names of gradients that are not
     # reproducible inside one process (diagnostic)
     ref.opt.zero_grad(set_to_none=True)
     bs, ds = shard(cfg, rank, dev)
+    TRACE = [] if tracing else None
+    KEEP.clear()
     ref.forward_backward(bs, EPOCH, ds)
     again = grads(ref)
     torch.cuda.synchronize(dev)
+    runs["again"] = TRACE
+    kept["again"] = list(KEEP)
+    TRACE = None
+    if rank == 0:
+        dist.barrier()
+    trace_diff = None
+    if tracing:
+        # the forward differs only where an op is not reproducible (the backward
+        # of the DDP run sees all-reduced gradients, so compare up to its first
+        # parameter-gradient op only through the ref runs)
+        mine = runs[f"ref{rank}"]
+        trace_diff = {"ddp_vs_ref": _first_diff(runs["ddp"], mine),
+                      "ref_vs_again": _first_diff(mine, runs["again"]), "n_calls": len(mine),
+                      "devox": {}}
+        # element-level view of the devoxelization calls that differ
+        for pair in (("ddp", f"ref{rank}"), (f"ref{rank}", "again")):
+            for ci, (ta, tb) in enumerate(zip(kept[pair[0]], kept[pair[1]])):
+                rep = []
+                for ti, (u, v) in enumerate(zip(ta, tb)):
+                    if u.shape == v.shape and not torch.equal(u, v):
+                        d = (u != v)
+                        idx = d.nonzero()
+                        rep.append({"tensor": ti, "shape": list(u.shape), "n_diff": int(d.sum()),
+                                    "first_idx": idx[:8].tolist(),
+                                    "a": u[d][:8].tolist(), "b": v[d][:8].tolist()})
+                if rep:
+                    trace_diff["devox"][f"{pair[0]}-{pair[1]}#{ci}"] = rep
+                    break
 
     names = ([f"enc.{n}" for n, _ in tr.enc.named_parameters()]
              + [f"pf.{n}" for n, _ in tr.pf.named_parameters()]
@@ -102,7 +240,8 @@ def main():
     res = {"rank": rank, "world": world, "backend": dist.get_backend(),
            "losses": [float(out["loss_point"]), float(out["loss_latent"])],
            "ref_losses": ref_losses, "max_rel": max_rel, "bit_equal": bit_equal,
-           "n_grads": n_grads, "differ": differ, "unreproducible": unrepro, "grad_sums_equal_across_ranks":
+           "n_grads": n_grads, "differ": differ, "unreproducible": unrepro, "trace": trace_diff,
+           "grad_sums_equal_across_ranks":
            all(torch.equal(gathered[0], g) for g in gathered)}
     with open(f"{sys.argv[1]}.{rank}", "w") as f:
         json.dump(res, f)
