@@ -52,7 +52,7 @@ VOXEL_OPS = ("avg_voxelize_fwd", "avg_voxelize_bwd", "trilinear_devoxelize_fwd",
 BF16X3_PEAK_TF = BF16_DENSE_TF / 3  # fp32-equivalent peak of the 3-product split
 H100_DERIVED_PTS = 1.88e6       # 25 s/epoch at <= 293 steps/epoch (derived)
 # HBM bytes per launch of the voxel ops from rocprofv3 PMC passes (tools/op_traffic.py)
-TRAFFIC_FILE = os.path.join(REPO, "profiles", "r02_traffic.json")
+TRAFFIC_FILE = os.path.join(REPO, "profiles", "r03_traffic.json")
 
 
 def measured_traffic(op, batch, points):
@@ -66,19 +66,23 @@ def measured_traffic(op, batch, points):
         return None
     if (blob.get("batch", 8), blob.get("points", 20000)) != (batch, points):
         return None
-    vals = [v["traffic_bytes"] for k, v in data.items() if k.split("@")[0] == op]
-    return sum(vals) / len(vals) if len(vals) == 3 else None
+    ops_ = op.split("+")  # several ops of one kernel: the mean over all their shapes
+    vals = [v["traffic_bytes"] for k, v in data.items() if k.split("@")[0] in ops_]
+    return sum(vals) / len(vals) if len(vals) == 3 * len(ops_) else None
 
 
 # MFMA-pipe busy fractions of the conv kernels (rocprofv3 SQ_VALU_MFMA_BUSY_CYCLES
 # over GRBM_GUI_ACTIVE, tools/kernel_pmc.py at the C2 stage shapes)
-KERNEL_PMC_FILE = os.path.join(REPO, "profiles", "r02_kernel_pmc.json")
+KERNEL_PMC_FILE = os.path.join(REPO, "profiles", "r03_kernel_pmc.json")
 CONV_KERNEL = {"conv3d_fwd": "conv3_igemm_glds_kernel", "conv3d_bwd_data": "conv3_igemm_glds_kernel",
                "conv3d_wgrad": "conv3_wgrad3_kernel"}
 # launches that skip empty-voxel work (PVConv's first conv: chunk lists / tile
 # masks) are timed under "<op>_sparse" with the DENSE algorithmic FLOPs as their
 # amount, so they never stand for a roofline (their rate would overstate it)
 SPARSE_SUFFIX = "_sparse"
+# the dominant kernel of the step, conv3_igemm_glds, runs as two ops (forward and
+# backward-data): its roofline is taken over both ops' dense launches together
+IGEMM_OPS = ("conv3d_fwd", "conv3d_bwd_data")
 
 
 def committed_mfma_busy(op):
@@ -86,7 +90,7 @@ def committed_mfma_busy(op):
         kern = json.load(open(KERNEL_PMC_FILE))["kernels"]
     except (OSError, ValueError, KeyError):
         return None
-    name = CONV_KERNEL.get(op)
+    name = CONV_KERNEL.get(op.split("+")[0])
     for k, v in kern.items():
         if name and name in k and "mfma_busy_frac" in v:
             return v["mfma_busy_frac"]
@@ -320,12 +324,15 @@ def main():
         torch.cuda.synchronize(dev)
         ops.timer.enabled = False
         full = ops.timer.summary()
-        dense = [k for k in full if not k.endswith(SPARSE_SUFFIX)]
-        if dense:
-            roof_ops.add(max(dense, key=lambda k: full[k]["ms"]))
-            hbm = [k for k in full if k in VOXEL_OPS]
-            if hbm:
-                roof_ops.add(max(hbm, key=lambda k: full[k]["ms"]))
+        if all(k in full for k in IGEMM_OPS):
+            roof_ops.update(IGEMM_OPS)
+        else:
+            dense = [k for k in full if not k.endswith(SPARSE_SUFFIX)]
+            if dense:
+                roof_ops.add(max(dense, key=lambda k: full[k]["ms"]))
+        hbm = [k for k in full if k in VOXEL_OPS]
+        if hbm:
+            roof_ops.add(max(hbm, key=lambda k: full[k]["ms"]))
     ops.timer.reset()
     ops.timer.only = roof_ops
     ops.timer.enabled = bool(roof_ops)
@@ -365,14 +372,20 @@ def main():
                    for k, v in full.items()}
 
         def roof(op):
-            d = summary[op]
+            if isinstance(op, tuple):  # one kernel over several ops: their launches together
+                parts = [summary[o] for o in op]
+                d = {"ms": sum(p["ms"] for p in parts), "amount": sum(p["amount"] for p in parts),
+                     "launches": sum(p["launches"] for p in parts), "kind": parts[0]["kind"]}
+                op = "+".join(op)
+            else:
+                d = summary[op]
             sec = d["ms"] * 1e-3
             if d["kind"] == "hbm":
                 achieved = d["amount"] / sec / 1e9
                 traffic = measured_traffic(op, cfg.batch_size, cfg.num_points)
                 return {"kernel": op, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                        "traffic_unit": "bytes per launch (PMC, profiles/r02_traffic.json)"
+                        "traffic_unit": "bytes per launch (PMC, profiles/r03_traffic.json)"
                         if traffic else None,
                         "algorithmic_bytes_per_launch": d["amount"] / d["launches"],
                         "avg_launch_ms": d["ms"] / d["launches"]}
@@ -387,18 +400,22 @@ def main():
             return {"kernel": op, "bound": "mfma", "achieved": achieved, "peak": BF16X3_PEAK_TF,
                     "unit": "TFLOP/s", "frac": achieved / BF16X3_PEAK_TF, "traffic": traffic,
                     "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE + WRITE_SIZE, "
-                                    "profiles/r02_traffic.json)" if traffic else None,
+                                    "profiles/r03_traffic.json)" if traffic else None,
                     "note": "achieved = algorithmic fp32 conv FLOPs / time; each is 3 bf16 "
                             "MFMA products, so peak = dense bf16 2500 TF / 3; raw bf16 MFMA "
                             f"utilisation = {3 * achieved / BF16_DENSE_TF:.3f}",
                     "mfma_busy_frac": committed_mfma_busy(op),
                     "mfma_busy_source": "SQ_VALU_MFMA_BUSY_CYCLES / (1024 * GRBM_GUI_ACTIVE / 8), "
-                                        "profiles/r02_kernel_pmc.json",
+                                        "profiles/r03_kernel_pmc.json",
                     "algorithmic_flops_per_launch": d["amount"] / d["launches"],
                     "avg_launch_ms": d["ms"] / d["launches"]}
 
-        dense = [k for k in summary if not k.endswith(SPARSE_SUFFIX)]
-        roofline = roof(max(dense, key=lambda k: summary[k]["ms"])) if dense else None
+        dense = [k for k in summary if not k.endswith(SPARSE_SUFFIX) and k not in VOXEL_OPS]
+        if all(k in summary for k in IGEMM_OPS):
+            roofline = roof(IGEMM_OPS)
+            roofline["kernel"] = "conv3_igemm_glds (conv3d_fwd + conv3d_bwd_data, dense launches)"
+        else:
+            roofline = roof(max(dense, key=lambda k: summary[k]["ms"])) if dense else None
         hbm_ops = [k for k in summary if k in VOXEL_OPS]
         roofline_scatter = roof(max(hbm_ops, key=lambda k: summary[k]["ms"])) if hbm_ops else None
         log(f"{ms:.2f} ms/step, {value / 1e6:.3f} M points/s; losses {loss_p:.4f} {loss_z:.4f}")

@@ -508,8 +508,12 @@ __global__ void __launch_bounds__(kThreads)
 
 bool emd_persistent_enabled() {
   static const bool on = [] {
-    const char* e = std::getenv("PCFM_EMD_PERSISTENT");  // 0: the multi-launch form
-    return e == nullptr || std::atoi(e) != 0;
+    // opt-in (PCFM_EMD_PERSISTENT=1): bit-identical, but measured 6x slower than
+    // the multi-launch form at B = 8 (N = 2048: 4.5 vs 0.75 ms forward,
+    // profiles/r03_bench.json vs r02) -- the grid barriers cost more than the
+    // launches they replace
+    const char* e = std::getenv("PCFM_EMD_PERSISTENT");
+    return e != nullptr && std::atoi(e) != 0;
   }();
   return on;
 }

@@ -204,25 +204,41 @@ __global__ void __launch_bounds__(1024)
         ob[(size_t)cc * NI + i] = acc;
       }
     } else {
-      // epilogue: scale[b, c] * sum + add[b, c, i], one channel at a time.
-      // (A 4-channel prefetch of the operands ahead of the taps needed 48
-      // SGPRs spilled to VGPR lanes; with two processes sharing the GPU its
-      // outputs occasionally differed in lanes 48-63 of a wave -- the lanes
-      // the spill register leaves free -- so the plain form is kept.)
+      // epilogue operands of 4 channels at a time, the first 4 fetched before
+      // the taps so their latency overlaps the index computation (the plain
+      // per-channel form: devox forward 0.71 -> 1.14 ms/step, vox backward
+      // 0.55 -> 0.88 ms/step, profiles/r03_bench_step_breakdown.txt notes)
       const float* __restrict__ ab =
           epi.add != nullptr ? epi.add + ((size_t)b * C + c0) * NI + i : nullptr;
       const float* __restrict__ sb = epi.scale != nullptr ? epi.scale + (size_t)b * C + c0 : nullptr;
-      prov.get(b, i, primary, id, w);
-      for (int cc = 0; cc < nc; ++cc) {
-        float acc;
-        if constexpr (USE_LDS) {
-          acc = tap_sum<T>(lds + (size_t)cc * V, id, w);
-        } else {
-          acc = tap_sum<T>(rb + (size_t)cc * V, id, w);
+      float ad[4], sc[4];
+      auto fetch = [&](int cq) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int cc = min(cq + k, nc - 1);
+          ad[k] = ab != nullptr ? nt_ld(ab + (size_t)cc * NI) : 0.0f;
+          sc[k] = sb != nullptr ? sb[cc] : 1.0f;
         }
-        if (sb != nullptr) acc *= sb[cc];
-        if (ab != nullptr) acc += nt_ld(ab + (size_t)cc * NI);
-        ob[(size_t)cc * NI + i] = acc;
+      };
+      fetch(0);
+      prov.get(b, i, primary, id, w);
+      for (int cq = 0; cq < nc; cq += 4) {
+        if (cq > 0) fetch(cq);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int cc = cq + k;
+          if (cc < nc) {
+            float acc;
+            if constexpr (USE_LDS) {
+              acc = tap_sum<T>(lds + (size_t)cc * V, id, w);
+            } else {
+              acc = tap_sum<T>(rb + (size_t)cc * V, id, w);
+            }
+            if (sb != nullptr) acc *= sc[k];
+            if (ab != nullptr) acc += ad[k];
+            ob[(size_t)cc * NI + i] = acc;
+          }
+        }
       }
     }
   }
