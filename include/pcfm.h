@@ -43,7 +43,8 @@ extern "C" {
  * pcfm_conv3d_igemm_cl; 10: fused AdamW + clip + EMA parameter update; 11: segment
  * plans shared by scatters over the same points; 12: the BatchNorm forward entry
  * points take the module's num_batches_tracked counter; 13: occupancy-masked
- * voxel convolution entry points; 14: voxel-list form of the voxel convolution). */
+ * voxel convolution entry points; 14: voxel-list form of the voxel convolution;
+ * 15: the head FiLM backward takes shift and recomputes u). */
 int pcfm_abi_version(void);
 /* Thread-local text of the last non-zero return code. */
 const char* pcfm_last_error(void);
@@ -423,11 +424,15 @@ size_t pcfm_head_bwd_workspace_bytes(int b, int n, int w);
  *   dh = LayerNorm backward (f32, written if dh != NULL) and bf16(dh) -> dh16;
  *   dbias = sum_rows bf16(dh) (the bias gradient of the Linear that produced h),
  *   dbias_b[b] = the same sum per batch element (the hbias rows' gradient).
- * dsp1/dshift/dbias_b f32 [b][w], dgamma/dbeta/dbias f32 [w]; any may be NULL. */
+ * dsp1/dshift/dbias_b f32 [b][w], dgamma/dbeta/dbias f32 [w]; any may be NULL.
+ * u (the forward's f32 output) may be NULL when shift (bf16 [b][w]) is given: u
+ * is then recomputed from h, mean, rstd, gamma, beta, sp1, shift with the
+ * forward's expression -- bit-identical, 2 fewer bytes read per element (ABI 15). */
 int pcfm_head_film_bwd(const float* dh_next, const void* da16, const float* u, const void* h16,
                        const float* hbias, const float* uprev, const void* gprev,
                        const float* mean, const float* rstd, const float* gamma,
-                       const float* beta, const void* sp1, int b, int n, int w, float* dh,
+                       const float* beta, const void* sp1, const void* shift, int b, int n, int w,
+                       float* dh,
                        void* dh16, float* dsp1, float* dshift, float* dgamma, float* dbeta,
                        float* dbias, float* dbias_b, void* ws, size_t ws_bytes, void* stream);
 

@@ -177,7 +177,7 @@ __global__ void __launch_bounds__(256)
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const float y = __builtin_fmaf(gm[j][e], rstd * (x[j][e] - mean), bt[j][e]);
-          uu[j][e] = y * sp[j][e] + sh[j][e];
+          uu[j][e] = y * sp[j][e] + sh[j][e];  // unfused (-ffp-contract=off), as the backward
           o[j][e] = silu(uu[j][e]);
         }
       st_f32<NV>(u + off, lane, uu);
@@ -203,15 +203,20 @@ __global__ void __launch_bounds__(256)
                     const float* __restrict__ uprev, const uint16_t* __restrict__ gprev,
                     const float* __restrict__ mean_i, const float* __restrict__ rstd_i,
                     const float* __restrict__ gamma, const float* __restrict__ beta,
-                    const uint16_t* __restrict__ sp1, const float* __restrict__ hbias, int n,
-                    float* __restrict__ dh, uint16_t* __restrict__ dh16, float* __restrict__ part) {
+                    const uint16_t* __restrict__ sp1, const uint16_t* __restrict__ shift,
+                    const float* __restrict__ hbias, int n, float* __restrict__ dh,
+                    uint16_t* __restrict__ dh16, float* __restrict__ part) {
   constexpr int W = 256 * NV;
   __shared__ float red[4][kSums][W];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int b = blockIdx.y;
   const int i0 = blockIdx.x * kRowsPerBlock, i1 = min(n, i0 + kRowsPerBlock);
-  float gm[NV][4], bt[NV][4], sp[NV][4], hb[NV][4];
+  float gm[NV][4], bt[NV][4], sp[NV][4], sh[NV][4], hb[NV][4];
   const bool has_hb = hbias != nullptr;
+  // u == nullptr: u recomputed from h and the saved row statistics with the
+  // forward's own expression (bit-identical), instead of read back (2 of the
+  // 11 KB a 512-wide row costs)
+  const bool keep_u = u != nullptr;
   if (has_hb) ld_f32<NV>(hbias + (size_t)b * W, lane, hb);
   float acc[kSums][NV][4];
 #pragma unroll
@@ -224,6 +229,7 @@ __global__ void __launch_bounds__(256)
     ld_f32<NV>(gamma, lane, gm);
     ld_f32<NV>(beta, lane, bt);
     ld_bf16<NV>(sp1 + (size_t)b * W, lane, sp);
+    if (!keep_u) ld_bf16<NV>(shift + (size_t)b * W, lane, sh);
   }
   for (int i = i0 + wave; i < i1; i += 4) {
     const size_t row = (size_t)b * n + i;
@@ -234,10 +240,18 @@ __global__ void __launch_bounds__(256)
     if (FILM) {
       float du[NV][4], uu[NV][4];
       ld_f32<NV>(dhn + off, lane, du);
-      ld_f32<NV>(u + off, lane, uu);
+      if (keep_u) ld_f32<NV>(u + off, lane, uu);
       const float mean = mean_i[row], rstd = rstd_i[row];
       float s1 = 0.0f, s2 = 0.0f;
       float xh[NV][4], dxh[NV][4];
+      if (!keep_u) {
+#pragma unroll
+        for (int j = 0; j < NV; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            uu[j][e] = __builtin_fmaf(gm[j][e], rstd * (x[j][e] - mean), bt[j][e]) * sp[j][e] +
+                       sh[j][e];
+      }
 #pragma unroll
       for (int j = 0; j < NV; ++j)
 #pragma unroll
@@ -365,8 +379,8 @@ int launch_fwd(const void* h16, const float* uprev, const void* gprev, const flo
 template <bool FILM>
 int launch_bwd(const float* dhn, const void* da16, const float* u, const void* h16,
                const float* uprev, const void* gprev, const float* mean, const float* rstd,
-               const float* gamma, const float* beta, const void* sp1, const float* hbias, int b,
-               int n, int w, float* dh, void* dh16, float* dsp1, float* dshift, float* dgamma,
+               const float* gamma, const float* beta, const void* sp1, const void* shift,
+               const float* hbias, int b, int n, int w, float* dh, void* dh16, float* dsp1, float* dshift, float* dgamma,
                float* dbeta, float* dbias, float* dbias_b, void* ws, hipStream_t st) {
   const int chunks = ceil_div(n, kRowsPerBlock);
   const dim3 grid(chunks, b), blk(256);
@@ -374,16 +388,17 @@ int launch_bwd(const float* dhn, const void* da16, const float* u, const void* h
   const uint16_t* H = (const uint16_t*)h16;
   const uint16_t* G = (const uint16_t*)gprev;
   const uint16_t* S1 = (const uint16_t*)sp1;
+  const uint16_t* SH = (const uint16_t*)shift;
   uint16_t* D16 = (uint16_t*)dh16;
   float* part = (float*)ws;
   switch (w) {
     case 256:
       hipLaunchKernelGGL((film_bwd_kernel<1, FILM>), grid, blk, 0, st, dhn, DA, u, H, uprev, G,
-                         mean, rstd, gamma, beta, S1, hbias, n, dh, D16, part);
+                         mean, rstd, gamma, beta, S1, SH, hbias, n, dh, D16, part);
       break;
     default:
       hipLaunchKernelGGL((film_bwd_kernel<2, FILM>), grid, blk, 0, st, dhn, DA, u, H, uprev, G,
-                         mean, rstd, gamma, beta, S1, hbias, n, dh, D16, part);
+                         mean, rstd, gamma, beta, S1, SH, hbias, n, dh, D16, part);
   }
   float* perb = part + (size_t)b * chunks * kSums * w;
   hipLaunchKernelGGL(film_bwd_reduce_kernel, dim3(ceil_div(w, 64), kSums, b), dim3(256), 0, st,
@@ -434,17 +449,19 @@ extern "C" size_t pcfm_head_bwd_workspace_bytes(int b, int n, int w) {
 extern "C" int pcfm_head_film_bwd(const float* dh_next, const void* da16, const float* u,
                                   const void* h16, const float* hbias, const float* uprev,
                                   const void* gprev, const float* mean, const float* rstd,
-                                  const float* gamma, const float* beta, const void* sp1, int b,
-                                  int n, int w, float* dh, void* dh16, float* dsp1, float* dshift,
+                                  const float* gamma, const float* beta, const void* sp1,
+                                  const void* shift, int b, int n, int w, float* dh, void* dh16,
+                                  float* dsp1, float* dshift,
                                   float* dgamma, float* dbeta, float* dbias, float* dbias_b,
                                   void* ws, size_t ws_bytes, void* stream) {
   PCFM_CHECK_ARG(film_ok(b, n, w), "head_film_bwd: bad shape b=%d n=%d w=%d", b, n, w);
   PCFM_CHECK_ARG(h16 != nullptr || (uprev != nullptr && gprev != nullptr),
                  "head_film_bwd: need h16 or (uprev, gprev)");
+  PCFM_CHECK_ARG(u != nullptr || shift != nullptr, "head_film_bwd: need u or shift");
   PCFM_CHECK_ARG(ws_bytes >= pcfm_head_bwd_workspace_bytes(b, n, w),
                  "head_film_bwd: workspace %zu < %zu bytes", ws_bytes,
                  pcfm_head_bwd_workspace_bytes(b, n, w));
-  return launch_bwd<true>(dh_next, da16, u, h16, uprev, gprev, mean, rstd, gamma, beta, sp1,
+  return launch_bwd<true>(dh_next, da16, u, h16, uprev, gprev, mean, rstd, gamma, beta, sp1, shift,
                           h16 != nullptr ? hbias : nullptr, b, n, w, dh, dh16, dsp1, dshift,
                           dgamma, dbeta, dbias, dbias_b, ws, (hipStream_t)stream);
 }
@@ -457,6 +474,6 @@ extern "C" int pcfm_head_silu_bwd(const void* da16, const float* uprev, const vo
                  "head_silu_bwd: workspace %zu < %zu bytes", ws_bytes,
                  pcfm_head_bwd_workspace_bytes(b, n, w));
   return launch_bwd<false>(nullptr, da16, nullptr, nullptr, uprev, gprev, nullptr, nullptr,
-                           nullptr, nullptr, nullptr, nullptr, b, n, w, dh, dh16, nullptr, nullptr,
-                           nullptr, nullptr, dbias, nullptr, ws, (hipStream_t)stream);
+                           nullptr, nullptr, nullptr, nullptr, nullptr, b, n, w, dh, dh16, nullptr,
+                           nullptr, nullptr, nullptr, dbias, nullptr, ws, (hipStream_t)stream);
 }

@@ -112,11 +112,23 @@ struct ProvDevox {
         wgts_out[o] = wt[k];
       }
     }
+#ifndef PCFM_DEVOX_CHECK_EACH
+    // every corner is inside the volume when the low cell and the high offsets
+    // are (the usual case: coords in [0, r-1]); only then are the 8 checks skipped
+    const int xi = (int)xl, yi = (int)yl, zi = (int)zl;
+    const bool inside = (unsigned)xi < (unsigned)r && (unsigned)yi < (unsigned)r &&
+                        (unsigned)zi < (unsigned)r && (unsigned)(xi + (xh != 0)) < (unsigned)r &&
+                        (unsigned)(yi + (yh != 0)) < (unsigned)r &&
+                        (unsigned)(zi + zh) < (unsigned)r;
+    if (!inside)
+#endif
+    {
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const bool ok = (unsigned)id[k] < (unsigned)r3;
-      wt[k] = ok ? wt[k] : 0.0f;
-      id[k] = ok ? id[k] : 0;
+      for (int k = 0; k < 8; ++k) {
+        const bool ok = (unsigned)id[k] < (unsigned)r3;
+        wt[k] = ok ? wt[k] : 0.0f;
+        id[k] = ok ? id[k] : 0;
+      }
     }
   }
 };

@@ -94,7 +94,7 @@ SIGNATURES = {
                                    _P, _P]),
     "pcfm_head_silu_fwd": (_I, [_P, _P, _I, _I, _I, _P, _P]),
     "pcfm_head_bwd_workspace_bytes": (_Z, [_I, _I, _I]),
-    "pcfm_head_film_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I,
+    "pcfm_head_film_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I,
                                    _P, _P, _P, _P, _P, _P, _P, _P, _P, _Z, _P]),
     "pcfm_head_silu_bwd": (_I, [_P, _P, _P, _I, _I, _I, _P, _P, _P, _P, _Z, _P]),
     "pcfm_bn_workspace_bytes": (_Z, [_I, _I, _I]),
@@ -124,7 +124,7 @@ SIGNATURES = {
     "pcfm_adamw_ema_step": (_I, [_P, _P, _I, _P, _P, _I, _DP, _DP, _D, _D, _D, _D, _P]),
 }
 
-ABI_VERSION = 14
+ABI_VERSION = 15
 
 _lock = threading.Lock()
 _lib = None

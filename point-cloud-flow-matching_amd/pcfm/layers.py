@@ -116,16 +116,17 @@ class _HeadTrunkBF16(torch.autograd.Function):
         dh, dh16, dbias = ops.head_silu_bwd(da, us[-1], gs[-1], n)
         d_blk = [None] * len(blk)
         for k in range(nb - 1, -1, -1):
-            lw, lb, sp1, _, wk, _ = blk[_PER_BLOCK * k:_PER_BLOCK * (k + 1)]
+            lw, lb, sp1, sh, wk, _ = blk[_PER_BLOCK * k:_PER_BLOCK * (k + 1)]
             # dh16 is dL/dg_k (the bf16 operand of h_{k+1} = u_k + g_k)
             d_blk[_PER_BLOCK * k + 4] = ops.rows_wgrad_bf16(dh16, as_[k])
             d_blk[_PER_BLOCK * k + 5] = dbias.to(torch.bfloat16)
             da = torch.mm(dh16, wk)
             first = k == 0
+            # u_k recomputed in the kernel from h_k and the row statistics (not read back)
             res = ops.head_film_bwd(
-                dh, da, us[k], h1 if first else None, None if first else us[k - 1],
+                dh, da, None, h1 if first else None, None if first else us[k - 1],
                 None if first else gs[k - 1], stats[2 * k], stats[2 * k + 1], lw, lb, sp1, n,
-                want_dh=not first, hbias=hb if first else None)
+                want_dh=not first, hbias=hb if first else None, shift=sh)
             dh, dh16, dsp1, dshift, dgamma, dbeta, dbias = res[:7]
             if first:
                 d_hb = res[7]

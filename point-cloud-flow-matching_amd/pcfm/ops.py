@@ -993,10 +993,11 @@ def head_silu_fwd(uprev, gprev, n: int):
 
 
 def head_film_bwd(dh_next, da16, u, h16, uprev, gprev, mean, rstd, gamma, beta, sp1, n: int,
-                  want_dh: bool, hbias=None):
+                  want_dh: bool, hbias=None, shift=None):
     """Returns dh f32 (or None), dh16 bf16, dsp1 f32 (B, W), dshift f32 (B, W),
     dgamma f32 (W,), dbeta f32 (W,), dbias f32 (W,), and with hbias (h16's per-batch
-    input bias) its gradient dbias_b f32 (B, W) as an 8th value."""
+    input bias) its gradient dbias_b f32 (B, W) as an 8th value.  u may be None when
+    shift (the forward's bf16 (B, W) shift) is given: the kernel recomputes it."""
     rows, w = da16.shape
     b = rows // n
     dev = da16.device
@@ -1007,10 +1008,14 @@ def head_film_bwd(dh_next, da16, u, h16, uprev, gprev, mean, rstd, gamma, beta, 
     dgamma, dbeta, dbias = small[2 * b], small[2 * b + 1], small[2 * b + 2]
     dbias_b = small[2 * b + 3:] if hbias is not None else None
     ws = _workspace(_lib.query("pcfm_head_bwd_workspace_bytes", b, n, w), da16)
-    with _timed("head_film_bwd", rows * w * (4 + 2 + 4 + (2 if h16 is not None else 6)
+    if u is None and shift is None:
+        raise ValueError("head_film_bwd: need u or shift")
+    with _timed("head_film_bwd", rows * w * (4 + 2 + (4 if u is not None else 0)
+                                             + (2 if h16 is not None else 6)
                                              + (4 if want_dh else 0) + 2), da16):
         _lib.call("pcfm_head_film_bwd", _p(dh_next), _p(da16), _p(u), _p(h16), _p(hbias),
-                  _p(uprev), _p(gprev), _p(mean), _p(rstd), _p(gamma), _p(beta), _p(sp1), b, n,
+                  _p(uprev), _p(gprev), _p(mean), _p(rstd), _p(gamma), _p(beta), _p(sp1),
+                  _p(shift), b, n,
                   w, _p(dh), _p(dh16), _p(dsp1), _p(dshift), _p(dgamma), _p(dbeta), _p(dbias),
                   _p(dbias_b), _p(ws), ws.numel(), _stream(da16))
     if hbias is not None:

@@ -136,6 +136,31 @@ def test_fused_trunk_matches_torch_trunk(ops, width, n):
         assert _relnorm(g1[k], g0[k]) < 2e-2, k
 
 
+@pytest.mark.parametrize("w,first", [(512, False), (512, True), (256, False)])
+def test_film_bwd_recomputed_u_is_bitwise(ops, w, first):
+    """pcfm_head_film_bwd with u = NULL (recomputed from h, the row statistics and
+    shift) returns exactly what it returns when handed the forward's u."""
+    b, n = 3, 1000
+    g = torch.Generator(device="cuda").manual_seed(w + first)
+    rnd = lambda *s: torch.randn(*s, device="cuda", generator=g)  # noqa: E731
+    gamma, beta = 1.0 + 0.2 * rnd(w), 0.2 * rnd(w)
+    sp1, sh = (1.0 + 0.1 * rnd(b, w)).bfloat16(), (0.1 * rnd(b, w)).bfloat16()
+    if first:
+        h16, hb, uprev, gprev = rnd(b * n, w).bfloat16(), rnd(b, w), None, None
+    else:
+        h16, hb, uprev, gprev = None, None, rnd(b * n, w), rnd(b * n, w).bfloat16()
+    u, a, mean, rstd = ops.head_film_fwd(h16, uprev, gprev, gamma, beta, sp1, sh, n, 1e-5,
+                                         hbias=hb)
+    dhn, da = rnd(b * n, w), rnd(b * n, w).bfloat16()
+    r0 = ops.head_film_bwd(dhn, da, u, h16, uprev, gprev, mean, rstd, gamma, beta, sp1, n,
+                           want_dh=True, hbias=hb)
+    r1 = ops.head_film_bwd(dhn, da, None, h16, uprev, gprev, mean, rstd, gamma, beta, sp1, n,
+                           want_dh=True, hbias=hb, shift=sh)
+    assert len(r0) == len(r1)
+    for x0, x1 in zip(r0, r1):
+        assert torch.equal(x0, x1)
+
+
 @pytest.mark.parametrize("b,n,c", [(8, 20000, 128), (2, 777, 6), (3, 50, 384)])
 def test_rows_max_matches_torch(ops, b, n, c):
     from pcfm.layers import max_over_points

@@ -46,6 +46,14 @@ def run():
             ops.conv3d_igemm_split(gys, img_b, None, b, c, c, r, "b")
             ops.conv3d_wgrad_split(xs, gys, b, c, c, r)
         torch.cuda.synchronize()
+    for c, r in ((128, 32), (256, 16)):  # devoxelization forward (SE scale + point add)
+        x = torch.rand(b, 3, 20000, device="cuda", generator=g) * (r - 1)
+        grid = torch.randn(b, c, r ** 3, device="cuda", generator=g)
+        sc = torch.rand(b, c, device="cuda", generator=g)
+        pf = torch.randn(b, c, 20000, device="cuda", generator=g)
+        for _ in range(K):
+            ops.trilinear_devoxelize_scale_add(r, True, x, grid, sc, pf)
+        torch.cuda.synchronize()
     a = torch.randn(8, 20000, 3, device="cuda", generator=g)
     p = torch.randn(8, 20000, 3, device="cuda", generator=g)
     d1, d2 = torch.empty(8, 20000, device="cuda"), torch.empty(8, 20000, device="cuda")

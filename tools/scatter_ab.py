@@ -39,7 +39,14 @@ def main():
         _, inds, wgts = ops.trilinear_devoxelize_forward(r, True, nc, grid)
         vplan = ops.avg_voxelize_plan(vc, r)
         dplan = ops.trilinear_devoxelize_backward_plan(inds, wgts, r)
+        sc = torch.rand(b, c, device="cuda", generator=g)
+        pf = torch.randn(b, c, n, device="cuda", generator=g)
+        cnt = torch.randint(1, 4, (b, r ** 3), device="cuda", generator=g, dtype=torch.int32)
+        ind = torch.randint(0, r ** 3, (b, n), device="cuda", generator=g, dtype=torch.int32)
         res[f"C{c}R{r}"] = {
+            "devox_fwd_scale_add_ms": timeit(
+                lambda: ops.trilinear_devoxelize_scale_add(r, True, nc, grid, sc, pf)),
+            "vox_bwd_add_ms": timeit(lambda: ops.avg_voxelize_backward_add(grid, ind, cnt, pf)),
             "vox_fwd_ms": timeit(lambda: ops.avg_voxelize_forward(feat, vc, r)),
             "devox_bwd_ms": timeit(lambda: ops.trilinear_devoxelize_backward(feat, inds, wgts, r)),
             "vox_fwd_planned_ms": timeit(lambda: ops.avg_voxelize_forward_planned(feat, vplan)),
@@ -47,7 +54,9 @@ def main():
                 lambda: ops.trilinear_devoxelize_backward_planned(feat, dplan))}
         if os.environ.get("SCATTER_SAVE"):  # outputs for a bitwise comparison across variants
             OUT[f"C{c}R{r}"] = (ops.avg_voxelize_forward_planned(feat, vplan).cpu(),
-                                ops.trilinear_devoxelize_backward_planned(feat, dplan).cpu())
+                                ops.trilinear_devoxelize_backward_planned(feat, dplan).cpu(),
+                                ops.trilinear_devoxelize_scale_add(r, True, nc, grid, sc, pf)[0].cpu(),
+                                ops.avg_voxelize_backward_add(grid, ind, cnt, pf).cpu())
     if os.environ.get("SCATTER_SAVE"):
         path = os.environ["SCATTER_SAVE"]
         if os.path.exists(path):
