@@ -211,13 +211,26 @@ __global__ void __launch_bounds__(256)
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int b = blockIdx.y;
   const int i0 = blockIdx.x * kRowsPerBlock, i1 = min(n, i0 + kRowsPerBlock);
-  float gm[NV][4], bt[NV][4], sp[NV][4], sh[NV][4], hb[NV][4];
   const bool has_hb = hbias != nullptr;
   // u == nullptr: u recomputed from h and the saved row statistics with the
   // forward's own expression (bit-identical), instead of read back (2 of the
   // 11 KB a 512-wide row costs)
   const bool keep_u = u != nullptr;
-  if (has_hb) ld_f32<NV>(hbias + (size_t)b * W, lane, hb);
+  // The block's channel constants (gamma, beta, sp1[b], shift[b], hbias[b])
+  // live in LDS during the row loop -- in `red`, which is only needed after it
+  // -- and are read per row: in registers they took 40 VGPRs and held the
+  // kernel to 2-3 waves per SIMD on a latency-bound row stream.
+  float* cst = &red[0][0][0];
+  for (int c = threadIdx.x; c < W; c += 256) {
+    if (FILM) {
+      cst[c] = gamma[c];
+      cst[W + c] = beta[c];
+      cst[2 * W + c] = bf2f(sp1[(size_t)b * W + c]);
+      cst[3 * W + c] = keep_u ? 0.0f : bf2f(shift[(size_t)b * W + c]);
+    }
+    cst[4 * W + c] = has_hb ? hbias[(size_t)b * W + c] : 0.0f;
+  }
+  __syncthreads();
   float acc[kSums][NV][4];
 #pragma unroll
   for (int k = 0; k < kSums; ++k)
@@ -225,19 +238,22 @@ __global__ void __launch_bounds__(256)
     for (int j = 0; j < NV; ++j)
 #pragma unroll
       for (int e = 0; e < 4; ++e) acc[k][j][e] = 0.0f;
-  if (FILM) {
-    ld_f32<NV>(gamma, lane, gm);
-    ld_f32<NV>(beta, lane, bt);
-    ld_bf16<NV>(sp1 + (size_t)b * W, lane, sp);
-    if (!keep_u) ld_bf16<NV>(shift + (size_t)b * W, lane, sh);
-  }
+#pragma nounroll
   for (int i = i0 + wave; i < i1; i += 4) {
     const size_t row = (size_t)b * n + i;
     const size_t off = row * W;
-    float da[NV][4], x[NV][4], g[NV][4];
+    // keeps the constant reads inside the loop (not hoisted back into registers)
+    asm volatile("" ::: "memory");
+    float da[NV][4], x[NV][4], g[NV][4], hb[NV][4];
+    if (has_hb) ld_f32<NV>(cst + 4 * W, lane, hb);
     ld_bf16<NV>(da16 + off, lane, da);
     load_h<NV>(h16, uprev, gprev, off, lane, x, has_hb, hb);
     if (FILM) {
+      float gm[NV][4], bt[NV][4], sp[NV][4], sh[NV][4];
+      ld_f32<NV>(cst, lane, gm);
+      ld_f32<NV>(cst + W, lane, bt);
+      ld_f32<NV>(cst + 2 * W, lane, sp);
+      if (!keep_u) ld_f32<NV>(cst + 3 * W, lane, sh);
       float du[NV][4], uu[NV][4];
       ld_f32<NV>(dhn + off, lane, du);
       if (keep_u) ld_f32<NV>(u + off, lane, uu);
@@ -287,6 +303,7 @@ __global__ void __launch_bounds__(256)
 #pragma unroll
       for (int e = 0; e < 4; ++e) acc[4][j][e] += bf2f(f2bf(g[j][e]));  // bias grad of prev Linear
   }
+  __syncthreads();  // every wave is done with the constants in `red`
 #pragma unroll
   for (int k = 0; k < kSums; ++k)
 #pragma unroll
