@@ -17,6 +17,7 @@
 // the MFMA operands (8 consecutive r per lane) come out of gfx950's
 // transposing LDS read ds_read_b64_tr_b16 (cdna_hip_programming.md T10).
 #include <algorithm>
+#include <cstdlib>
 
 #include "pcfm_common.hpp"
 
@@ -89,10 +90,18 @@ __device__ __forceinline__ void store_tile(uint8_t* img, int t, const uint4 (&v)
   }
 }
 
+// 3 waves per SIMD (140 VGPRs, accumulators out of AGPRs) and 3 blocks per CU:
+// the compiler's own choice was 120 VGPRs + 64 AGPRs, 2 waves per SIMD.
+// tools/rows_ab.py on MI355X (R = 160000): 512x512 0.173 -> 0.160 ms,
+// 512x384 0.197 -> 0.119 ms, 6x512 0.047 -> 0.042 ms; 4 waves spill (0.22 ms)
+#ifndef PCFM_RW_W4
+#define PCFM_RW_W4 3
+#endif
+#define RW_WAVES __attribute__((amdgpu_waves_per_eu(PCFM_RW_W4, PCFM_RW_W4)))
 // grid = (tiles_m * tiles_n, S), 256 threads (2 x 2 waves of 64 x 64).
 // part[s][M][N] fp32 = sum over split s's rows of A[r][m] * B[r][n].
 template <int MA, int MB>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256) RW_WAVES
     rows_wgrad_kernel(const uint16_t* __restrict__ A, int lda, const uint16_t* __restrict__ B,
                       int ldb, long long R, int M, int N, int S, float* __restrict__ part) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[2 * kRT * 256];
@@ -220,10 +229,19 @@ __global__ void __launch_bounds__(256)
         uint16_t, (__bf16)(((red[0][cl] + red[1][cl]) + red[2][cl]) + red[3][cl]));
 }
 
+// blocks per CU the split count aims at (dev knob PCFM_RW_BPC, measurement)
+inline long long rows_wgrad_bpc() {
+  static const long long v = [] {
+    const char* e = std::getenv("PCFM_RW_BPC");
+    return e != nullptr ? std::max(1LL, std::atoll(e)) : 3LL;
+  }();
+  return v;
+}
+
 int rows_wgrad_splits(long long R, int M, int N) {
   const long long tiles = (long long)((M + kTile - 1) / kTile) * ((N + kTile - 1) / kTile);
   const long long steps = (R + kRT - 1) / kRT;
-  long long s = std::max(1LL, (2LL * kCUs + tiles - 1) / tiles);
+  long long s = std::max(1LL, (rows_wgrad_bpc() * kCUs + tiles - 1) / tiles);
   s = std::min(s, std::max(1LL, steps / 8));  // >= 8 K-steps per block
   return (int)std::min(s, 256LL);
 }
