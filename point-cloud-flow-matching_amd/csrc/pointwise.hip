@@ -445,7 +445,12 @@ __global__ void __launch_bounds__(kSW * 64)
 
 // dW partials: grid = (ceil(Cout/128) * ceil(Cin/128), S); K-steps of 32
 // points (a step never crosses a batch element).  part [S][Cout][Cin].
-__global__ void __launch_bounds__(256)
+#ifdef PCFM_PW_WG_WAVES
+#define PW_WG_WAVES __attribute__((amdgpu_waves_per_eu(PCFM_PW_WG_WAVES, PCFM_PW_WG_WAVES)))
+#else
+#define PW_WG_WAVES
+#endif
+__global__ void __launch_bounds__(256) PW_WG_WAVES
     pw_wgrad_kernel(const Parts x, const float* __restrict__ dy, int B, int cin,
                     int cout, int N, int S, float* __restrict__ part) {
   using T = Tile<128, 128>;
