@@ -305,6 +305,9 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))
 // fragment reads conflict-free.  grid = min(tiles / 8, CUs x blocks per CU),
 // 512 threads.
 constexpr int kSW = 8;  // waves per streaming block
+#ifndef PCFM_PW_STREAM_PF
+#define PCFM_PW_STREAM_PF 1  // B-operand chunks prefetched (1 or 2)
+#endif
 __device__ __forceinline__ bf16x8 split8(const float (&v)[8], bf16x8& lo) {
   bf16x8 hi;
 #pragma unroll
@@ -370,6 +373,91 @@ __global__ void __launch_bounds__(kSW * 64)
   if (tl >= tiles) return;  // wave-uniform; no barrier below
   const uint16_t* sah = sa;
   const uint16_t* sal = sa + 128 * ldr;
+#if PCFM_PW_STREAM_PF >= 2
+  // B-operand chunks two ahead in registers: (tile, chunk) positions walk the
+  // wave's tiles chunk by chunk; while chunk s computes, s+1 and s+2 are in
+  // flight (twice the bytes in flight of the one-ahead form)
+  auto adv = [&](int& t, int& c) {
+    if (++c == NCH) {
+      c = 0;
+      t += wstride;
+    }
+  };
+  auto load_at = [&](int t, int c, float (&v)[16]) {
+    const int bb = __builtin_amdgcn_readfirstlane(t / ntn);
+    pw_stream_load(x, bb, 32 * c, N, (t - bb * ntn) * 32 + n, h, v);
+  };
+  int t1 = tl, c1 = 0;
+  adv(t1, c1);
+  int t2 = t1, c2 = c1;
+  adv(t2, c2);
+  float nx[16], nx1[16];
+  load_at(tl, 0, nx);
+  if (t1 < tiles) load_at(t1, c1, nx1);
+  int ck = 0;
+  f32x16 acc[4];
+  while (true) {
+    const int b = __builtin_amdgcn_readfirstlane(tl / ntn);
+    const int p = (tl - b * ntn) * 32 + n;
+    float cur[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      cur[q] = nx[q];
+      nx[q] = nx1[q];
+    }
+    if (t2 < tiles) load_at(t2, c2, nx1);
+    if (ck == 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[i][e] = 0.0f;
+    }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 bh, bl;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        bh[j] = (__bf16)cur[8 * kk + j];
+        bl[j] = (__bf16)(cur[8 * kk + j] - (float)bh[j]);
+      }
+      const int ko = ck * 32 + kk * 16 + 8 * h;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int o = (32 * i + n) * ldr + ko;
+        const bf16x8 ah = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(sah + o));
+        const bf16x8 al = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(sal + o));
+        acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bh, acc[i], 0, 0, 0);
+        acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah, bl, acc[i], 0, 0, 0);
+        acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc[i], 0, 0, 0);
+      }
+    }
+    if (ck == NCH - 1) {
+      const int bo = b * bias_bstride;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int mg = m0 + 32 * i;
+        if (mg < M) {
+          float* __restrict__ yr = const_cast<float*>(uniform_ptr(y.row(b, mg, N)));
+          float* __restrict__ yl = yr + 4 * h * N + p;
+          float bv[16];
+          const float* bl = bias != nullptr ? uniform_ptr(bias + bo + mg) + 4 * h : nullptr;
+#pragma unroll
+          for (int e = 0; e < 16; ++e) bv[e] = bl != nullptr ? bl[(e & 3) + 8 * (e >> 2)] : 0.0f;
+          if (p < N) {
+#pragma unroll
+            for (int e = 0; e < 16; ++e)
+              out_store(yl + ((e & 3) + 8 * (e >> 2)) * N, acc[i][e] + bv[e]);
+          }
+        }
+      }
+    }
+    adv(tl, ck);
+    adv(t1, c1);
+    adv(t2, c2);
+    if (tl >= tiles) break;
+  }
+}
+#else
   float nx[16];
   {
     const int b = tl / ntn;
@@ -442,6 +530,7 @@ __global__ void __launch_bounds__(kSW * 64)
     if (tl >= tiles) break;
   }
 }
+#endif
 
 // dW partials: grid = (ceil(Cout/128) * ceil(Cin/128), S); K-steps of 32
 // points (a step never crosses a batch element).  part [S][Cout][Cin].
