@@ -13,3 +13,5 @@ for rep in 1 2; do
 done
 timeout -k 10 300 env PCFM_LIB=$VD/libpcfm_pf2.so python -u -m pytest tests/test_gpu_pointwise.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_pf.log 2>&1; echo "pytest rc=$?"; tail -1 gpurun_out/pytest_pf.log
 cat gpurun_out/pw_pf.jsonl
+PCFM_REPORT=gpurun_out/parity_head.json timeout -k 10 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread > gpurun_out/pytest_head.log 2>&1
+echo "full suite rc=$?"; tail -1 gpurun_out/pytest_head.log
