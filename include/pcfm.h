@@ -44,7 +44,8 @@ extern "C" {
  * plans shared by scatters over the same points; 12: the BatchNorm forward entry
  * points take the module's num_batches_tracked counter; 13: occupancy-masked
  * voxel convolution entry points; 14: voxel-list form of the voxel convolution;
- * 15: the head FiLM backward takes shift and recomputes u). */
+ * 15: the head FiLM backward takes shift and recomputes u; 16: devoxelization
+ * self-check entry point). */
 int pcfm_abi_version(void);
 /* Thread-local text of the last non-zero return code. */
 const char* pcfm_last_error(void);
@@ -99,6 +100,16 @@ int pcfm_trilinear_devoxelize_scale_add_fwd(const float* coords, const float* fe
                                             const float* scale, const float* add, int b, int c,
                                             int n, int r, int training, float* out, int* inds,
                                             float* wgts, void* stream);
+
+/* Diagnosis only (not a reference interface): recompute scale * devox(feat) + add
+ * per output in the plainest form and compare bit for bit with `out` (and, when
+ * inds / wgts are given, the stored corners).  rec i32 [2 + 16 * 8], zeroed by the
+ * caller: rec[0] mismatches, rec[1] points whose stored weights do not sum to 1,
+ * then up to 16 records {kind (0 out, 1 ind, 2 wgt), b, c, i, got, want, lane, wave}. */
+int pcfm_debug_devox_verify(const float* coords, const float* feat, const float* scale,
+                            const float* add, const float* out, const int* inds,
+                            const float* wgts, int b, int c, int n, int r, int* rec,
+                            void* stream);
 
 /* out[r] = scale * sum_v a[r][v] * b[r][v] (b NULL: plain row sum), rows of
  * `len` floats; deterministic.  (SE3d pooling and its scale gradient.) */

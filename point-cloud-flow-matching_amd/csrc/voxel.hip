@@ -89,10 +89,75 @@ __global__ void __launch_bounds__(256)
   x4[v] = q;
 }
 
+// Diagnosis: recompute scale * devox(feat) + add for every (b, c, i) in the
+// plainest form (one thread per output, global reads, no LDS, no batching) and
+// compare bit for bit with what the gather stored; training mode also checks
+// the stored inds / wgts.  rec[0] counts mismatches, rec[1] counts points whose
+// stored weights do not sum to 1 within 1e-5; rec[2 + 8k ..] holds up to 16
+// records {kind, b, c, i, got bits, want bits, lane, i / 64}.
+constexpr int kVerifyRecs = 16;
+__global__ void __launch_bounds__(256)
+    devox_verify_kernel(const float* __restrict__ coords, const float* __restrict__ feat,
+                        const float* __restrict__ scale, const float* __restrict__ add,
+                        const float* __restrict__ out, const int* __restrict__ inds,
+                        const float* __restrict__ wgts, int C, int n, int r, int* __restrict__ rec) {
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int b = blockIdx.y;
+  if (t >= (long long)C * n) return;
+  const int c = (int)(t / n), i = (int)(t % n);
+  const int s = r * r * r;
+  ProvDevox prov{coords, n, r, r * r, s, nullptr, nullptr};
+  int id[8];
+  float w[8];
+  prov.get(b, i, false, id, w);
+  const float* row = feat + ((size_t)b * C + c) * s;
+  float a = tap_sum<8>(row, id, w);
+  if (scale != nullptr) a *= scale[(size_t)b * C + c];
+  if (add != nullptr) a += add[((size_t)b * C + c) * n + i];
+  const float got = out[((size_t)b * C + c) * n + i];
+  auto note = [&](int kind, float gv, float wv) {
+    const int k = atomicAdd(rec, 1);
+    if (k < kVerifyRecs) {
+      int* e = rec + 2 + 8 * k;
+      e[0] = kind; e[1] = b; e[2] = c; e[3] = i;
+      e[4] = __float_as_int(gv); e[5] = __float_as_int(wv); e[6] = i & 63; e[7] = i >> 6;
+    }
+  };
+  if (__float_as_int(got) != __float_as_int(a)) note(0, got, a);
+  if (c == 0 && inds != nullptr) {
+    // the stored pairs are the unclamped ones (trilinear_devox.cu:64-75): compare
+    // where the recomputed corner is inside the volume with a non-zero weight
+    float sum = 0.0f;
+    for (int k = 0; k < 8; ++k) {
+      const size_t o = ((size_t)b * 8 + k) * n + i;
+      sum += wgts[o];
+      if ((unsigned)inds[o] < (unsigned)s && inds[o] != id[k] && w[k] != 0.0f)
+        note(1, __int_as_float(inds[o]), __int_as_float(id[k]));
+      if ((unsigned)id[k] < (unsigned)s && w[k] != 0.0f &&
+          __float_as_int(wgts[o]) != __float_as_int(w[k]))
+        note(2, wgts[o], w[k]);
+    }
+    if (fabsf(sum - 1.0f) > 1e-5f) atomicAdd(rec + 1, 1);
+  }
+}
+
 }  // namespace
 }  // namespace pcfm
 
 using namespace pcfm;
+
+extern "C" int pcfm_debug_devox_verify(const float* coords, const float* feat, const float* scale,
+                                       const float* add, const float* out, const int* inds,
+                                       const float* wgts, int b, int c, int n, int r, int* rec,
+                                       void* stream) {
+  int s = 0;
+  PCFM_CHECK_ARG(b >= 0 && c >= 0 && n >= 0 && cube_fits(r, &s) && rec != nullptr,
+                 "debug_devox_verify: bad arguments");
+  if ((long long)b * c * n == 0) return PCFM_OK;
+  hipLaunchKernelGGL(devox_verify_kernel, dim3(ceil_div((long long)c * n, 256), b), dim3(256), 0,
+                     (hipStream_t)stream, coords, feat, scale, add, out, inds, wgts, c, n, r, rec);
+  return check_launch("debug_devox_verify");
+}
 
 extern "C" size_t pcfm_avg_voxelize_fwd_workspace_bytes(int b, int c, int n, int r) {
   int s = 0;

@@ -75,6 +75,7 @@ SIGNATURES = {
     "pcfm_pointwise_wgrad": (_I, [_P, _P, _I, _I, _I, _I, _P, _P, _Z, _P]),
     "pcfm_trilinear_devoxelize_scale_add_fwd": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P,
                                                      _P, _P]),
+    "pcfm_debug_devox_verify": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _P]),
     "pcfm_rows_dot": (_I, [_P, _P, _L, _I, _F, _P, _P]),
     "pcfm_rows_affine": (_I, [_P, _P, _P, _L, _I, _P]),
     "pcfm_rows_colsum_workspace_bytes": (_Z, [_I, _L, _I]),
@@ -124,7 +125,7 @@ SIGNATURES = {
     "pcfm_adamw_ema_step": (_I, [_P, _P, _I, _P, _P, _I, _DP, _DP, _D, _D, _D, _D, _P]),
 }
 
-ABI_VERSION = 15
+ABI_VERSION = 16
 
 _lock = threading.Lock()
 _lib = None

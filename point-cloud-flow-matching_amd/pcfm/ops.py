@@ -224,6 +224,9 @@ def trilinear_devoxelize_forward(r: int, is_training: bool, coords: torch.Tensor
     with _timed("trilinear_devoxelize_fwd", nbytes, features):  # devox-fwd
         _lib.call("pcfm_trilinear_devoxelize_fwd", _ptr(coords), _ptr(features), b, c, n, r,
                   1 if is_training else 0, _ptr(outs), pi, pw, _stream(features))
+    if devox_verify.enabled:
+        devox_verify(coords, features, None, None, outs, inds if is_training else None,
+                     wgts if is_training else None, r)
     return [outs, inds, wgts]
 
 
@@ -263,7 +266,49 @@ def trilinear_devoxelize_scale_add(r: int, is_training: bool, coords: torch.Tens
                   _ptr(scale) if scale is not None else None,
                   _ptr(add) if add is not None else None, b, c, n, r, 1 if is_training else 0,
                   _ptr(outs), pi, pw, _stream(features))
+    if devox_verify.enabled:
+        devox_verify(coords, features, scale, add, outs, inds if is_training else None,
+                     wgts if is_training else None, r)
     return [outs, inds, wgts]
+
+
+class _DevoxVerify:
+    """Diagnosis switch (PCFM_DEVOX_VERIFY=1): after every devoxelization gather,
+    pcfm_debug_devox_verify recomputes each output in the plainest form on the
+    same stream and compares bit for bit; mismatches accumulate on the device
+    (report() reads them once, at the end)."""
+
+    def __init__(self):
+        import os
+        self.enabled = os.environ.get("PCFM_DEVOX_VERIFY") == "1"
+        self.rec = None
+        self.calls = 0
+
+    def __call__(self, coords, features, scale, add, outs, inds, wgts, r):
+        if self.rec is None or self.rec.device != outs.device:
+            self.rec = torch.zeros(2 + 16 * 8, dtype=torch.int32, device=outs.device)
+        b, c, n = outs.shape
+        self.calls += 1
+        _lib.call("pcfm_debug_devox_verify", _ptr(coords), _ptr(features),
+                  _ptr(scale) if scale is not None else None,
+                  _ptr(add) if add is not None else None, _ptr(outs),
+                  _ptr(inds) if inds is not None else None,
+                  _ptr(wgts) if wgts is not None else None, b, c, n, int(r), _ptr(self.rec),
+                  _stream(outs))
+
+    def report(self):
+        if self.rec is None:
+            return {"calls": self.calls, "mismatches": 0, "bad_weight_sums": 0, "records": []}
+        h = self.rec.cpu().tolist()
+        recs = []
+        for k in range(min(h[0], 16)):
+            e = h[2 + 8 * k: 10 + 8 * k]
+            recs.append({"kind": ("out", "ind", "wgt")[e[0]], "b": e[1], "c": e[2], "i": e[3],
+                         "got_bits": e[4], "want_bits": e[5], "lane": e[6], "wave_of_i": e[7]})
+        return {"calls": self.calls, "mismatches": h[0], "bad_weight_sums": h[1], "records": recs}
+
+
+devox_verify = _DevoxVerify()
 
 
 # --------------------------------------------------------------------------
@@ -334,7 +379,8 @@ def trilinear_devoxelize_backward_planned(grad_y: torch.Tensor, plan: SegPlan) -
     r = plan.r
     grad_x = torch.empty((b, c, r ** 3), dtype=torch.float32, device=grad_y.device)
     ws = _workspace(_lib.query("pcfm_seg_apply_workspace_bytes", b, c, n, r, 8), grad_y)
-    with _timed("trilinear_devoxelize_bwd", 4 * b * (c * n + c * r ** 3), grad_y):
+    # SURVEY 8d devox-bwd: grad_y in, inds + wgts (16N.4) in, grad_x out
+    with _timed("trilinear_devoxelize_bwd", 4 * b * (c * n + 16 * n + c * r ** 3), grad_y):
         _lib.call("pcfm_trilinear_devoxelize_bwd_planned", _ptr(grad_y), _ptr(plan.buf), b, c, n,
                   r, _ptr(grad_x), _ptr(ws), ws.numel(), _stream(grad_y))
     return grad_x

@@ -14,6 +14,12 @@ import json
 import os
 import sys
 
+if os.environ.get("PCFM_DDP_CU_SPLIT") == "1":
+    # diagnosis: each rank's queues on its own half of the GPU's 256 CUs, set
+    # before the HIP runtime starts (ROCr reads HSA_CU_MASK at initialisation)
+    _lr = int(os.environ.get("LOCAL_RANK", "0"))
+    os.environ["HSA_CU_MASK"] = "0:0-127" if _lr == 0 else "0:128-255"
+
 REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path[:0] = [REPO, os.path.join(REPO, "point-cloud-flow-matching_amd")]
 
@@ -144,9 +150,13 @@ def main():
     if tracing:
         _trace_ops()
     runs, kept = {}, {}
+    staggered = os.environ.get("PCFM_DDP_STAGGER", "1") == "1"
     stagger = _Stagger(f"{sys.argv[1]}.drained", rank, dev)
-    for m in (tr.model_enc, tr.model_pf, tr.model_lf):  # one hook per DDP module
-        m.register_comm_hook(None, stagger.hook)
+    if staggered:
+        for m in (tr.model_enc, tr.model_pf, tr.model_lf):  # one hook per DDP module
+            m.register_comm_hook(None, stagger.hook)
+    else:
+        stagger.wait_turn = lambda: None
     TRACE = [] if tracing else None
     KEEP.clear()
     batch, draws = shard(cfg, rank, dev)
@@ -163,7 +173,7 @@ def main():
         a.load_state_dict(b.state_dict())
     ref.train_mode()
     torch.cuda.synchronize(dev)
-    if rank == 1:  # the reference runs one rank at a time (see _Stagger)
+    if rank == 1 and staggered:  # the reference runs one rank at a time (see _Stagger)
         dist.barrier()
     per, ref_losses = [], []
     for s in range(world):
@@ -188,7 +198,7 @@ def main():
     runs["again"] = TRACE
     kept["again"] = list(KEEP)
     TRACE = None
-    if rank == 0:
+    if rank == 0 and staggered:
         dist.barrier()
     trace_diff = None
     if tracing:
@@ -242,7 +252,11 @@ def main():
            "ref_losses": ref_losses, "max_rel": max_rel, "bit_equal": bit_equal,
            "n_grads": n_grads, "differ": differ, "unreproducible": unrepro, "trace": trace_diff,
            "grad_sums_equal_across_ranks":
-           all(torch.equal(gathered[0], g) for g in gathered)}
+           all(torch.equal(gathered[0], g) for g in gathered),
+           "staggered": staggered, "cu_mask": os.environ.get("HSA_CU_MASK")}
+    from pcfm import ops
+    if ops.devox_verify.enabled:
+        res["devox_verify"] = ops.devox_verify.report()
     with open(f"{sys.argv[1]}.{rank}", "w") as f:
         json.dump(res, f)
     dist.barrier()
