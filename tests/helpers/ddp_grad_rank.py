@@ -53,6 +53,7 @@ def _trace_ops():
     every float output]) to TRACE (a diagnostic: where two runs of the same
     shard first part)."""
     import functools
+    import types
     from pcfm import ops
 
     def outs(x):
@@ -79,7 +80,8 @@ def _trace_ops():
         return inner
     for name in dir(ops):
         f = getattr(ops, name)
-        if callable(f) and not name.startswith("_") and getattr(f, "__module__", "") == ops.__name__:
+        if (isinstance(f, types.FunctionType) and not name.startswith("_")
+                and f.__module__ == ops.__name__):
             setattr(ops, name, wrap(name, f))
 
 
