@@ -25,11 +25,43 @@ AGGRESSORS = ["none", "devox", "conv_fwd", "conv_wgrad", "pointwise", "bn", "bla
 SHAPES = [(8, 256, 4096, 16), (8, 256, 4096, 8), (8, 128, 4096, 32)]
 
 
+def _canary(seconds):
+    """A victim with no spills and no LDS: torch elementwise kernels whose
+    result is compared with the first evaluation (bitwise)."""
+    import torch
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(0)
+    x = torch.randn(8, 256, 4096, device=dev, generator=g)
+    ref = torch.addcmul(x * 1.5 + 0.25, x, x)
+    bad = torch.zeros((), dtype=torch.int64, device=dev)
+    it = 0
+    t0 = time.time()
+    while time.time() - t0 < seconds:
+        y = torch.addcmul(x * 1.5 + 0.25, x, x)
+        bad += (y != ref).sum()
+        it += 1
+        if it % 50 == 0:
+            torch.cuda.synchronize(dev)
+    print(json.dumps({"iterations": it, "mismatches": int(bad), "calls": it,
+                      "bad_weight_sums": 0, "records": []}), flush=True)
+
+
 def _victim(seconds):
     import torch
     from pcfm import ops
+    if os.environ.get("PROBE_VICTIM") == "canary":
+        return _canary(seconds)
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev).manual_seed(0)
+    if os.environ.get("PROBE_SAME_PROCESS"):
+        # the aggressor in this process on a second stream (a Python thread)
+        import threading
+        side = torch.cuda.Stream(dev)
+
+        def agg():
+            with torch.cuda.stream(side):
+                _aggressor(os.environ["PROBE_SAME_PROCESS"], seconds + 2, quiet=True)
+        threading.Thread(target=agg, daemon=True).start()
     cases = []
     for b, c, n, r in SHAPES:
         coords = torch.rand(b, 3, n, device=dev, generator=g) * (r - 1)
@@ -51,7 +83,7 @@ def _victim(seconds):
     print(json.dumps(rep), flush=True)
 
 
-def _aggressor(name, seconds):
+def _aggressor(name, seconds, quiet=False):
     import torch
     from pcfm import ops
     dev = torch.device("cuda", 0)
@@ -105,7 +137,8 @@ def _aggressor(name, seconds):
         if it % 20 == 0:
             torch.cuda.synchronize(dev)
     torch.cuda.synchronize(dev)
-    print(json.dumps({"iterations": it}), flush=True)
+    if not quiet:
+        print(json.dumps({"iterations": it}), flush=True)
 
 
 def main():
@@ -116,14 +149,22 @@ def main():
     secs = float(sys.argv[1]) if len(sys.argv) > 1 else 12.0
     names = sys.argv[2].split(",") if len(sys.argv) > 2 else AGGRESSORS
     me = os.path.abspath(__file__)
-    for name in names:
+    for spec in names:
+        # NAME | NAME@canary (torch elementwise victim) | NAME@stream (same process)
+        name, _, how = spec.partition("@")
         env = dict(os.environ, PCFM_DEVOX_VERIFY="1")
-        agg = subprocess.Popen([sys.executable, me, "aggressor", name, str(secs + 4)],
+        if how == "canary":
+            env["PROBE_VICTIM"] = "canary"
+        agg_name = name
+        if how == "stream":
+            env["PROBE_SAME_PROCESS"] = name
+            agg_name = "none"
+        agg = subprocess.Popen([sys.executable, me, "aggressor", agg_name, str(secs + 4)],
                                stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env)
         vic = subprocess.run([sys.executable, me, "victim", str(secs)], capture_output=True,
                              text=True, env=env, timeout=secs + 120)
         a_out, a_err = agg.communicate(timeout=secs + 120)
-        res = {"aggressor": name, "victim_rc": vic.returncode, "aggressor_rc": agg.returncode}
+        res = {"aggressor": spec, "victim_rc": vic.returncode, "aggressor_rc": agg.returncode}
         try:
             res["victim"] = json.loads(vic.stdout.strip().splitlines()[-1])
             res["aggressor_iterations"] = json.loads(a_out.strip().splitlines()[-1])["iterations"]
