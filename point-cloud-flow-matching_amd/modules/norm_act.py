@@ -14,6 +14,9 @@ import torch.nn.functional as F
 
 __all__ = ["bn_act", "conv_bn_act", "gn_film_residual"]
 
+# PCFM_DEBUG_CHECKS=1: assert the preconditions of the exact-skip fast paths
+_DEBUG_CHECKS = __import__("os").environ.get("PCFM_DEBUG_CHECKS") == "1"
+
 
 class _BNAct(torch.autograd.Function):
     @staticmethod
@@ -180,11 +183,23 @@ class _Conv3dBnActPair(torch.autograd.Function):
 
 
 def conv_bn_act_pair(conv1, bn1, slope1: float, conv2, bn2, slope2: float,
-                     x: torch.Tensor, occ=None) -> torch.Tensor:
+                     x: torch.Tensor, voxelized_input_occ=None) -> torch.Tensor:
     """act2(bn2(conv2(act1(bn1(conv1(x)))))) for two VoxelConv3d layers: one
     autograd node on the GPU path when both layers qualify, else two
-    conv_bn_act calls.  `occ`: occupancy masks when x is a voxelized grid
-    (_Conv3dBnActPair)."""
+    conv_bn_act calls.
+
+    voxelized_input_occ (pcfm.plans.conv_occupancy of the points x was
+    voxelized from; PVConv only): x must be exactly 0 at every empty voxel, and
+    the returned input gradient is then computed at the OCCUPIED voxels only
+    (0 elsewhere) -- correct for the voxelization's backward, which reads it
+    there only (vox.cu:86-110), wrong for any other consumer of dx.  With
+    PCFM_DEBUG_CHECKS=1 the zero-outside-occupancy precondition is asserted."""
+    occ = voxelized_input_occ
+    if occ is not None and _DEBUG_CHECKS and x.is_cuda:
+        empty = (occ.cnt == 0).view(x.shape[0], 1, -1).expand(-1, x.shape[1], -1)
+        if bool((x.reshape(x.shape[0], x.shape[1], -1)[empty] != 0).any()):
+            raise AssertionError("conv_bn_act_pair: voxelized_input_occ given but x is non-zero "
+                                 "at an empty voxel")
     from modules.shared_mlp import PointwiseConv1d
     ok = (not isinstance(conv1, PointwiseConv1d) and not isinstance(conv2, PointwiseConv1d)
           and _fusable_pre(bn1) and _fusable_pre(bn2) and hasattr(conv1, "x3_ok")

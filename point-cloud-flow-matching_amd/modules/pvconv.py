@@ -130,7 +130,8 @@ class PVConv(nn.Module):
             from pcfm import plans
             occ = plans.conv_occupancy(self.voxelization._coords(coords)[1], self.resolution)
         grid = conv_bn_act_pair(layers[0], layers[1], layers[2].negative_slope,
-                                layers[3], layers[4], layers[5].negative_slope, grid, occ=occ)
+                                layers[3], layers[4], layers[5].negative_slope, grid,
+                                voxelized_input_occ=occ)
         pf = self.point_features(features)
         if (len(layers) > 6 and _se_devox_ok(layers[6], grid, pf)
                 and (self.training or not torch.is_grad_enabled())):

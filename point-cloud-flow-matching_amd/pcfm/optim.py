@@ -172,6 +172,11 @@ class FusedAdamWEMA:
                 if st is None:
                     continue
                 m, v = self._moments(pos)
+                for name, dst in (("exp_avg", m), ("exp_avg_sq", v)):
+                    if tuple(st[name].shape) != tuple(dst.shape):  # copy_ would broadcast
+                        raise ValueError(f"FusedAdamWEMA.load_state_dict: state {key} {name} "
+                                         f"shape {tuple(st[name].shape)} != parameter shape "
+                                         f"{tuple(dst.shape)}")
                 m.copy_(st["exp_avg"])
                 v.copy_(st["exp_avg_sq"])
                 steps[pos] = float(st["step"])

@@ -173,6 +173,16 @@ def dopri5(velocity: Velocity, x: torch.Tensor, t0: float = 0.0, t1: float = 1.0
     every velocity evaluation (as torchdiffeq's func sees it, in x's dtype).
     `fixed_steps=k` instead takes k equal Dormand-Prince steps ending exactly on
     t1, no error control (this build's fixed-grid variant; 1 + 6k evaluations)."""
+    if float(t1) == float(t0):  # torchdiffeq rejects a degenerate grid (misc.py:101, :286)
+        raise AssertionError("t must be strictly increasing or decreasing")
+    if float(t1) < float(t0):
+        # decreasing time as torchdiffeq integrates it (misc.py:259-269): t -> -t and
+        # f -> -f(-t, y) over the increasing grid [-t0, -t1]
+        def rev(y, s):
+            if trace is not None:
+                trace.append(float(-s[0]))
+            return -velocity(y, -s)
+        return dopri5(rev, x, -float(t0), -float(t1), rtol, atol, fixed_steps, max_steps, None)
     nfe = 0
 
     def f(t, y, prev=False):

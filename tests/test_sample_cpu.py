@@ -40,6 +40,19 @@ def test_dopri5_is_exact_on_polynomials_in_t():
     assert torch.allclose(x, x0 + 1.0, rtol=0, atol=1e-14)
 
 
+def test_dopri5_degenerate_and_reversed_spans():
+    # torchdiffeq: equal times are rejected (misc.py:101, :286); a decreasing span is
+    # integrated as -f(-t, y) over the negated grid (misc.py:259-269)
+    x0 = torch.tensor([[1.0, 0.5]], dtype=torch.float64)
+    with pytest.raises(AssertionError, match="strictly increasing or decreasing"):
+        sample.dopri5(lambda x, t: -x, x0, t0=0.5, t1=0.5)
+    seen = []
+    x, nfe = sample.dopri5(lambda x, t: (seen.append(float(t[0])), -x)[1], x0, t0=1.0, t1=0.0,
+                           rtol=1e-9, atol=1e-9)
+    assert torch.allclose(x, x0 * math.e, rtol=1e-7, atol=0)
+    assert len(seen) == nfe and seen[0] == 1.0 and max(seen) == 1.0  # the user sees t, not -t
+
+
 def test_dopri5_fixed_steps_nfe():
     _, nfe = sample.dopri5(lambda x, t: -x, torch.ones(1, 1), fixed_steps=10)
     assert nfe == 1 + 10 * 6  # FSAL: 6 new evaluations per step
