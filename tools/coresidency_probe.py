@@ -61,7 +61,8 @@ def _victim(seconds):
         def agg():
             with torch.cuda.stream(side):
                 _aggressor(os.environ["PROBE_SAME_PROCESS"], seconds + 2, quiet=True)
-        threading.Thread(target=agg, daemon=True).start()
+        th = threading.Thread(target=agg, daemon=True)
+        th.start()
     cases = []
     for b, c, n, r in SHAPES:
         coords = torch.rand(b, 3, n, device=dev, generator=g) * (r - 1)
@@ -78,6 +79,9 @@ def _victim(seconds):
         if it % 50 == 0:
             torch.cuda.synchronize(dev)
     torch.cuda.synchronize(dev)
+    if os.environ.get("PROBE_SAME_PROCESS"):
+        th.join()  # the side stream's work drains before the process exits
+        torch.cuda.synchronize(dev)
     rep = ops.devox_verify.report()
     rep["iterations"] = it
     print(json.dumps(rep), flush=True)
