@@ -85,6 +85,26 @@ SPARSE_SUFFIX = "_sparse"
 IGEMM_OPS = ("conv3d_fwd", "conv3d_bwd_data")
 
 
+# every kernel of the PVConv voxel scatter/gather machinery: the four ops and the
+# segment plans (sort + work units) they run on
+SCATTER_GATHER_OPS = VOXEL_OPS + ("avg_voxelize_plan", "trilinear_devoxelize_bwd_plan")
+
+
+def scatter_gather_bytes(batch, points, stages=((128, 32), (256, 16), (256, 8)), blocks=2):
+    """algorithmic bytes of every PVConv voxelize / devoxelize call of
+    one train step, forward and backward (each distinct tensor read or written once):
+    4.81 GB at C2 (B=8, N=20000)."""
+    b, n, tot = batch, points, 0
+    for c, r in stages:
+        v = r ** 3
+        vf = b * (3 * n * 4 + c * n * 4 + n * 4 + v * 4 + c * v * 4)
+        vb = b * (c * v * 4 + n * 4 + v * 4 + c * n * 4)
+        df = b * (3 * n * 4 + c * v * 4 + c * n * 4 + 16 * n * 4)
+        db = b * (c * n * 4 + 16 * n * 4 + c * v * 4)
+        tot += blocks * (vf + vb + df + db)
+    return tot
+
+
 def committed_mfma_busy(op):
     try:
         kern = json.load(open(KERNEL_PMC_FILE))["kernels"]
@@ -173,7 +193,12 @@ def cpu_baseline(args, cfg_kwargs):
     Chamfer (train.py:80-84: cdist, squared, min both ways) on one cloud pair."""
     from pcfm.train import TrainConfig, Trainer, synthetic_batch
 
-    threads = torch.get_num_threads()  # OMP_NUM_THREADS: the box's CPU share
+    # SURVEY 8(d): the host's physical cores (lscpu); the box caps OMP_NUM_THREADS at
+    # its CPU share, so the count used is stated next to the host's core count
+    host = host_cpu()
+    want = host.get("physical_cores") or os.cpu_count() or 1
+    torch.set_num_threads(int(want))
+    threads = torch.get_num_threads()
     cfg = TrainConfig(**{**cfg_kwargs, "batch_size": args.cpu_batch, "film_per_point": True})
     tr = Trainer(cfg, "cpu")
     tr.train_mode()
@@ -193,7 +218,7 @@ def cpu_baseline(args, cfg_kwargs):
     cd = time.perf_counter() - t1
     del d2
     return {"value": pts / dt, "unit": "points/s", "cores": threads, "kind": "port",
-            "host_cpu": host_cpu(),
+            "host_cpu": host,
             "sample": f"1 timed train step (after a B=1, N=2048 warm-up) at B={cfg.batch_size}, "
                       f"N={n}, {cfg.pf_backbone} backbone, fp32 torch CPU, per-point FiLM, "
                       f"pcfm.cpu_ops voxel ops, {threads} threads; {dt:.2f} s/step",
@@ -418,6 +443,21 @@ def main():
             roofline = roof(max(dense, key=lambda k: summary[k]["ms"])) if dense else None
         hbm_ops = [k for k in summary if k in VOXEL_OPS]
         roofline_scatter = roof(max(hbm_ops, key=lambda k: summary[k]["ms"])) if hbm_ops else None
+        # the whole voxel scatter/gather chain of a step: SURVEY 8(d)'s bytes over the
+        # summed time of all its kernels (the profiled steps' HIP events)
+        sg_ms = sum(full[k]["ms"] for k in full if k in SCATTER_GATHER_OPS) / max(1, prof_steps)
+        sg_bytes = scatter_gather_bytes(cfg.batch_size, cfg.num_points) \
+            if args.backbone == "hybrid" else None
+        roofline_sg_all = None
+        if sg_ms > 0 and sg_bytes:
+            ach = sg_bytes / (sg_ms * 1e-3) / 1e9
+            roofline_sg_all = {
+                "bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": ach / HBM_PEAK_GBS, "algorithmic_bytes_per_step": sg_bytes,
+                "ms_per_step": sg_ms, "ops": [k for k in SCATTER_GATHER_OPS if k in full],
+                "note": "SURVEY 8d bytes of all 6 PVConv voxelize/devoxelize calls, fwd + bwd, "
+                        "over the summed HIP-event time of every scatter/gather kernel incl. "
+                        "the segment plans"}
         log(f"{ms:.2f} ms/step, {value / 1e6:.3f} M points/s; losses {loss_p:.4f} {loss_z:.4f}")
         cham = None
         extra = {}
@@ -469,6 +509,7 @@ def main():
                        "global_batch": world * cfg.batch_size, "points_per_cloud": cfg.num_points,
                        "backbone": cfg.pf_backbone, "parallelism": f"dp{world}"},
             "roofline": roofline, "roofline_voxel_scatter_gather": roofline_scatter,
+            "roofline_voxel_scatter_gather_all": roofline_sg_all,
             "kernels": kernels, "cpu_baseline": cpu, "chamfer": cham, **extra,
             "loss_point": loss_p, "loss_latent": loss_z,
             "distributed": {"backend": dist.get_backend() if ddp else None,
