@@ -92,48 +92,6 @@ def _first_diff(a, b):
     return None if len(a) == len(b) else {"call": min(len(a), len(b)), "why": "lengths differ"}
 
 
-class _Stagger:
-    """Keeps the two ranks' GPU work from overlapping on the one shared GPU (a
-    rehearsal-only arrangement; the product runs one process per GPU).  With
-    two processes computing on one MI355X at once, this repository's
-    measurements found rare corrupted 16-lane chunks in the devoxelization's
-    output -- never with one process -- so rank 1 starts
-    its DDP step only once rank 0's step has no GPU work left but the gradient
-    exchange: a DDP communication hook on rank 0 sees the last bucket, a
-    helper thread waits for the device to drain and drops a flag file that
-    rank 1 polls for.  The all-reduce itself still runs across both ranks."""
-
-    def __init__(self, path, rank, dev, modules=3):
-        import threading
-        self.path, self.rank, self.dev = path, rank, dev
-        self.last = threading.Event()
-        self.pending = modules  # DDP modules whose last bucket is still to come
-        if rank == 0:
-            def drain():
-                self.last.wait()
-                torch.cuda.synchronize(dev)
-                open(path, "w").close()
-            self.thread = threading.Thread(target=drain, daemon=True)
-            self.thread.start()
-
-    def hook(self, state, bucket):
-        fut = dist.all_reduce(bucket.buffer(), async_op=True).get_future()
-        if self.rank == 0 and bucket.is_last():
-            self.pending -= 1
-            if self.pending == 0:
-                self.last.set()
-        return fut.then(lambda f: f.value()[0].div_(dist.get_world_size()))
-
-    def wait_turn(self):
-        import time
-        if self.rank == 1:
-            t0 = time.time()
-            while not os.path.exists(self.path):
-                if time.time() - t0 > 120:
-                    raise RuntimeError("rank 0's DDP step did not drain")
-                time.sleep(0.01)
-
-
 def grads(tr):
     return [p.grad.detach().clone() if p.grad is not None else None for p in tr._clip_params]
 
@@ -152,17 +110,9 @@ def main():
     if tracing:
         _trace_ops()
     runs, kept = {}, {}
-    staggered = os.environ.get("PCFM_DDP_STAGGER", "1") == "1"
-    stagger = _Stagger(f"{sys.argv[1]}.drained", rank, dev)
-    if staggered:
-        for m in (tr.model_enc, tr.model_pf, tr.model_lf):  # one hook per DDP module
-            m.register_comm_hook(None, stagger.hook)
-    else:
-        stagger.wait_turn = lambda: None
     TRACE = [] if tracing else None
     KEEP.clear()
     batch, draws = shard(cfg, rank, dev)
-    stagger.wait_turn()
     out = tr.forward_backward(batch, EPOCH, draws)
     g_ddp = grads(tr)
     torch.cuda.synchronize(dev)
@@ -175,8 +125,6 @@ def main():
         a.load_state_dict(b.state_dict())
     ref.train_mode()
     torch.cuda.synchronize(dev)
-    if rank == 1 and staggered:  # the reference runs one rank at a time (see _Stagger)
-        dist.barrier()
     per, ref_losses = [], []
     for s in range(world):
         ref.opt.zero_grad(set_to_none=True)
@@ -200,8 +148,6 @@ def main():
     runs["again"] = TRACE
     kept["again"] = list(KEEP)
     TRACE = None
-    if rank == 0 and staggered:
-        dist.barrier()
     trace_diff = None
     if tracing:
         # the forward differs only where an op is not reproducible (the backward
@@ -255,7 +201,7 @@ def main():
            "n_grads": n_grads, "differ": differ, "unreproducible": unrepro, "trace": trace_diff,
            "grad_sums_equal_across_ranks":
            all(torch.equal(gathered[0], g) for g in gathered),
-           "staggered": staggered, "cu_mask": os.environ.get("HSA_CU_MASK")}
+           "cu_mask": os.environ.get("HSA_CU_MASK")}
     from pcfm import ops
     if ops.devox_verify.enabled:
         res["devox_verify"] = ops.devox_verify.report()

@@ -1,6 +1,6 @@
 """Diagnosis of the devoxelization results that differed between identical runs
 when two ranks shared one GPU: runs the two-rank helper
-tests/helpers/ddp_grad_rank.py unstaggered with the in-stream self-check
+tests/helpers/ddp_grad_rank.py (ranks concurrent) with the in-stream self-check
 (PCFM_DEVOX_VERIFY=1: every devoxelization output recomputed in the plainest
 form right after the gather and compared bit for bit) and the op-level trace,
 once per variant, and prints one JSON line per run:
@@ -20,7 +20,7 @@ HELPER = os.path.join(REPO, "tests", "helpers", "ddp_grad_rank.py")
 
 
 def run(variant, k, port):
-    env = dict(os.environ, MASTER_ADDR="127.0.0.1", PCFM_DDP_STAGGER="0", PCFM_DEVOX_VERIFY="1",
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", PCFM_DEVOX_VERIFY="1",
                PCFM_DDP_TRACE="1")
     if variant == "cu_split":
         env["PCFM_DDP_CU_SPLIT"] = "1"

@@ -14,7 +14,7 @@
 #   traffic   FETCH_SIZE / WRITE_SIZE passes of the voxel ops (tools/pmc_traffic.sh)
 #   c5        bench.py at B=4, N=100000     -> gpurun_out/c5_train.json
 #   sample    bf16 Heun / dopri5 sampling bench  -> gpurun_out/sample_amp.json
-#   ddp       the two-rank DDP gradient test, unstaggered, once, with the
+#   ddp       the two-rank DDP tests, ranks concurrent on the one GPU, with the
 #             devoxelization self-check on   -> gpurun_out/ddp_check.log
 #   script:F  run python F (a measurement script of tools/) -> gpurun_out/F.jsonl
 set -e
@@ -53,7 +53,7 @@ for task in "$@"; do
     sample)
       timeout -k 10 300 python tools/sample_bench.py --amp > gpurun_out/sample_amp.json 2> gpurun_out/sample_amp.err ;;
     ddp)
-      PCFM_DDP_STAGGER=0 PCFM_DEVOX_VERIFY=1 timeout -k 10 400 python -u -m pytest \
+      PCFM_DEVOX_VERIFY=1 timeout -k 10 400 python -u -m pytest \
         tests/test_gpu_ddp.py -m gpu -v -rxX --timeout 300 --timeout-method thread \
         > gpurun_out/ddp_check.log 2>&1 ;;
     script:*)
