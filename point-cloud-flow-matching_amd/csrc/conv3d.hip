@@ -640,7 +640,10 @@ __global__ void __launch_bounds__(GN * 2)  // GK<KT, GN>::NW = GN / 32 waves
   // B pieces: I = BPW w + q -> image I / BPI (waves 0-3: hi, 4-7: lo)
   const uint16_t* bbase[G::BPW];
   const uint16_t* zbase[G::BPW];
-  int bxyz[G::BPW];  // x | y << 10 | z << 20 of the piece's voxel
+  // bit t: tap t's neighbour of the piece's voxel is inside the volume (all 0 for
+  // padding).  Built once, so a step selects its source with a bit test instead
+  // of three range checks (which hipcc compiled to exec-mask branches per piece)
+  uint32_t bval[G::BPW];
 #pragma unroll
   for (int q = 0; q < G::BPW; ++q) {
     const int I = G::BPW * w + q;
@@ -654,8 +657,16 @@ __global__ void __launch_bounds__(GN * 2)  // GK<KT, GN>::NW = GN / 32 waves
     const int cofs = (pch ^ G::swz(row)) << 3;
     bbase[q] = ((I / G::BPI) ? xl : xh) + (size_t)(gv >= 0 ? gv : 0) * 2 * K + cofs;
     zbase[q] = zrow + cofs;
-    // x = 1023 for padding: every tap's neighbour is out of the volume
-    bxyz[q] = gv >= 0 ? (v / R2) | (((v / R) % R) << 10) | ((v % R) << 20) : 1023;
+    const int x = v / R2, yy = (v / R) % R, z = v % R;
+    // per axis: bit (d + 1) set when coordinate + d is inside [0, R)
+    const uint32_t ax = (x > 0 ? 1u : 0u) | 2u | (x + 1 < R ? 4u : 0u);
+    const uint32_t ay = (yy > 0 ? 1u : 0u) | 2u | (yy + 1 < R ? 4u : 0u);
+    const uint32_t az = (z > 0 ? 1u : 0u) | 2u | (z + 1 < R ? 4u : 0u);
+    uint32_t m = 0u;
+#pragma unroll
+    for (int t = 0; t < 27; ++t)
+      m |= (((ax >> (t / 9)) & (ay >> ((t / 3) % 3)) & (az >> (t % 3))) & 1u) << t;
+    bval[q] = gv >= 0 ? m : 0u;
   }
 
   auto issue = [&](int sl, int buf) {
@@ -690,15 +701,14 @@ __global__ void __launch_bounds__(GN * 2)  // GK<KT, GN>::NW = GN / 32 waves
 #pragma unroll
     for (int q = 0; q < G::BPW; ++q) {
       const int I = G::BPW * w + q;
-      const int x = bxyz[q] & 1023, yy = (bxyz[q] >> 10) & 1023, z = bxyz[q] >> 20;
-      const bool inb = (unsigned)(x + dx) < (unsigned)R && (unsigned)(yy + dy) < (unsigned)R &&
-                       (unsigned)(z + dz) < (unsigned)R;
       // branch-free select of the source row (a divergent ?: on the pointer
       // compiled to an exec-mask branch around every piece)
       const unsigned long long src = (unsigned long long)(bbase[q] + bofs);
       const unsigned long long zsrc = (unsigned long long)zbase[q];
-      const unsigned long long msk = 0ull - (unsigned long long)inb;
-      glds16((const void*)((src & msk) | (zsrc & ~msk)),
+      const bool inb = (bval[q] >> tap) & 1u;
+      const uint32_t slo = inb ? (uint32_t)src : (uint32_t)zsrc;
+      const uint32_t shi = inb ? (uint32_t)(src >> 32) : (uint32_t)(zsrc >> 32);
+      glds16((const void*)(((unsigned long long)shi << 32) | slo),
              base + 2 * G::A + (I / G::BPI) * G::B + (I % G::BPI) * 1024);
     }
   };
