@@ -917,6 +917,218 @@ __device__ __forceinline__ void glds16_asm(const void* g, uint32_t lds) {
 }
 
 // ---------------------------------------------------------------------------
+// Forward / backward-data, SLAB form (r = 32, 16; dense unsplit launches).
+// Same tile (128 m x 256 voxels, 8 waves of 64 x 64), K-steps (32 channels,
+// chunk-major, taps 0..26 in order: the accumulation order of
+// conv3_igemm_glds_kernel, so the results are bit-identical) and A operand
+// (three-stage LDS-DMA ring of the weight slice) as the LDS-DMA kernel above.
+// The difference is the B operand.  There every step DMAs the tile's 256 input
+// rows shifted by its tap: 32 KiB per step, 2/3 of the bytes moved and 4 of the
+// 6 DMA pieces a wave issues per step (each piece costs 60-185 issue cycles,
+// MI355X_MICROARCH.md).  The 256 voxels of a tile are YT = 256 / R whole
+// z-rows of one x-plane, so the nine taps of one dx read rows of ONE 2-D slab
+// of the plane x + dx: y in [y0 - 1, y0 + YT], z in [-1, R] (zero rows at the
+// borders), 340 / 324 rows x 32 channels (hi | lo), 44 KiB.  The slab is
+// staged once per (chunk, dx) -- double-buffered, its 42-44 pieces spread one
+// per wave-step over the previous slab's nine steps -- and a tap (dy, dz) reads
+// its fragments at row offset dy (R + 2) + dz.  Per step a wave issues 2 A
+// pieces + 1 slab piece instead of 6, and the block moves 21 KiB instead of 48.
+// ---------------------------------------------------------------------------
+template <int R_>
+struct SlabGeo {
+  static constexpr int R = R_, R2 = R * R, V = R * R * R;
+  static constexpr int YT = 256 / R;                 // z-rows (y) per tile: 8 / 16
+  static constexpr int SZ = R + 2, SY = YT + 2;      // slab extent in z and y
+  static constexpr int NS = SY * SZ;                 // 340 / 324 rows
+  static constexpr int NSP = (NS + 15) / 16 * 16;    // whole 16-row pieces
+  static constexpr int PPI = NSP / 16;               // pieces per image (22 / 21)
+  static constexpr int PIECES = 2 * PPI;             // hi + lo
+  static constexpr int WQ = (PIECES + 7) / 8;        // slab pieces per wave (6)
+  static constexpr int IMG = NSP * 64;               // bytes of one image (64-B rows)
+  static constexpr int SLAB = 2 * IMG;
+  static constexpr int ASTAGE = GK<32>::STAGE - 2 * GK<32>::B;  // A hi | lo: 16 KiB
+  static constexpr int LDS = 3 * ASTAGE + 2 * SLAB;
+  static_assert(R * YT == 256 && LDS <= 160 * 1024 && WQ <= 9, "slab geometry");
+};
+
+template <int R_>
+__global__ void __launch_bounds__(512)
+    conv3_igemm_slab_kernel(const uint16_t* __restrict__ xh, const uint16_t* __restrict__ wh,
+                            const uint16_t* __restrict__ zrow, const float* __restrict__ bias,
+                            float* __restrict__ y, int K, int M) {
+  using G = GK<32>;
+  using SG = SlabGeo<R_>;
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  uint8_t* aring = lds;                       // 3 x (A hi | A lo)
+  uint8_t* slabs = lds + 3 * SG::ASTAGE;      // 2 x (slab hi | slab lo)
+  constexpr int R = SG::R, R2 = SG::R2, V = SG::V;
+  const int nmt = M / kGM, nvt = V / 256;
+  int id = (int)blockIdx.x;
+  {
+    const int nwg = (int)gridDim.x, q = nwg / 8, rr = nwg % 8, xcd = id % 8;
+    id = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + id / 8;
+  }
+  const int m0 = (id % nmt) * kGM;
+  id /= nmt;
+  const int v0 = (id % nvt) * 256;
+  const int b = id / nvt;
+  const int x0 = v0 / R2, y0 = (v0 % R2) / R;
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wr = w / 4, wc = w % 4, r = lane & 31, h = lane >> 5;
+  const int nck = K / 32, T = 27 * nck;
+  const int prow = lane / G::CPR, pch = lane % G::CPR;
+  const uint16_t* __restrict__ wl = wh + kSplitLo;
+
+  // A pieces (as the LDS-DMA kernel): I = APW w + q -> image I / API, rows (I % API) * RPP + prow
+  const uint16_t* abase[G::APW];
+#pragma unroll
+  for (int q = 0; q < G::APW; ++q) {
+    const int I = G::APW * w + q;
+    const int row = (I % G::API) * G::RPP + prow;
+    abase[q] = ((I / G::API) ? wl : wh) + (size_t)(m0 + row) * 2 * K + ((pch ^ G::swz(row)) << 3);
+  }
+  // this lane's B fragment rows at tap (0, 0): slab row (yl + 1) SZ + z + 1
+  int brow[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int col = wc * 64 + j * 32 + r;
+    brow[j] = (col / R + 1) * SG::SZ + (col % R) + 1;
+  }
+  const size_t bV = (size_t)b * V;
+
+  // slab sl = (chunk, dx) -> slab buffer sbuf; q: this wave's piece
+  // piece q of this wave (I = w + 8 q; a wave with no piece q re-issues its
+  // piece 0: same bytes) of slab sl -> slab buffer sbuf.  Lane -> slab row
+  // 16 P + prow (y' = y0 - 1 + row / SZ, z' = row % SZ - 1), physical chunk pch;
+  // rows outside the volume or past the slab's NS rows read the zero row.
+  // Recomputed per step (a per-q table indexed by the runtime q went to scratch)
+  auto slab_piece = [&](int sl, int q, int sbuf) {
+    int I = w + 8 * q;
+    if (I >= SG::PIECES) I = w;
+    const int img = I / SG::PPI, P = I % SG::PPI;
+    const int row = 16 * P + prow;
+    const int ys = row / SG::SZ, zs = row - ys * SG::SZ;
+    const int yy = y0 - 1 + ys, zz = zs - 1;
+    const int c0 = (sl / 3) * 32, xx = x0 + sl % 3 - 1;
+    const bool ok = (unsigned)xx < (unsigned)R && row < SG::NS && (unsigned)yy < (unsigned)R &&
+                    (unsigned)zz < (unsigned)R;
+    const int cofs = img * 32 + ((pch ^ G::swz(row)) << 3);
+    // the plane's first row (uniform; an out-of-volume plane is never read)
+    const uint16_t* plane = xh + (bV + (size_t)(xx < 0 ? 0 : xx) * R2) * 2 * K + 2 * c0;
+    const unsigned long long src = (unsigned long long)(plane + (yy * R + zz) * 2 * K + cofs);
+    const unsigned long long zs64 = (unsigned long long)(zrow + (cofs & 31));
+    const uint32_t slo = ok ? (uint32_t)src : (uint32_t)zs64;
+    const uint32_t shi = ok ? (uint32_t)(src >> 32) : (uint32_t)(zs64 >> 32);
+    glds16((const void*)(((unsigned long long)shi << 32) | slo),
+           slabs + sbuf * SG::SLAB + img * SG::IMG + P * 1024);
+  };
+  auto a_pieces = [&](int s, int buf) {
+    const int c0 = (s / 27) * 32, tap = s % 27;
+    const int cof = ((c0 >> 5) << 6) + (c0 & 31);
+    const size_t aofs = (size_t)tap * M * 2 * K + cof;
+#pragma unroll
+    for (int q = 0; q < G::APW; ++q) {
+      const int I = G::APW * w + q;
+      glds16(abase[q] + aofs, aring + buf * SG::ASTAGE + (I / G::API) * G::A + (I % G::API) * 1024);
+    }
+  };
+  // fragments of a step: A from ring slot `ring`, B from slab buffer `sbuf` at
+  // the offset of the slab's tap u = 3 (dy + 1) + dz + 1
+  auto frags = [&](int ring, int u, int sbuf, bf16x8 (&F)[2][8]) {
+    const uint8_t* ab = aring + ring * SG::ASTAGE;
+    const int toff = (u / 3 - 1) * SG::SZ + (u % 3 - 1);
+    const uint8_t* sb = slabs + sbuf * SG::SLAB;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int kc = 2 * kk + h;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int row = wr * 64 + i * 32 + r;
+        const int off = row * G::RB + ((kc ^ G::swz(row)) << 4);
+        F[kk][i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(ab + off));
+        F[kk][2 + i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(ab + G::A + off));
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int row = brow[j] + toff;
+        const int off = row * G::RB + ((kc ^ G::swz(row)) << 4);
+        F[kk][4 + j] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(sb + off));
+        F[kk][6 + j] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(sb + SG::IMG + off));
+      }
+    }
+  };
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
+
+  const int nslab = 3 * nck;  // even (nck even: the launcher's condition)
+  // prologue: slab 0 whole, A of steps 0..2
+#pragma unroll
+  for (int q = 0; q < SG::WQ; ++q) slab_piece(0, q, 0);
+  a_pieces(0, 0);
+  a_pieces(1, 1);
+  a_pieces(2, 2);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  bf16x8 F[2][2][8];
+  frags(0, 0, 0, F[0]);
+  // step s: its fragments are in Fc; read step s + 1's (past the end: unused),
+  // run step s's MFMAs, DMA A of step s + 3 into ring s % 3 and one piece of
+  // the next slab.  Every step issues exactly APW + 1 pieces (the extra ones
+  // re-issue data that is already there or never read again), so the wait at
+  // the next step's top is one immediate.
+  auto step = [&](int s, bf16x8 (&Fc)[2][8], bf16x8 (&Fn)[2][8]) {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::APW + 1) : "memory");
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+    __builtin_amdgcn_s_barrier();
+    const int sl = s / 9, u = s - 9 * sl;
+    const int un = u == 8 ? 0 : u + 1;
+    frags((s + 1) % 3, un, (sl + (u == 8 ? 1 : 0)) & 1, Fn);
+    glds_mfma<32>(Fc, acc);
+    a_pieces(min(s + 3, T - 1), s % 3);
+    slab_piece(min(sl + 1, nslab - 1), min(u, SG::WQ - 1), (sl + 1) & 1);
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+    }
+#pragma unroll
+    for (int g = 0; g < G::APW + 1; ++g) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x008, 16 - 4 * (G::APW + 1), 0);
+  };
+  for (int s = 0; s < T; s += 2) {  // T = 27 nck is even (nck even)
+    step(s, F[0], F[1]);
+    step(s + 1, F[1], F[0]);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may outlive the wave
+
+  float* __restrict__ yb = y + (size_t)b * M * V;
+  float biasv[2][16];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) load_bias16(bias, m0 + wr * 64 + i * 32, h, M, biasv[i]);
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      float* ycol = yb + v0 + wc * 64 + j * 32 + r;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int m = m0 + wr * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+        nt_st(acc[i][j][e] + biasv[i][e], ycol + (size_t)m * V);
+      }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Forward / backward-data, BRICK form (r = 32, 16; unsplit launches).  The
 // LDS-DMA kernel above fetches its B operand (the 256 input rows a tap
 // reads) once per tap: 27 re-fetches of nearly the same rows per channel
@@ -1972,6 +2184,13 @@ static bool conv_brick() {
   return on;
 }
 
+// Slab form of the dense r = 32 / 16 launches (PCFM_CONV_SLAB=0: the LDS-DMA
+// kernel that refetches B per tap)
+static bool conv_slab() {
+  const char* e = getenv("PCFM_CONV_SLAB");  // read per call: tests compare both forms
+  return e == nullptr || e[0] != '0';
+}
+
 static bool list_gn128(long long blocks256) {
   static const int mode = [] {
     const char* e = getenv("PCFM_CONV_LIST_GN");
@@ -2050,6 +2269,19 @@ static int igemm_cl(const void* xs, const void* wsplit, const float* bias, int b
       else
         hipLaunchKernelGGL(conv3_igemm_brick_kernel<16>, dim3((unsigned)glds_blocks), dim3(512),
                            BrickGeo<16>::LDS, st, xh, wh, zrow, bias, y, cin, cout);
+      return check_launch("conv3d_igemm_cl");
+    }
+    if (S == 1 && mm == 0 && vl == nullptr && cin % 64 == 0 && (r == 32 || r == 16) &&
+        conv_slab()) {  // cin % 64: an even number of 32-channel chunks (the step loop's pairs)
+      const int e = r == 32 ? allow_big_lds((const void*)conv3_igemm_slab_kernel<32>)
+                            : allow_big_lds((const void*)conv3_igemm_slab_kernel<16>);
+      if (e) return e;
+      if (r == 32)
+        hipLaunchKernelGGL(conv3_igemm_slab_kernel<32>, dim3((unsigned)glds_blocks), dim3(512),
+                           SlabGeo<32>::LDS, st, xh, wh, zrow, bias, y, cin, cout);
+      else
+        hipLaunchKernelGGL(conv3_igemm_slab_kernel<16>, dim3((unsigned)glds_blocks), dim3(512),
+                           SlabGeo<16>::LDS, st, xh, wh, zrow, bias, y, cin, cout);
       return check_launch("conv3d_igemm_cl");
     }
     if (S == 1 && PCFM_CONV_GK == 32 && cin % 32 == 0 && vl == nullptr && conv_pp()) {

@@ -105,3 +105,43 @@ def test_voxel_conv_module_matches_conv3d(ops):
                  (ref.bias.grad, mod.bias.grad)):
         a64 = a.detach().double().cpu()
         assert _rel(b, a64) < 2 * TOL
+
+
+@pytest.mark.parametrize("b,cin,cout,r", [(2, 128, 128, 32), (2, 256, 256, 16), (1, 128, 256, 16),
+                                          (1, 256, 128, 32)])
+def test_slab_form_is_bit_identical(ops, monkeypatch, b, cin, cout, r):
+    """The slab form of the dense r = 32 / 16 GEMM (conv3_igemm_slab_kernel: B from a
+    per-(chunk, dx) 2-D slab in LDS) runs the LDS-DMA kernel's K-steps in the same
+    order with the same operands: forward and backward-data outputs bit-identical,
+    including the volume's border voxels (zero rows of the slab)."""
+    g = torch.Generator(device="cuda").manual_seed(7 * r + cin)
+    x = torch.randn(b, cin, r, r, r, device="cuda", generator=g)
+    w = torch.randn(cout, cin, 3, 3, 3, device="cuda", generator=g) / (27 * cin) ** 0.5
+    bias = torch.randn(cout, device="cuda", generator=g)
+    xs = ops.conv3d_split(x)
+    img, imgt = ops.conv3d_prep_weight(w, False), ops.conv3d_prep_weight(w, True)
+    gys = ops.conv3d_split(torch.randn(b, cout, r, r, r, device="cuda", generator=g))
+    out = {}
+    for slab in ("1", "0"):
+        monkeypatch.setenv("PCFM_CONV_SLAB", slab)
+        out[slab] = (ops.conv3d_igemm_split(xs, img, bias, b, cin, cout, r, "t"),
+                     ops.conv3d_igemm_split(gys, imgt, None, b, cout, cin, r, "t"))
+    assert torch.equal(out["1"][0], out["0"][0])
+    assert torch.equal(out["1"][1], out["0"][1])
+    y64 = torch.nn.functional.conv3d(x.double().cpu(), w.double().cpu(), bias.double().cpu(),
+                                     padding=1)
+    assert _rel(out["1"][0], y64) < TOL
+
+
+@pytest.mark.parametrize("r", [16, 32])
+def test_slab_form_padding_counts(ops, r):
+    """All-ones input and kernel at the slab form's resolutions: every output is the
+    number of in-grid neighbours times C (zero rows at all six faces)."""
+    c = 128
+    x = torch.ones(1, c, r, r, r, device="cuda")
+    w = torch.ones(c, c, 3, 3, 3, device="cuda")
+    y = ops.conv3d_forward(x, w, None)
+    idx = torch.arange(r, device="cuda")
+    n1 = 3 - (idx == 0).int() - (idx == r - 1).int()
+    cnt = (n1[:, None, None] * n1[None, :, None] * n1[None, None, :]).float() * c
+    assert torch.equal(y[0, 0], cnt) and torch.equal(y[0, c - 1], cnt)
