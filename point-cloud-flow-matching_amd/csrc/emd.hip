@@ -9,7 +9,8 @@
 //   * every pass of every level is a full-chip launch: lanes own rows, the
 //     inner (column) loop is wave-uniform so the column points arrive through
 //     scalar loads, and the column range is split S ways into a partial-sum
-//     buffer that a small finalize kernel reduces in a fixed order;
+//     buffer that the NEXT phase reduces in a fixed order while it stages its
+//     column coefficients (the finalize folded in: 33 launches per approxmatch);
 //   * match is NOT accumulated level by level.  Each level only needs the
 //     vectors ratioL (n) and ratioR (m), which are kept per level (10 x (n+m));
 //     match is written once at the end as
@@ -20,8 +21,6 @@
 //   * exp is the hardware exp2 on x*log2(e): the reference is built with
 //     --use_fast_math (__expf, backend.py:20), so EMD parity is tolerance-based.
 #include "pcfm_common.hpp"
-
-#include <hip/hip_cooperative_groups.h>
 
 #include <algorithm>
 #include <cstdlib>
@@ -341,13 +340,12 @@ inline dim3 grid1d(size_t total, int threads = 256) {
 }
 
 // ---------------------------------------------------------------------------
-// Persistent form: the whole auction (10 levels) + the match write in ONE
-// cooperative launch, the levels' phases separated by grid barriers instead of
-// kernel boundaries.  At the metric's sizes (B = 8, N = 2048: 33 M exp per
-// pass, ~1 us of v_exp issue) every pass of the multi-launch form above is
-// launch/drain bound; here a level is 3 barriers.  Same per-element
-// expressions and the same partial-sum order as the multi-launch form, so the
-// two are bit-identical (tests/test_gpu_ops.py::test_emd_persistent_bit_identical).
+// Phase form (the default): one launch per phase of each level.  The round-3
+// form ran the whole auction as ONE cooperative launch with grid barriers
+// between the phases; it was bit-identical but 6x slower (4.5 vs 0.75 ms at
+// B = 8, N = 2048): hipLaunchCooperativeKernel and its grid barriers cost more
+// than the launches they replaced, so it is gone.  What it did keep is used
+// here: the split form's finalize kernels disappear into the phases.
 //
 // Each finalize is folded into the phase that consumes it:
 //   P1 (rows k, cols l, coef remR)            -> partA;  also level j-1's fin3
@@ -454,94 +452,44 @@ __device__ void p_pass(const EmdPState<T>& s, const EmdPlan& p, int ph, int lvl,
   }
 }
 
+// One phase of one level per launch: the unit loop of p_pass over (row tile,
+// split, b), each finalize folded into the phase that consumes it.  30 phase
+// launches + init + the last level's levL + the match write: half the
+// launches of the split form below, whose every pass and every finalize is
+// its own launch (at B = 8, N = 2048 the passes are ~1 us of exp issue each,
+// so launches, not exps, set the time).  Same per-element expressions and
+// partial-sum order: bit-identical to the split form
+// (tests/test_gpu_ops.py::test_emd_phase_form_bit_identical).
 template <typename T>
 __global__ void __launch_bounds__(kThreads)
-    emd_persistent_kernel(EmdPState<T> s, EmdPlan p) {
+    emd_phase_kernel(EmdPState<T> s, EmdPlan p, int ph, int lvl) {
   __shared__ T lcoef[kPChunk];
-  cooperative_groups::grid_group grid = cooperative_groups::this_grid();
-  const size_t bn = (size_t)p.b * p.n, bm = (size_t)p.b * p.m;
-  const size_t gtid = (size_t)blockIdx.x * kThreads + threadIdx.x;
-  const size_t gstride = (size_t)gridDim.x * kThreads;
-  for (size_t i = gtid; i < (bn > bm ? bn : bm); i += gstride) {  // emd_init_kernel
-    if (i < bn) s.remL[i] = s.multiL;
-    if (i < bm) s.remR[0][i] = s.multiR;
-  }
-  grid.sync();
-  for (int lvl = 0; lvl < kLevels; ++lvl) {
-    for (int ph = 0; ph < 3; ++ph) {
-      p_pass(s, p, ph, lvl, lcoef);
-      grid.sync();
-    }
-  }
-  for (size_t k = gtid; k < bn; k += gstride)  // the last level's fin3 (levL only)
-    s.levL[(size_t)(kLevels - 1) * bn + k] = s.ratL[k];
-  grid.sync();
-  // emd_match_kernel's units: (k tile, l group of kLPer, b)
-  const int lgroups = (p.m + kLPer - 1) / kLPer;
-  const int units = p.tilesN * lgroups * p.b;
-  for (int u = blockIdx.x; u < units; u += gridDim.x) {
-    const int tile = u % p.tilesN;
-    const int lg = (u / p.tilesN) % lgroups;
-    const int bb = u / (p.tilesN * lgroups);
-    const int k = tile * kThreads + threadIdx.x;
-    const int kk = k < p.n ? k : p.n - 1;
-    const T* p1 = s.xyz1 + ((size_t)bb * p.n + kk) * 3;
-    const T x1 = p1[0], y1 = p1[1], z1 = p1[2];
-    T rl[kLevels];
-#pragma unroll
-    for (int j = 0; j < kLevels; ++j) rl[j] = s.levL[(size_t)j * bn + (size_t)bb * p.n + kk];
-    const int l0 = lg * kLPer, l1 = min(p.m, l0 + kLPer);
-    for (int l = l0; l < l1; ++l) {
-      const T* p2 = s.xyz2 + ((size_t)bb * p.m + l) * 3;
-      const T d2 = sqdist3(p2[0] - x1, p2[1] - y1, p2[2] - z1);
-      T acc = 0;
-#pragma unroll
-      for (int j = 0; j < kLevels; ++j) {
-        const T rr = s.levR[(size_t)j * bm + (size_t)bb * p.m + l];
-        const T e = emd_exp<T>((T)c_levels[j] * d2);
-        acc += (e * rl[j]) * rr;
-      }
-      if (k < p.n) s.match[((size_t)bb * p.m + l) * p.n + k] = acc;
-    }
-  }
-}
-
-bool emd_persistent_enabled() {
-  static const bool on = [] {
-    // opt-in (PCFM_EMD_PERSISTENT=1): bit-identical, but measured 6x slower than
-    // the multi-launch form at B = 8 (N = 2048: 4.5 vs 0.75 ms forward,
-    // profiles/r03_bench.json vs r02) -- the grid barriers cost more than the
-    // launches they replace
-    const char* e = std::getenv("PCFM_EMD_PERSISTENT");
-    return e != nullptr && std::atoi(e) != 0;
-  }();
-  return on;
+  p_pass(s, p, ph, lvl, lcoef);
 }
 
 template <typename T>
-int approxmatch_persistent(const T* xyz1, const T* xyz2, int b, int n, int m, T* match,
-                           EmdWs<T> w, int S, hipStream_t st, bool* launched) {
-  *launched = false;
-  const void* fn = (const void*)emd_persistent_kernel<T>;
-  int dev = 0, per_cu = 0, cus = 0, coop = 0;
-  if (hipGetDevice(&dev) != hipSuccess ||
-      hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, dev) != hipSuccess ||
-      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kThreads, 0) != hipSuccess ||
-      coop == 0 || per_cu <= 0) {
-    (void)hipGetLastError();
-    return PCFM_OK;  // caller runs the multi-launch form
-  }
+__global__ void emd_levlast_kernel(const T* __restrict__ ratL, size_t bn, T* __restrict__ levL) {
+  const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < bn) levL[k] = ratL[k];  // the last level's fin3 (levL only)
+}
+
+// PCFM_EMD_FORM=split: every pass and finalize its own launch (measurement /
+// the bit-identity test); default: the phase form
+bool emd_split_form() {
+  const char* e = std::getenv("PCFM_EMD_FORM");
+  return e != nullptr && e[0] == 's';
+}
+
+template <typename T>
+int approxmatch_phases(const T* xyz1, const T* xyz2, int b, int n, int m, T* match, EmdWs<T> w,
+                       int S, hipStream_t st) {
   EmdPlan p{b, n, m, S, ceil_div(n, kThreads), ceil_div(m, kThreads)};
-  const long long want = (long long)std::max(p.tilesN, p.tilesM) * S * b;
-  // at most what is co-resident (a grid barrier needs every block resident)
-  const int blocks = (int)std::max(1LL, std::min(want, (long long)per_cu * cus));
   EmdPState<T> s;
   s.xyz1 = xyz1;
   s.xyz2 = xyz2;
   s.remL = w.remL;
   s.remR[0] = w.remR;
-  s.remR[1] = w.ratR;  // the multi-launch form's ratioR buffer: free here (ratR lives in LDS)
+  s.remR[1] = w.ratR;  // the split form's ratioR buffer: free here (ratR is per column on the fly)
   s.ratL = w.ratL;
   s.levL = w.levL;
   s.levR = w.levR;
@@ -552,13 +500,19 @@ int approxmatch_persistent(const T* xyz1, const T* xyz2, int b, int n, int m, T*
   s.match = match;
   s.multiL = n >= m ? (T)1 : (T)(m / n);
   s.multiR = n >= m ? (T)(n / m) : (T)1;
-  void* args[] = {&s, &p};
-  hipError_t e = hipLaunchCooperativeKernel(fn, dim3(blocks), dim3(kThreads), args, 0, st);
-  if (e != hipSuccess) {
-    set_error("approxmatch: hipLaunchCooperativeKernel: %s", hipGetErrorString(e));
-    return (int)e;
-  }
-  *launched = true;
+  const size_t bn = (size_t)b * n, bm = (size_t)b * m;
+  hipLaunchKernelGGL(emd_init_kernel<T>, grid1d(std::max(bn, bm)), dim3(256), 0, st, w.remL, bn,
+                     s.multiL, w.remR, bm, s.multiR);
+  const unsigned unitsL = (unsigned)p.tilesN * S * b, unitsR = (unsigned)p.tilesM * S * b;
+  for (int lvl = 0; lvl < kLevels; ++lvl)
+    for (int ph = 0; ph < 3; ++ph)
+      hipLaunchKernelGGL(emd_phase_kernel<T>, dim3(ph == 1 ? unitsR : unitsL), dim3(kThreads), 0,
+                         st, s, p, ph, lvl);
+  hipLaunchKernelGGL(emd_levlast_kernel<T>, grid1d(bn), dim3(256), 0, st, (const T*)w.ratL, bn,
+                     w.levL + (size_t)(kLevels - 1) * bn);
+  dim3 gm(ceil_div(n, kThreads), ceil_div(m, kLPer), b);
+  hipLaunchKernelGGL(emd_match_kernel<T>, gm, dim3(kThreads), 0, st, xyz1, xyz2, b, n, m, w.levL,
+                     w.levR, match);
   return check_launch("approxmatch");
 }
 
@@ -572,11 +526,7 @@ int approxmatch(const T* xyz1, const T* xyz2, int b, int n, int m, T* match, voi
   if (b == 0 || n == 0 || m == 0) return PCFM_OK;
   EmdWs<T> w = carve<T>(ws, b, n, m);
   const int S = emd_splits(b, n, m);
-  if (emd_persistent_enabled()) {
-    bool launched = false;
-    const int rc = approxmatch_persistent(xyz1, xyz2, b, n, m, match, w, S, st, &launched);
-    if (rc != PCFM_OK || launched) return rc;
-  }
+  if (!emd_split_form()) return approxmatch_phases(xyz1, xyz2, b, n, m, match, w, S, st);
   // multiL/multiR: integer ratio of the cloud sizes (:27-33)
   const T multiL = n >= m ? (T)1 : (T)(m / n);
   const T multiR = n >= m ? (T)(n / m) : (T)1;

@@ -421,25 +421,26 @@ def test_chamfer_c2_product_path(tmp_path, report):
     assert d["bwd_close"], d
 
 
-def test_emd_persistent_bit_identical(tmp_path, report):
-    """The one-launch cooperative approxmatch (grid barriers between the
-    levels' phases, finalizes folded into the consuming phase) against the
-    multi-launch form: bit-identical matches over f32/f64, n >< m and ragged
-    sizes (tests/helpers/emd_forms.py; emd_kernel.cu:24-156)."""
+def test_emd_phase_form_bit_identical(tmp_path, report):
+    """approxmatch's phase form (one launch per phase of each level, the
+    finalizes folded into the consuming phase: 33 launches) against the split
+    form (every pass and finalize its own launch: 62): bit-identical matches
+    over f32/f64, n >< m and ragged sizes (tests/helpers/emd_forms.py;
+    emd_kernel.cu:24-156), and the launch time of each at B=8, N=2048."""
     import json
     import os
     import subprocess
     import sys
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     res = {}
-    for mode in ("0", "1"):
-        env = dict(os.environ, PCFM_EMD_PERSISTENT=mode)
+    for form in ("split", "phase"):
+        env = dict(os.environ, PCFM_EMD_FORM=form)
         subprocess.run([sys.executable, os.path.join(repo, "tests", "helpers", "emd_forms.py"),
-                        str(tmp_path / f"m{mode}.npz"), str(tmp_path / f"t{mode}.json")],
+                        str(tmp_path / f"m{form}.npz"), str(tmp_path / f"t{form}.json")],
                        check=True, timeout=120, env=env, cwd=repo)
-        res[mode] = json.load(open(tmp_path / f"t{mode}.json"))
-    a, b = np.load(tmp_path / "m0.npz"), np.load(tmp_path / "m1.npz")
+        res[form] = json.load(open(tmp_path / f"t{form}.json"))
+    a, b = np.load(tmp_path / "msplit.npz"), np.load(tmp_path / "mphase.npz")
     for k in a.files:
         np.testing.assert_array_equal(a[k], b[k], err_msg=k)
-    report("emd_persistent", {"multi_launch_ms": res["0"]["approxmatch_ms_b8_n2048"],
-                              "persistent_ms": res["1"]["approxmatch_ms_b8_n2048"]})
+    report("emd_forms", {"split_ms": res["split"]["approxmatch_ms_b8_n2048"],
+                         "phase_ms": res["phase"]["approxmatch_ms_b8_n2048"]})
