@@ -1794,27 +1794,43 @@ __global__ void __launch_bounds__(kW3Threads)
 
   // LDS-DMA pieces of this wave: I = w + 12 q; lane -> (row 4P + lane / 16,
   // physical chunk lane % 16 = logical chunk ^ swizzle): the swz256 image is
-  // produced by choosing the source chunk.
+  // produced by choosing the source chunk.  The lane's part of each source
+  // address (its row within the step's rows, its chunk, hi / lo) is fixed:
+  // built once here, so a step adds one uniform row base (and for X clamps the
+  // row) instead of a 64-bit split_off per piece.
+  int prow_[kW3Q], pofs[kW3Q];
+#pragma unroll
+  for (int q = 0; q < kW3Q; ++q) {
+    const int I = w + (kW3Threads / 64) * q;
+    const bool isA = I < 2 * kW3APieces;
+    const int I2 = isA ? I : I - 2 * kW3APieces;
+    const int np = isA ? kW3APieces : kW3BPieces;
+    const int img = I2 / np, P = I2 % np;
+    const int row = 4 * P + (lane >> 4);
+    const int ch = (lane & 15) ^ (((row & 3) << 2) | ((row >> 2) & 3));
+    const int c = (isA ? co0 : ci0) + ch * 8;
+    prow_[q] = row;
+    // dY pieces: the whole in-step offset (the row is never clamped)
+    pofs[q] = ((c >> 5) << 6) + (c & 31) + (img ? kSplitLo : 0) + (isA ? row * 2 * cout : 0);
+  }
   auto issue = [&](int b, int v0, uint8_t* buf) {
     const size_t base = (size_t)b * V;
+    const uint16_t* ga = gh + (base + v0) * 2 * cout;  // dY rows of the step
+    const uint16_t* xb = xh + base * 2 * cin;
+    const int g0 = v0 + off - 1;  // X row of the halo's first row
 #pragma unroll
     for (int q = 0; q < kW3Q; ++q) {
       const int I = w + (kW3Threads / 64) * q;
       if (I < 2 * kW3APieces) {
         const int img = I / kW3APieces, P = I % kW3APieces;
-        const int row = 4 * P + (lane >> 4);
-        const int ch = (lane & 15) ^ (((row & 3) << 2) | ((row >> 2) & 3));
-        const uint16_t* src = (img ? gl : gh) + split_off(base + v0 + row, co0 + ch * 8, cout);
-        glds16_asm(src, lds_addr(buf + img * kW3AImg + P * 1024));
+        glds16_asm(ga + pofs[q],
+                   lds_addr(buf + img * kW3AImg + P * 1024));
       } else if (I < kW3Pieces) {
         const int I2 = I - 2 * kW3APieces;
         const int img = I2 / kW3BPieces, P = I2 % kW3BPieces;
-        const int row = 4 * P + (lane >> 4);
-        const int ch = (lane & 15) ^ (((row & 3) << 2) | ((row >> 2) & 3));
-        int gv = v0 + off - 1 + row;
-        gv = gv < 0 ? 0 : (gv >= V ? V - 1 : gv);  // out-of-volume rows are masked at use
-        const uint16_t* src = (img ? xl : xh) + split_off(base + gv, ci0 + ch * 8, cin);
-        glds16_asm(src, lds_addr(buf + 2 * kW3AImg + img * kW3BImg + P * 1024));
+        const int gv = min(max(g0 + prow_[q], 0), V - 1);  // out-of-volume rows are masked at use
+        glds16_asm(xb + ((size_t)gv * 2 * cin + pofs[q]),
+                   lds_addr(buf + 2 * kW3AImg + img * kW3BImg + P * 1024));
       }
     }
   };

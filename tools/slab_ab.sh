@@ -11,3 +11,5 @@ for rep in 1 2; do
     python -c "import json; d=json.load(open('gpurun_out/lib_one.json')); print(json.dumps({'slab': $S, 'ms': d['ms_per_step'], 'frac': d['roofline']['frac']}))" >> gpurun_out/slab_ab.jsonl
   done
 done
+timeout -k 10 300 python -u -m pytest tests/test_gpu_ops.py -m gpu -x -v -k "emd" --timeout 120 --timeout-method thread > gpurun_out/pytest_emd.log 2>&1
+PCFM_REPORT=gpurun_out/emd_report.json timeout -k 10 200 python -u -m pytest tests/test_gpu_ops.py -m gpu -q -k "emd_phase" --timeout 120 --timeout-method thread >> gpurun_out/pytest_emd.log 2>&1
