@@ -45,7 +45,8 @@ extern "C" {
  * points take the module's num_batches_tracked counter; 13: occupancy-masked
  * voxel convolution entry points; 14: voxel-list form of the voxel convolution;
  * 15: the head FiLM backward takes shift and recomputes u; 16: devoxelization
- * self-check entry point). */
+ * self-check entry point; 17: BatchNorm statistics from the pointwise GEMM's
+ * epilogue). */
 int pcfm_abi_version(void);
 /* Thread-local text of the last non-zero return code. */
 const char* pcfm_last_error(void);
@@ -474,6 +475,23 @@ int pcfm_bn_act_fwd(const float* x, const float* gamma, const float* beta, int b
                     float eps, float slope, float momentum, float* running_mean,
                     float* running_var, long long* num_batches_tracked, float* y, float* mean,
                     float* invstd, void* ws, size_t ws_bytes, void* stream);
+
+/* SharedMLP layer forward with the BatchNorm statistics produced by the GEMM
+ * (shared_mlp.py:21-25: Conv1d -> BatchNorm1d -> ReLU).  For the shapes where
+ * pcfm_pointwise_bnstats_groups(b, cin, cout, n) = P > 0,
+ * pcfm_pointwise_gemm_bnstats writes y = W x + bias as pcfm_pointwise_gemm and
+ * stats f32 [cout][P][2]: per 64-point group (mean, centred sum of squares);
+ * pcfm_bn_act_fwd_parts then finalizes them (fixed order, deterministic) and
+ * applies the BatchNorm + activation like pcfm_bn_act_fwd, without a
+ * statistics pass over y. */
+int pcfm_pointwise_bnstats_groups(int b, int cin, int cout, int n);
+int pcfm_pointwise_gemm_bnstats(const float* x, const void* wsplit, const float* bias, int b,
+                                int cin, int cout, int n, float* y, float* stats, void* stream);
+int pcfm_bn_act_fwd_parts(const float* x, const float* part, int P, const float* gamma,
+                          const float* beta, int b, int c, int s, float eps, float slope,
+                          float momentum, float* running_mean, float* running_var,
+                          long long* num_batches_tracked, float* y, float* mean, float* invstd,
+                          void* stream);
 
 /* Backward of pcfm_bn_act_fwd given dz = dL/dy: dx [b][c][s] and
  * dgamma / dbeta [c] (all fully written); if dbias_in is non-NULL it receives

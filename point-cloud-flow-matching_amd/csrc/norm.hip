@@ -167,6 +167,53 @@ __device__ __forceinline__ void bn_bwd_fin(const float* part, int P, int c, floa
   }
 }
 
+// Statistics from a producer's epilogue (pw_gemm256_kernel with stats): part
+// float2 [C][P], the (mean, centred sum of squares) of P groups of up to 64
+// values, group p holding min(64, S - (p % G) 64) values (G = ceil(S / 64)).
+// One wave per channel: lane l combines groups l, l + 64, ... in order (Chan's
+// update, fp64), then a fixed xor tree; lane 0 publishes mean / invstd and the
+// running statistics exactly as BnFwdFin::publish.  Deterministic.
+__global__ void __launch_bounds__(64)
+    bn_fin_parts_kernel(const float2* __restrict__ part, int P, int S, float eps, float momentum,
+                        float* __restrict__ rmean, float* __restrict__ rvar,
+                        long long* __restrict__ nbt, float* __restrict__ mean,
+                        float* __restrict__ invstd) {
+  const int c = blockIdx.x, l = threadIdx.x;
+  const int G = (S + 63) / 64;
+  double n = 0.0, mu = 0.0, m2 = 0.0;
+  for (int p = l; p < P; p += 64) {
+    const float2 v = part[(size_t)c * P + p];
+    const double nb = (double)min(64, S - (p % G) * 64);
+    const double nn = n + nb, d = (double)v.x - mu;
+    mu += d * nb / nn;
+    m2 += (double)v.y + d * d * n * nb / nn;
+    n = nn;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const double nb = __shfl_xor(n, o, 64), mb = __shfl_xor(mu, o, 64),
+                 qb = __shfl_xor(m2, o, 64);
+    const double nn = n + nb;
+    if (nn > 0.0) {
+      const double d = mb - mu;
+      mu += d * nb / nn;
+      m2 += qb + d * d * n * nb / nn;
+    }
+    n = nn;
+  }
+  if (l == 0) {
+    const float var = fmaxf((float)(m2 / n), 0.0f);
+    const float m = (float)mu;
+    mean[c] = m;
+    invstd[c] = rsqrtf(var + eps);
+    if (rmean != nullptr) {
+      rmean[c] = (1.0f - momentum) * rmean[c] + momentum * m;
+      rvar[c] = (1.0f - momentum) * rvar[c] + momentum * (float)(var * n / (n - 1.0));
+    }
+    if (nbt != nullptr && c == 0) nbt[0] += 1;
+  }
+}
+
 // y = act((x - mean) * invstd * gamma + beta), kApplyU float4 per thread;
 // grid = (bn_apply_blocks(S), B * C).  Thread 0 derives the channel's
 // statistics from the P partials once per block (LDS broadcast).
@@ -199,8 +246,13 @@ __global__ void __launch_bounds__(256)
   if (threadIdx.x == 0) {
     float m, is, var;
     double n;
-    fin.get(x, c, m, is, var, n);
-    if (bx == 0 && row < (unsigned)C) fin.publish(c, m, is, var, n, mean, invstd);
+    if (fin.part != nullptr) {
+      fin.get(x, c, m, is, var, n);
+      if (bx == 0 && row < (unsigned)C) fin.publish(c, m, is, var, n, mean, invstd);
+    } else {  // statistics already final (bn_fin_parts_kernel)
+      m = mean[c];
+      is = invstd[c];
+    }
     st[0] = m;
     st[1] = is;
   }
@@ -806,6 +858,29 @@ extern "C" int pcfm_bn_act_fwd(const float* x, const float* gamma, const float* 
   hipLaunchKernelGGL(bn_act_apply_kernel, dim3(bn_apply_blocks(s), b * c), dim3(256), 0, st, x,
                      fin, mean, invstd, gamma, beta, c, s / 4, slope, y);
   return check_launch("bn_act_fwd");
+}
+
+// pcfm_bn_act_fwd with the statistics from the producer's epilogue (part float2
+// [c][P], see bn_fin_parts_kernel): no statistics pass over x.
+extern "C" int pcfm_bn_act_fwd_parts(const float* x, const float* part, int P, const float* gamma,
+                                     const float* beta, int b, int c, int s, float eps,
+                                     float slope, float momentum, float* running_mean,
+                                     float* running_var, long long* num_batches_tracked, float* y,
+                                     float* mean, float* invstd, void* stream) {
+  PCFM_CHECK_ARG(bn_ok(b, c, s), "bn_act_fwd_parts: bad shape b=%d c=%d s=%d", b, c, s);
+  PCFM_CHECK_ARG(part != nullptr && P == b * ceil_div(s, 64),
+                 "bn_act_fwd_parts: need b * ceil(s / 64) = %d groups per channel, got %d",
+                 b * ceil_div(s, 64), P);
+  PCFM_CHECK_ARG((running_mean == nullptr) == (running_var == nullptr),
+                 "bn_act_fwd_parts: running_mean and running_var must both be given or both NULL");
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(bn_fin_parts_kernel, dim3(c), dim3(64), 0, st,
+                     reinterpret_cast<const float2*>(part), P, s, eps, momentum, running_mean,
+                     running_var, num_batches_tracked, mean, invstd);
+  const BnFwdFin fin{nullptr, b, s, 0, eps, momentum, running_mean, running_var, nullptr};
+  hipLaunchKernelGGL(bn_act_apply_kernel, dim3(bn_apply_blocks(s), b * c), dim3(256), 0, st, x,
+                     fin, mean, invstd, gamma, beta, c, s / 4, slope, y);
+  return check_launch("bn_act_fwd_parts");
 }
 
 extern "C" int pcfm_bn_act_bwd(const float* dz, const float* x, const float* gamma,

@@ -178,10 +178,23 @@ __global__ void __launch_bounds__(256)
 // 64 x 64 (4 x 2), 512 threads, 60 KiB LDS (two blocks per CU).  Every output
 // channel of a point tile comes from one block, so x is read from HBM once
 // (the 128-row tile above reads it Mpad / 128 times).
+// stats != nullptr (a SharedMLP layer's BatchNorm follows): per output channel m
+// and 64-point group g of batch element b, the group's mean and centred sum of
+// squares of y go to stats[m * P + b * ngroups + g] (P = B * ngroups), two-pass
+// over the values in registers and a fixed xor tree across the 32 lanes of a
+// row segment -- the BatchNorm statistics pass over y is not needed
+// (bn_fin_parts_kernel combines the groups, Chan's formula, in a fixed order).
+__device__ __forceinline__ float half_wave_sum(float v) {
+#pragma unroll
+  for (int o = 1; o < 32; o <<= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4)))
     pw_gemm256_kernel(const Parts x, const uint16_t* __restrict__ wh,
                       const uint16_t* __restrict__ wl, const float* __restrict__ bias,
-                      int bias_bstride, const Parts y, int K, int M, int N, int Kpad) {
+                      int bias_bstride, const Parts y, int K, int M, int N, int Kpad,
+                      float2* __restrict__ stats = nullptr) {
   constexpr int TM = 256, TN = 128;
   constexpr int A_ELEMS = TM * kLDR, B_ELEMS = TN * kLDR;
   __shared__ __attribute__((aligned(16))) uint16_t lds[2 * A_ELEMS + 2 * B_ELEMS];
@@ -273,6 +286,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))
     __syncthreads();
   }
   const int bo = b * bias_bstride;
+  const int pw0 = p0 + wc * 64;  // this wave's 64 points
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int mg = m0 + wr * 64 + i * 32;
@@ -285,9 +299,23 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))
       for (int e = 0; e < 16; ++e) {
         const int dm = (e & 3) + 8 * (e >> 2) + 4 * h;
         const int m = mg + dm;
-        const int p = p0 + wc * 64 + j * 32 + r;
+        const int p = pw0 + j * 32 + r;
         if (m < M && p < N) out_store(yr + (size_t)dm * N + p, acc[i][j][e] + bv[e]);
       }
+    if (stats != nullptr && pw0 < N) {
+      const int nv = min(64, N - pw0);
+      const int ngroups = (N + 63) / 64, P = (int)gridDim.z * ngroups;
+      const bool ok0 = pw0 + r < N, ok1 = pw0 + 32 + r < N;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const float v0 = acc[i][0][e] + bv[e], v1 = acc[i][1][e] + bv[e];
+        const float mu = half_wave_sum((ok0 ? v0 : 0.0f) + (ok1 ? v1 : 0.0f)) / (float)nv;
+        const float d0 = ok0 ? v0 - mu : 0.0f, d1 = ok1 ? v1 - mu : 0.0f;
+        const float q = half_wave_sum(__builtin_fmaf(d1, d1, d0 * d0));
+        const int m = mg + (e & 3) + 8 * (e >> 2) + 4 * h;
+        if (r == 0 && m < M) stats[(size_t)m * P + b * ngroups + pw0 / 64] = make_float2(mu, q);
+      }
+    }
   }
 }
 
@@ -863,8 +891,20 @@ extern "C" int pcfm_pointwise_prep_weight(const float* w, int cout, int cin, int
   return check_launch("pointwise_prep_weight");
 }
 
+// Does pw_gemm_launch take the 256-row tile (the one with the BatchNorm
+// statistics epilogue) for this shape?
+static bool pw_takes_256(int b, int cin, int cout, int n) {
+  const int Mpad = pw_mpad(cout), Kpad = pad_to(cin, kKT);
+  const long long big = (long long)ceil_div(n, 128) * (Mpad / 128) * b;
+#ifndef PCFM_PW_NOSTREAM
+  if (Mpad == 128 && Kpad <= 256 && cin % 32 == 0 && cout % 32 == 0) return false;
+#endif
+  return Mpad % 256 == 0 && big / 2 >= 2 * kCUs;
+}
+
 static int pw_gemm_launch(const Parts& x, const void* wsplit, const float* bias, int bias_bstride,
-                          int b, int cin, int cout, int n, const Parts& y, hipStream_t st) {
+                          int b, int cin, int cout, int n, const Parts& y, hipStream_t st,
+                          float2* stats = nullptr) {
   const int Mpad = pw_mpad(cout), Kpad = pad_to(cin, kKT);
   const size_t total = (size_t)Mpad * Kpad;
   const uint16_t* wh = (const uint16_t*)wsplit;
@@ -908,7 +948,7 @@ static int pw_gemm_launch(const Parts& x, const void* wsplit, const float* bias,
 #ifndef PCFM_PW_NO256
   if (Mpad % 256 == 0 && big / 2 >= 2 * kCUs) {
     hipLaunchKernelGGL(pw_gemm256_kernel, dim3(ceil_div(n, 128), Mpad / 256, b), dim3(512), 0, st,
-                       x, wh, wh + total, bias, bias_bstride, y, cin, cout, n, Kpad);
+                       x, wh, wh + total, bias, bias_bstride, y, cin, cout, n, Kpad, stats);
     return check_launch("pointwise_gemm");
   }
 #endif
@@ -949,6 +989,24 @@ extern "C" int pcfm_pointwise_gemm(const float* x, const void* wsplit, const flo
   if (b == 0 || n == 0) return PCFM_OK;
   return pw_gemm_launch(one_part(x, cin), wsplit, bias, 0, b, cin, cout, n, one_part(y, cout),
                         (hipStream_t)stream);
+}
+
+// y = W x + bias with the BatchNorm statistics of y per (channel, 64-point
+// group): stats float2 [cout][b * ceil(n / 64)] (mean, centred sum of squares);
+// pcfm_pointwise_bnstats_groups() > 0 for the shapes that take this path.
+extern "C" int pcfm_pointwise_bnstats_groups(int b, int cin, int cout, int n) {
+  if (!pw_ok(b, cin, cout, n) || b <= 0 || n <= 0 || !pw_takes_256(b, cin, cout, n)) return 0;
+  return b * ceil_div(n, 64);
+}
+
+extern "C" int pcfm_pointwise_gemm_bnstats(const float* x, const void* wsplit, const float* bias,
+                                           int b, int cin, int cout, int n, float* y,
+                                           float* stats, void* stream) {
+  PCFM_CHECK_ARG(pcfm_pointwise_bnstats_groups(b, cin, cout, n) > 0 && stats != nullptr,
+                 "pointwise_gemm_bnstats: unsupported shape b=%d cin=%d cout=%d n=%d", b, cin,
+                 cout, n);
+  return pw_gemm_launch(one_part(x, cin), wsplit, bias, 0, b, cin, cout, n, one_part(y, cout),
+                        (hipStream_t)stream, reinterpret_cast<float2*>(stats));
 }
 
 extern "C" int pcfm_pointwise_gemm_parts(int nx, const float* const* x, const int* xw,

@@ -16,6 +16,8 @@ __all__ = ["bn_act", "conv_bn_act", "gn_film_residual"]
 
 # PCFM_DEBUG_CHECKS=1: assert the preconditions of the exact-skip fast paths
 _DEBUG_CHECKS = __import__("os").environ.get("PCFM_DEBUG_CHECKS") == "1"
+# SharedMLP BatchNorm statistics from the GEMM epilogue (PCFM_BN_FROM_GEMM=0: separate pass)
+_BN_FROM_GEMM = __import__("os").environ.get("PCFM_BN_FROM_GEMM", "1") != "0"
 
 
 class _BNAct(torch.autograd.Function):
@@ -64,9 +66,16 @@ class _PwBnAct(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, gamma, beta, rmean, rvar, nbt, eps, momentum, slope):
         from pcfm import ops
-        y = ops.pointwise_forward(x, w, b)
-        z, mean, invstd = ops.bn_act_forward(y, gamma, beta, eps, slope, momentum, rmean, rvar,
-                                             nbt)
+        # the 256-row GEMM hands the BatchNorm its statistics (no pass over y)
+        ys = ops.pointwise_forward_bnstats(x, w, b) if _BN_FROM_GEMM else None
+        if ys is not None:
+            y, stats = ys
+            z, mean, invstd = ops.bn_act_forward_parts(y, stats, gamma, beta, eps, slope,
+                                                       momentum, rmean, rvar, nbt)
+        else:
+            y = ops.pointwise_forward(x, w, b)
+            z, mean, invstd = ops.bn_act_forward(y, gamma, beta, eps, slope, momentum, rmean,
+                                                 rvar, nbt)
         ctx.save_for_backward(x, w, y, gamma, beta, mean, invstd)
         ctx.slope, ctx.has_bias = slope, b is not None
         return z

@@ -101,6 +101,10 @@ SIGNATURES = {
     "pcfm_bn_workspace_bytes": (_Z, [_I, _I, _I]),
     "pcfm_bn_act_fwd": (_I, [_P, _P, _P, _I, _I, _I, _F, _F, _F, _P, _P, _P, _P, _P, _P, _P,
                              _Z, _P]),
+    "pcfm_pointwise_bnstats_groups": (_I, [_I, _I, _I, _I]),
+    "pcfm_pointwise_gemm_bnstats": (_I, [_P, _P, _P, _I, _I, _I, _I, _P, _P, _P]),
+    "pcfm_bn_act_fwd_parts": (_I, [_P, _P, _I, _P, _P, _I, _I, _I, _F, _F, _F, _P, _P, _P, _P,
+                                   _P, _P, _P]),
     "pcfm_bn_act_bwd": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _F, _P, _P, _P, _P, _P, _Z,
                              _P]),
     "pcfm_bn_act_fwd_split": (_I, [_P, _P, _P, _I, _I, _I, _F, _F, _F, _P, _P, _P, _P, _P, _P,
@@ -125,7 +129,7 @@ SIGNATURES = {
     "pcfm_adamw_ema_step": (_I, [_P, _P, _I, _P, _P, _I, _DP, _DP, _D, _D, _D, _D, _P]),
 }
 
-ABI_VERSION = 16
+ABI_VERSION = 17
 
 _lock = threading.Lock()
 _lib = None

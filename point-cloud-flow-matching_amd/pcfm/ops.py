@@ -837,6 +837,27 @@ def pointwise_forward(x: torch.Tensor, weight: torch.Tensor, bias) -> torch.Tens
     return y
 
 
+def pointwise_forward_bnstats(x: torch.Tensor, weight: torch.Tensor, bias):
+    """pointwise_forward with the BatchNorm statistics of y from the GEMM's
+    epilogue -> (y, stats f32 (Cout, P, 2)), or None for the shapes without that
+    path (pcfm_pointwise_bnstats_groups)."""
+    _check(x, "input", "f")
+    x = x.contiguous()
+    b, cin, n = x.shape
+    cout = weight.shape[0]
+    groups = _lib.query("pcfm_pointwise_bnstats_groups", b, cin, cout, n)
+    if groups <= 0:
+        return None
+    img = pointwise_prep_weight(weight, False)
+    y = torch.empty((b, cout, n), dtype=torch.float32, device=x.device)
+    stats = torch.empty((cout, groups, 2), dtype=torch.float32, device=x.device)
+    bias_p = _ptr(bias.contiguous()) if bias is not None else None
+    with _timed("pointwise_fwd", 2 * b * n * cin * cout, x, "mfma"):
+        _lib.call("pcfm_pointwise_gemm_bnstats", _ptr(x), _ptr(img), bias_p, b, cin, cout, n,
+                  _ptr(y), _ptr(stats), _stream(x))
+    return y, stats
+
+
 def pointwise_backward_data(grad_y: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
     _check(grad_y, "grad_output", "f")
     g = grad_y.contiguous()
@@ -1114,6 +1135,25 @@ def bn_act_forward(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, ep
                   _p(_counter(num_batches_tracked, x)), _ptr(y),
                   _ptr(stats[0]), _ptr(stats[1]), _ptr(ws), ws.numel(), _stream(x))
     return y, stats[0], stats[1]
+
+
+def bn_act_forward_parts(x: torch.Tensor, stats: torch.Tensor, weight: torch.Tensor,
+                         bias: torch.Tensor, eps: float, slope: float, momentum: float,
+                         running_mean, running_var, num_batches_tracked=None):
+    """bn_act_forward for x whose statistics came out of its producer
+    (pointwise_forward_bnstats): the finalize + apply only -> (y, mean, invstd)."""
+    _check(x, "input", "f")
+    _check(stats, "stats", "f")
+    b, c = x.shape[0], x.shape[1]
+    s = x.numel() // max(1, b * c)
+    y = torch.empty_like(x)
+    out = torch.empty((2, c), dtype=torch.float32, device=x.device)
+    with _timed("bn_act_fwd", 4 * 2 * x.numel(), x):
+        _lib.call("pcfm_bn_act_fwd_parts", _ptr(x), _ptr(stats), int(stats.shape[1]),
+                  _ptr(weight), _ptr(bias), b, c, s, float(eps), float(slope), float(momentum),
+                  _p(running_mean), _p(running_var), _p(_counter(num_batches_tracked, x)),
+                  _ptr(y), _ptr(out[0]), _ptr(out[1]), _stream(x))
+    return y, out[0], out[1]
 
 
 def bn_act_forward_split(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, eps: float,
