@@ -6,11 +6,11 @@
 // match[b, m, n] matrix once per level (:144).
 //
 // MI355X design:
-//   * every pass of every level is a full-chip launch: lanes own rows, the
-//     inner (column) loop is wave-uniform so the column points arrive through
-//     scalar loads, and the column range is split S ways into a partial-sum
-//     buffer that the NEXT phase reduces in a fixed order while it stages its
-//     column coefficients (the finalize folded in: 33 launches per approxmatch);
+//   * every pass of every level is a full-chip launch with its finalize
+//     included: a block owns 64 rows (lanes), its 16 waves split the column
+//     range (wave-uniform, so the column points arrive through scalar loads),
+//     the wave sums of a row are added in a fixed order in LDS and the row's
+//     finalize runs in the same block (31 launches per approxmatch);
 //   * match is NOT accumulated level by level.  Each level only needs the
 //     vectors ratioL (n) and ratioR (m), which are kept per level (10 x (n+m));
 //     match is written once at the end as
@@ -309,8 +309,11 @@ struct EmdWs {
 size_t emd_ws_elems(int b, int n, int m) {
   const size_t bn = (size_t)b * n, bm = (size_t)b * m;
   const int S = emd_splits(b, n, m);
-  const size_t part = std::max((size_t)S * b * std::max(n, m) * 3,
-                               (size_t)b * S * ceil_div(std::max(n, 1), kThreads));
+  // the partials of the split form / the row-pass form's point packs (4 (bn + 2 bm));
+  // the region starts at 12 (bn + bm) elements: 16-B aligned for f32, 32-B for f64
+  const size_t part = std::max({(size_t)S * b * std::max(n, m) * 3,
+                                (size_t)b * S * ceil_div(std::max(n, 1), kThreads),
+                                4 * (bn + 2 * bm)});
   return 2 * (bn + bm) + kLevels * (bn + bm) + part;
 }
 
@@ -340,176 +343,137 @@ inline dim3 grid1d(size_t total, int threads = 256) {
 }
 
 // ---------------------------------------------------------------------------
-// Phase form (the default): one launch per phase of each level.  The round-3
-// form ran the whole auction as ONE cooperative launch with grid barriers
-// between the phases; it was bit-identical but 6x slower (4.5 vs 0.75 ms at
-// B = 8, N = 2048): hipLaunchCooperativeKernel and its grid barriers cost more
-// than the launches they replaced, so it is gone.  What it did keep is used
-// here: the split form's finalize kernels disappear into the phases.
-//
-// Each finalize is folded into the phase that consumes it:
-//   P1 (rows k, cols l, coef remR)            -> partA;  also level j-1's fin3
-//        for the unit's rows (remL -= sum partC, levL[j-1] = ratL)
-//   P2 (rows l, cols k, coef ratL)            -> partB;  ratL = remL / (1e-9 + sum partA)
-//        computed per column into LDS (row tile 0 also stores it)
-//   P3 (rows k, cols l, coef ratR, rowscale ratL) -> partC;  ratR / remR' from
-//        partB per column into LDS (row tile 0 stores levR[j] and remR')
-// remR is double-buffered (P3 reads the level's remR while remR' is written).
+// Row-pass form (the default): ONE launch per pass of each level, its finalize
+// included, and no partial-sum buffer.  A block owns 64 rows (one per lane)
+// and splits the column range over its 16 waves; the 16 wave sums of a row
+// are added in wave order in LDS and the row's finalize (fin1 / fin2 / fin3
+// of the split form) runs right there, so the next pass reads finished
+// coefficients.  31 launches per approxmatch (init + 30) plus the match write.
+// Measured history (B = 8, N = 2048, MI355X): the split form below (6 launches
+// per level, S-way partials reduced by separate finalize kernels) 0.67 ms; a
+// form with the finalizes folded into the next pass, each block re-reducing
+// the S partials of its columns, 0.80 ms (the serial partial reads sat in front
+// of every pass); the round-3 cooperative one-launch form with
+// cooperative_groups grid barriers 4.45 ms (a grid.sync() costs ~0.1 us per
+// block on ROCm 7.2, ~100 us at 1024 blocks, against ~1.7 us for a kernel
+// boundary).
 // ---------------------------------------------------------------------------
-constexpr int kPChunk = 1024;  // columns staged in LDS per chunk
+constexpr int kRowWaves = 16;  // column splits per block, one wave each
 
-struct EmdPlan {
-  int b, n, m, S;
-  int tilesN, tilesM;  // ceil(n / kThreads), ceil(m / kThreads)
+// A point with the coefficient it carries into a pass, 16 (f32) / 32 (f64)
+// bytes: a wave-uniform column read is one scalar load of point + coefficient
+// (the compiler merges consecutive columns into s_load_dwordx8/x16).
+template <typename T>
+struct alignas(4 * sizeof(T)) Col4 {
+  T x, y, z, c;
 };
 
+// packK[b, k] = {xyz1, ratL};  packL0[b, l] = {xyz2, remR};  packL1[b, l] = {xyz2, ratR}
 template <typename T>
-struct EmdPState {
-  const T* xyz1;
-  const T* xyz2;
+struct EmdRowState {
+  Col4<T>* packK;
+  Col4<T>* packL0;
+  Col4<T>* packL1;
   T* remL;
-  T* remR[2];
-  T* ratL;
-  T* levL;
-  T* levR;
-  T* part[3];
-  T* match;
-  T multiL, multiR;
+  T* levL;  // [kLevels][b * n]
+  T* levR;  // [kLevels][b * m]
 };
 
-// The column coefficient of phase `ph` for column c of batch bb.
 template <typename T>
-__device__ __forceinline__ T p_coef(const EmdPState<T>& s, const EmdPlan& p, int ph, int lvl,
-                                    int bb, int c, bool store) {
-  if (ph == 0) return s.remR[lvl & 1][(size_t)bb * p.m + c];
-  if (ph == 1) {  // fin1: ratioL = remainL / (1e-9 + suml)
-    const size_t bn = (size_t)p.b * p.n, i = (size_t)bb * p.n + c;
-    const T v = s.remL[i] / ((T)1e-9f + sum_parts(s.part[0], p.S, bn, i));
-    if (store) s.ratL[i] = v;
-    return v;
+__global__ void emd_pack_kernel(const T* __restrict__ xyz1, size_t bn, T multiL,
+                                const T* __restrict__ xyz2, size_t bm, T multiR,
+                                EmdRowState<T> s) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < bn) {
+    s.packK[i] = Col4<T>{xyz1[3 * i], xyz1[3 * i + 1], xyz1[3 * i + 2], (T)0};
+    s.remL[i] = multiL;
   }
-  // fin2: ratioR, remainR' (emd_fin2_kernel)
-  const size_t bm = (size_t)p.b * p.m, i = (size_t)bb * p.m + c;
-  const T r = s.remR[lvl & 1][i];
-  T sumr = sum_parts(s.part[1], p.S, bm, i);
-  sumr *= r;
-  const T cons = (T)fminf((float)(r / (sumr + (T)1e-9f)), 1.0f);
-  const T rat = cons * r;
-  if (store) {
-    s.levR[(size_t)lvl * bm + i] = rat;
-    s.remR[(lvl + 1) & 1][i] = (T)fmaxf(0.0f, (float)(r - sumr));
+  if (i < bm) {
+    const T x = xyz2[3 * i], y = xyz2[3 * i + 1], z = xyz2[3 * i + 2];
+    s.packL0[i] = Col4<T>{x, y, z, multiR};
+    s.packL1[i] = Col4<T>{x, y, z, (T)0};
   }
-  return rat;
 }
 
-template <typename T>
-__device__ void p_pass(const EmdPState<T>& s, const EmdPlan& p, int ph, int lvl, T* lcoef) {
-  const T level = (T)c_levels[lvl];
-  const bool rows_k = ph != 1;
-  const int nr = rows_k ? p.n : p.m, ncol = rows_k ? p.m : p.n;
-  const int tiles = rows_k ? p.tilesN : p.tilesM;
-  const T* rows = rows_k ? s.xyz1 : s.xyz2;
-  const T* cols = rows_k ? s.xyz2 : s.xyz1;
-  T* part = s.part[ph];
-  const int units = tiles * p.S * p.b;
-  for (int u = blockIdx.x; u < units; u += gridDim.x) {
-    const int tile = u % tiles;
-    const int sp = (u / tiles) % p.S;
-    const int bb = u / (tiles * p.S);
-    const int i = tile * kThreads + threadIdx.x;
-    const int ii = i < nr ? i : nr - 1;
-    const T* rp = rows + ((size_t)bb * nr + ii) * 3;
-    const T x1 = rp[0], y1 = rp[1], z1 = rp[2];
-    if (ph == 0 && lvl > 0 && sp == 0 && i < nr) {  // level lvl-1's fin3 for these rows
-      const size_t bn = (size_t)p.b * p.n, k = (size_t)bb * p.n + i;
-      s.remL[k] = (T)fmaxf(0.0f, (float)(s.remL[k] - sum_parts(s.part[2], p.S, bn, k)));
-      s.levL[(size_t)(lvl - 1) * bn + k] = s.ratL[k];
+// PH 0: rows k (packK), cols packL0 (coef remR);  suml -> ratL = remL / (1e-9 + suml)  (:57-81)
+// PH 1: rows l (packL0), cols packK (coef ratL);  sumr -> ratR, levR[lvl], remR (fin2) (:86-116)
+// PH 2: rows k (packK, row scale ratL), cols packL1 (coef ratR);  -> remL, levL[lvl]   (:119-151)
+// grid = (ceil(nr / 64), b), 1024 threads.
+template <typename T, int PH>
+__global__ void __launch_bounds__(64 * kRowWaves)
+    emd_rowpass_kernel(int nr, int ncol, T level, int lvl, EmdRowState<T> s) {
+  __shared__ T red[kRowWaves][64];
+  Col4<T>* rows = PH == 1 ? s.packL0 : s.packK;
+  const Col4<T>* __restrict__ cols = PH == 0 ? s.packL0 : (PH == 1 ? s.packK : s.packL1);
+  const int bb = blockIdx.y, lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int i = blockIdx.x * 64 + lane;
+  const int ii = i < nr ? i : nr - 1;
+  const Col4<T> rp = rows[(size_t)bb * nr + ii];
+  const T rl = rp.c;  // PH 2: ratL of the row
+  const int c0 = (int)(((long long)ncol * w) / kRowWaves);
+  const int c1 = (int)(((long long)ncol * (w + 1)) / kRowWaves);
+  const Col4<T>* __restrict__ cb = cols + (size_t)bb * ncol;
+  T acc = 0;
+#pragma unroll 8
+  for (int c = c0; c < c1; ++c) {
+    const Col4<T> q = cb[c];
+    const T d2 = sqdist3(q.x - rp.x, q.y - rp.y, q.z - rp.z);
+    const T e = emd_exp<T>(level * d2);
+    if constexpr (PH == 2) {
+      acc = fmaT<T>(e * rl, q.c, acc);
+    } else {
+      acc = fmaT<T>(e, q.c, acc);
     }
-    T rl = (T)0;
-    if (ph == 2) rl = s.ratL[(size_t)bb * p.n + ii];
-    const int c0 = (int)(((long long)ncol * sp) / p.S);
-    const int c1 = (int)(((long long)ncol * (sp + 1)) / p.S);
-    const T* __restrict__ cb = cols + (size_t)bb * ncol * 3;
-    T acc = 0;
-    for (int q0 = c0; q0 < c1; q0 += kPChunk) {
-      const int q1 = min(c1, q0 + kPChunk);
-      __syncthreads();  // the previous chunk / unit is done with lcoef
-      for (int c = q0 + (int)threadIdx.x; c < q1; c += kThreads)
-        lcoef[c - q0] = p_coef(s, p, ph, lvl, bb, c, tile == 0);
-      __syncthreads();
-#pragma unroll 4
-      for (int c = q0; c < q1; ++c) {
-        const T d2 = sqdist3(cb[3 * c] - x1, cb[3 * c + 1] - y1, cb[3 * c + 2] - z1);
-        const T e = emd_exp<T>(level * d2);
-        if (ph == 2) {
-          acc = fmaT<T>(e * rl, lcoef[c - q0], acc);
-        } else {
-          acc = fmaT<T>(e, lcoef[c - q0], acc);
-        }
-      }
-    }
-    if (i < nr) part[(size_t)sp * p.b * nr + (size_t)bb * nr + i] = acc;
+  }
+  red[w][lane] = acc;
+  __syncthreads();
+  if (w != 0 || i >= nr) return;
+  T t = 0;
+#pragma unroll
+  for (int q = 0; q < kRowWaves; ++q) t += red[q][lane];
+  const size_t idx = (size_t)bb * nr + i;
+  const size_t lv = (size_t)lvl * gridDim.y * nr + idx;
+  if constexpr (PH == 0) {
+    rows[idx].c = s.remL[idx] / ((T)1e-9f + t);
+  } else if constexpr (PH == 1) {
+    const T r = rp.c;
+    const T sumr = t * r;
+    const T cons = (T)fminf((float)(r / (sumr + (T)1e-9f)), 1.0f);
+    const T rat = cons * r;
+    s.packL1[idx].c = rat;
+    s.levR[lv] = rat;
+    rows[idx].c = (T)fmaxf(0.0f, (float)(r - sumr));
+  } else {
+    s.remL[idx] = (T)fmaxf(0.0f, (float)(s.remL[idx] - t));
+    s.levL[lv] = rl;
   }
 }
 
-// One phase of one level per launch: the unit loop of p_pass over (row tile,
-// split, b), each finalize folded into the phase that consumes it.  30 phase
-// launches + init + the last level's levL + the match write: half the
-// launches of the split form below, whose every pass and every finalize is
-// its own launch (at B = 8, N = 2048 the passes are ~1 us of exp issue each,
-// so launches, not exps, set the time).  Same per-element expressions and
-// partial-sum order: bit-identical to the split form
-// (tests/test_gpu_ops.py::test_emd_phase_form_bit_identical).
-template <typename T>
-__global__ void __launch_bounds__(kThreads)
-    emd_phase_kernel(EmdPState<T> s, EmdPlan p, int ph, int lvl) {
-  __shared__ T lcoef[kPChunk];
-  p_pass(s, p, ph, lvl, lcoef);
-}
-
-template <typename T>
-__global__ void emd_levlast_kernel(const T* __restrict__ ratL, size_t bn, T* __restrict__ levL) {
-  const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k < bn) levL[k] = ratL[k];  // the last level's fin3 (levL only)
-}
-
-// PCFM_EMD_FORM=split: every pass and finalize its own launch (measurement /
-// the bit-identity test); default: the phase form
+// PCFM_EMD_FORM=split: every pass and finalize its own launch, S-way partials
+// (measurement / the cross-form test); default: the row-pass form
 bool emd_split_form() {
   const char* e = std::getenv("PCFM_EMD_FORM");
   return e != nullptr && e[0] == 's';
 }
 
 template <typename T>
-int approxmatch_phases(const T* xyz1, const T* xyz2, int b, int n, int m, T* match, EmdWs<T> w,
-                       int S, hipStream_t st) {
-  EmdPlan p{b, n, m, S, ceil_div(n, kThreads), ceil_div(m, kThreads)};
-  EmdPState<T> s;
-  s.xyz1 = xyz1;
-  s.xyz2 = xyz2;
-  s.remL = w.remL;
-  s.remR[0] = w.remR;
-  s.remR[1] = w.ratR;  // the split form's ratioR buffer: free here (ratR is per column on the fly)
-  s.ratL = w.ratL;
-  s.levL = w.levL;
-  s.levR = w.levR;
-  const size_t pstride = (size_t)S * b * std::max(n, m);
-  s.part[0] = w.part;
-  s.part[1] = w.part + pstride;
-  s.part[2] = w.part + 2 * pstride;
-  s.match = match;
-  s.multiL = n >= m ? (T)1 : (T)(m / n);
-  s.multiR = n >= m ? (T)(n / m) : (T)1;
+int approxmatch_rowpass(const T* xyz1, const T* xyz2, int b, int n, int m, T* match, EmdWs<T> w,
+                        hipStream_t st) {
   const size_t bn = (size_t)b * n, bm = (size_t)b * m;
-  hipLaunchKernelGGL(emd_init_kernel<T>, grid1d(std::max(bn, bm)), dim3(256), 0, st, w.remL, bn,
-                     s.multiL, w.remR, bm, s.multiR);
-  const unsigned unitsL = (unsigned)p.tilesN * S * b, unitsR = (unsigned)p.tilesM * S * b;
-  for (int lvl = 0; lvl < kLevels; ++lvl)
-    for (int ph = 0; ph < 3; ++ph)
-      hipLaunchKernelGGL(emd_phase_kernel<T>, dim3(ph == 1 ? unitsR : unitsL), dim3(kThreads), 0,
-                         st, s, p, ph, lvl);
-  hipLaunchKernelGGL(emd_levlast_kernel<T>, grid1d(bn), dim3(256), 0, st, (const T*)w.ratL, bn,
-                     w.levL + (size_t)(kLevels - 1) * bn);
+  Col4<T>* pk = reinterpret_cast<Col4<T>*>(w.part);  // 16/32-B aligned: see emd_ws_elems
+  EmdRowState<T> s{pk, pk + bn, pk + bn + bm, w.remL, w.levL, w.levR};
+  const T multiL = n >= m ? (T)1 : (T)(m / n);  // integer ratio of the cloud sizes (:27-33)
+  const T multiR = n >= m ? (T)(n / m) : (T)1;
+  hipLaunchKernelGGL(emd_pack_kernel<T>, grid1d(std::max(bn, bm)), dim3(256), 0, st, xyz1, bn,
+                     multiL, xyz2, bm, multiR, s);
+  const dim3 gL(ceil_div(n, 64), b), gR(ceil_div(m, 64), b), blk(64 * kRowWaves);
+  for (int j = 0; j < kLevels; ++j) {
+    const T level = (T)h_levels[j];
+    hipLaunchKernelGGL((emd_rowpass_kernel<T, 0>), gL, blk, 0, st, n, m, level, j, s);
+    hipLaunchKernelGGL((emd_rowpass_kernel<T, 1>), gR, blk, 0, st, m, n, level, j, s);
+    hipLaunchKernelGGL((emd_rowpass_kernel<T, 2>), gL, blk, 0, st, n, m, level, j, s);
+  }
   dim3 gm(ceil_div(n, kThreads), ceil_div(m, kLPer), b);
   hipLaunchKernelGGL(emd_match_kernel<T>, gm, dim3(kThreads), 0, st, xyz1, xyz2, b, n, m, w.levL,
                      w.levR, match);
@@ -525,8 +489,8 @@ int approxmatch(const T* xyz1, const T* xyz2, int b, int n, int m, T* match, voi
                  emd_ws_elems(b, n, m) * sizeof(T));
   if (b == 0 || n == 0 || m == 0) return PCFM_OK;
   EmdWs<T> w = carve<T>(ws, b, n, m);
+  if (!emd_split_form()) return approxmatch_rowpass(xyz1, xyz2, b, n, m, match, w, st);
   const int S = emd_splits(b, n, m);
-  if (!emd_split_form()) return approxmatch_phases(xyz1, xyz2, b, n, m, match, w, S, st);
   // multiL/multiR: integer ratio of the cloud sizes (:27-33)
   const T multiL = n >= m ? (T)1 : (T)(m / n);
   const T multiR = n >= m ? (T)(n / m) : (T)1;

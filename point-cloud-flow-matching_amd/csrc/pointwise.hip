@@ -180,14 +180,28 @@ __global__ void __launch_bounds__(256)
 // (the 128-row tile above reads it Mpad / 128 times).
 // stats != nullptr (a SharedMLP layer's BatchNorm follows): per output channel m
 // and 64-point group g of batch element b, the group's mean and centred sum of
-// squares of y go to stats[m * P + b * ngroups + g] (P = B * ngroups), two-pass
-// over the values in registers and a fixed xor tree across the 32 lanes of a
-// row segment -- the BatchNorm statistics pass over y is not needed
-// (bn_fin_parts_kernel combines the groups, Chan's formula, in a fixed order).
-__device__ __forceinline__ float half_wave_sum(float v) {
+// squares of y go to stats[m * P + b * ngroups + g] (P = B * ngroups) -- the
+// BatchNorm statistics pass over y is not needed (bn_fin_parts_kernel combines
+// the groups, Chan's formula, in a fixed order).  Sums are taken about a shift
+// (the group's first value of the row, so no cancellation) and reduced over the
+// 32 lanes of a row segment by a transposing butterfly: at each xor stage a
+// lane keeps one half of its values and sends the other, so the 32 sums of 16
+// rows cost 31 lane swizzles instead of 5 per value (measured: the per-value
+// shuffle tree, 320 ds_bpermute per wave, made the GEMM 0.28 ms/step slower
+// than the separate statistics pass it replaced).
+template <int MASK>
+__device__ __forceinline__ float swz_xor(float v) {  // lane ^ MASK within 32 lanes
+  return __builtin_bit_cast(
+      float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, v), (MASK << 10) | 0x1f));
+}
+template <int K, int MASK>
+__device__ __forceinline__ void xpose_reduce_stage(float* v, bool upper) {
 #pragma unroll
-  for (int o = 1; o < 32; o <<= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  for (int k = 0; k < K / 2; ++k) {
+    const float keep = upper ? v[k + K / 2] : v[k];
+    const float send = upper ? v[k] : v[k + K / 2];
+    v[k] = keep + swz_xor<MASK>(send);
+  }
 }
 
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4)))
@@ -306,14 +320,32 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))
       const int nv = min(64, N - pw0);
       const int ngroups = (N + 63) / 64, P = (int)gridDim.z * ngroups;
       const bool ok0 = pw0 + r < N, ok1 = pw0 + 32 + r < N;
+      float v[32], sr = 0.0f;
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
         const float v0 = acc[i][0][e] + bv[e], v1 = acc[i][1][e] + bv[e];
-        const float mu = half_wave_sum((ok0 ? v0 : 0.0f) + (ok1 ? v1 : 0.0f)) / (float)nv;
-        const float d0 = ok0 ? v0 - mu : 0.0f, d1 = ok1 ? v1 - mu : 0.0f;
-        const float q = half_wave_sum(__builtin_fmaf(d1, d1, d0 * d0));
-        const int m = mg + (e & 3) + 8 * (e >> 2) + 4 * h;
-        if (r == 0 && m < M) stats[(size_t)m * P + b * ngroups + pw0 / 64] = make_float2(mu, q);
+        const float s0 = __builtin_bit_cast(
+            float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v0), 0));
+        const float s1 = __builtin_bit_cast(
+            float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v0), 32));
+        const float sh = h ? s1 : s0;  // row (e, h)'s value at point pw0
+        sr = r == e ? sh : sr;
+        const float d0 = ok0 ? v0 - sh : 0.0f, d1 = ok1 ? v1 - sh : 0.0f;
+        v[e] = d0 + d1;
+        v[16 + e] = __builtin_fmaf(d1, d1, d0 * d0);
+      }
+      xpose_reduce_stage<32, 16>(v, r & 16);
+      xpose_reduce_stage<16, 8>(v, r & 8);
+      xpose_reduce_stage<8, 4>(v, r & 4);
+      xpose_reduce_stage<4, 2>(v, r & 2);
+      xpose_reduce_stage<2, 1>(v, r & 1);
+      // lane r: v[0] = sum of value r (r < 16: shifted sum of row e = r; else its squares)
+      const float q = swz_xor<16>(v[0]);
+      const int m = mg + (r & 3) + 8 * ((r >> 2) & 3) + 4 * h;
+      if (r < 16 && m < M) {
+        const float a = v[0], mu_s = a / (float)nv;
+        stats[(size_t)m * P + b * ngroups + pw0 / 64] =
+            make_float2(sr + mu_s, fmaxf(__builtin_fmaf(-a, mu_s, q), 0.0f));
       }
     }
   }

@@ -16,6 +16,9 @@
 #   sample    bf16 Heun / dopri5 sampling bench  -> gpurun_out/sample_amp.json
 #   ddp       the two-rank DDP tests, ranks concurrent on the one GPU, with the
 #             devoxelization self-check on   -> gpurun_out/ddp_check.log
+#   ab        bench.py (quick form) once per variant of $AB, a space-separated list
+#             of NAME or NAME:VAR=V,VAR2=V2 (env for that run; NAME alone = defaults)
+#             -> gpurun_out/ab.jsonl (ms/step, roofline frac, per-op ms)
 #   script:F  run python F (a measurement script of tools/) -> gpurun_out/F.jsonl
 set -e
 cd "$GRAFT_REPO_ROOT"
@@ -56,6 +59,15 @@ for task in "$@"; do
       PCFM_DEVOX_VERIFY=1 timeout -k 10 400 python -u -m pytest \
         tests/test_gpu_ddp.py -m gpu -v -rxX --timeout 300 --timeout-method thread \
         > gpurun_out/ddp_check.log 2>&1 ;;
+    ab)
+      : > gpurun_out/ab.jsonl
+      for v in ${AB:-base}; do
+        name="${v%%:*}"; envs=""
+        [ "$name" != "$v" ] && envs="${v#*:}" && envs="${envs//,/ }"
+        env $envs timeout -k 10 200 python bench.py --steps 20 --warmup 3 $BENCHQ \
+          > gpurun_out/ab_one.json 2> gpurun_out/ab_one.err
+        python -c "import json,sys; d=json.load(open('gpurun_out/ab_one.json')); print(json.dumps({'v': sys.argv[1], 'ms': d['ms_per_step'], 'frac': d['roofline']['frac'], 'ops': {k: round(v['ms_per_step'], 4) for k, v in d['kernels'].items()}}))" "$v" >> gpurun_out/ab.jsonl
+      done ;;
     script:*)
       f="${task#script:}"
       timeout -k 10 400 python "$f" ${SCRIPT_ARGS:-} > "gpurun_out/$(basename "$f" .py).jsonl" \
