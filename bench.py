@@ -234,17 +234,20 @@ def emd_ms(dev, b, n, iters=3):
     p1 = torch.rand(b, n, 3, device=dev, generator=g)
     p2 = torch.rand(b, n, 3, device=dev, generator=g)
     res = {}
-    for bwd in (False, True):
+    # fwd_ms: inputs need no gradient (cost only, match not materialised);
+    # fwd_with_match_ms: the forward a backward will follow (match written and kept)
+    for key, grad, bwd in (("fwd_ms", False, False), ("fwd_with_match_ms", True, False),
+                           ("fwd_bwd_ms", True, True)):
         for i in range(iters + 1):
             if i == 1:
                 torch.cuda.synchronize(dev)
                 t0 = time.perf_counter()
-            x = p1.detach().requires_grad_(bwd)
+            x = p1.detach().requires_grad_(grad)
             d = earth_mover_distance(x, p2, transpose=False)
             if bwd:
                 d.sum().backward()
         torch.cuda.synchronize(dev)
-        res["fwd_bwd_ms" if bwd else "fwd_ms"] = (time.perf_counter() - t0) * 1e3 / iters
+        res[key] = (time.perf_counter() - t0) * 1e3 / iters
     # 10 levels x 3 passes over the B*N*M pairs, one exp each (emd_kernel.cu:44-154)
     res["exps_per_s_fwd"] = 30.0 * b * n * n / (res["fwd_ms"] * 1e-3)
     return res

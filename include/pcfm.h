@@ -46,7 +46,7 @@ extern "C" {
  * voxel convolution entry points; 14: voxel-list form of the voxel convolution;
  * 15: the head FiLM backward takes shift and recomputes u; 16: devoxelization
  * self-check entry point; 17: BatchNorm statistics from the pointwise GEMM's
- * epilogue). */
+ * epilogue; 18: fused EMD approxmatch + matchcost). */
 int pcfm_abi_version(void);
 /* Thread-local text of the last non-zero return code. */
 const char* pcfm_last_error(void);
@@ -201,6 +201,18 @@ int pcfm_emd_matchcost_f32(const float* xyz1, const float* xyz2, const float* ma
 int pcfm_emd_matchcost_f64(const double* xyz1, const double* xyz2, const double* match,
                            int b, int n, int m, double* cost, void* ws, size_t ws_bytes,
                            void* stream);
+
+/* ApproxMatchForward + MatchCostForward in one call (the forward of the
+ * reference's EarthMoverDistanceFunction, PyTorchEMD/emd.py:14-19): the cost
+ * is summed from the match kernel's own values, so match is not read back.
+ * match may be NULL (cost only, match not written: a forward whose inputs
+ * need no gradient).  cost [b].  Same workspace as approxmatch.             */
+int pcfm_emd_approxmatch_cost_f32(const float* xyz1, const float* xyz2, int b, int n, int m,
+                                  float* match, float* cost, void* ws, size_t ws_bytes,
+                                  void* stream);
+int pcfm_emd_approxmatch_cost_f64(const double* xyz1, const double* xyz2, int b, int n, int m,
+                                  double* match, double* cost, void* ws, size_t ws_bytes,
+                                  void* stream);
 
 /* Replaces MatchCostBackward (emd_kernel.cu:371-396) -> matchcostgrad1/2
  * (:285-353).  grad1 [b, n, 3], grad2 [b, m, 3] fully written.                   */

@@ -9,7 +9,7 @@ AT_DISPATCH_FLOATING_TYPES.  CPU tensors run the pure-PyTorch backend
 """
 import torch
 
-from pcfm.ops import emd_cuda
+from pcfm.ops import approxmatch_cost_forward, emd_cuda
 
 __all__ = ["emd_cuda", "EarthMoverDistanceFunction", "earth_mover_distance"]
 
@@ -20,9 +20,11 @@ class EarthMoverDistanceFunction(torch.autograd.Function):
     def forward(ctx, xyz1, xyz2):
         xyz1 = xyz1.contiguous()
         xyz2 = xyz2.contiguous()
-        match = emd_cuda.approxmatch_forward(xyz1, xyz2)
-        cost = emd_cuda.matchcost_forward(xyz1, xyz2, match)
-        ctx.save_for_backward(xyz1, xyz2, match)
+        # approxmatch + matchcost in one native call; match is kept only when a
+        # gradient will need it (emd.py:14-19 computes both, then saves match)
+        need = any(ctx.needs_input_grad)
+        match, cost = approxmatch_cost_forward(xyz1, xyz2, want_match=need)
+        ctx.save_for_backward(xyz1, xyz2, match if need else None)
         return cost
 
     @staticmethod

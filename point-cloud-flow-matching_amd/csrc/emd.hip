@@ -216,14 +216,70 @@ __global__ void __launch_bounds__(kThreads)
   if (threadIdx.x == 0) part[((size_t)bb * S + s) * gridDim.x + blockIdx.x] = t;
 }
 
+// cost[bb] = sum of the batch element's per_b block partials: one wave per
+// batch element, lanes over strided partials, then a fixed xor tree
+// (deterministic; the serial form was 9 us at 512 partials).
 template <typename T>
-__global__ void emd_cost_fin_kernel(const T* __restrict__ part, int per_b, int b,
-                                    T* __restrict__ cost) {
-  const int bb = blockIdx.x * blockDim.x + threadIdx.x;
-  if (bb >= b) return;
+__global__ void __launch_bounds__(64)
+    emd_cost_fin_kernel(const T* __restrict__ part, int per_b, T* __restrict__ cost) {
+  const int bb = blockIdx.x, lane = threadIdx.x;
   T t = 0;
-  for (int i = 0; i < per_b; ++i) t += part[(size_t)bb * per_b + i];
-  cost[bb] = t;
+  for (int i = lane; i < per_b; i += 64) t += part[(size_t)bb * per_b + i];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o, 64);
+  if (lane == 0) cost[bb] = t;
+}
+
+// The match write with matchcost fused (the fused forward, pcfm_emd_approxmatch_cost_*):
+// match[b, l, k] as emd_match_kernel (skipped when match == nullptr), and per
+// block the partial sum over its entries of d2 * match -- matchcost's terms
+// (emd_kernel.cu:199-241) -- to part[(bb * lblocks + lb) * kblocks + kb], so
+// the 4-byte-per-entry match matrix is not read back for the cost.  A block
+// = 256 k (lanes, coalesced rows) x kMatchL l, the l points and their 10
+// ratioR values staged in LDS.
+constexpr int kMatchL = 32;
+template <typename T>
+__global__ void __launch_bounds__(kThreads)
+    emd_match_cost_kernel(const T* __restrict__ xyz1, const T* __restrict__ xyz2, int b, int n,
+                          int m, const T* __restrict__ levL, const T* __restrict__ levR,
+                          T* __restrict__ match, T* __restrict__ part) {
+  constexpr int kW = kLevels + 3;  // per l: ratioR_0..9, x, y, z
+  __shared__ T sl[kMatchL * kW];
+  __shared__ T red[kThreads / 64];
+  const int bb = blockIdx.z, kb = blockIdx.x, lb = blockIdx.y;
+  const int k = kb * kThreads + threadIdx.x;
+  const int kk = k < n ? k : n - 1;
+  const int l0 = lb * kMatchL, nl = min(kMatchL, m - l0);
+  for (int e = threadIdx.x; e < nl * kW; e += kThreads) {
+    const int li = e / kW, q = e - li * kW;
+    sl[e] = q < kLevels ? levR[(size_t)q * b * m + (size_t)bb * m + l0 + li]
+                        : xyz2[((size_t)bb * m + l0 + li) * 3 + (q - kLevels)];
+  }
+  const T* p1 = xyz1 + ((size_t)bb * n + kk) * 3;
+  const T x1 = p1[0], y1 = p1[1], z1 = p1[2];
+  T rl[kLevels];
+#pragma unroll
+  for (int j = 0; j < kLevels; ++j) rl[j] = levL[(size_t)j * b * n + (size_t)bb * n + kk];
+  __syncthreads();
+  T csum = 0;
+  T* mrow = match != nullptr ? match + ((size_t)bb * m + l0) * n + k : nullptr;
+  for (int li = 0; li < nl; ++li) {
+    const T* q = sl + li * kW;
+    const T d2 = sqdist3(q[kLevels] - x1, q[kLevels + 1] - y1, q[kLevels + 2] - z1);
+    T acc = 0;
+#pragma unroll
+    for (int j = 0; j < kLevels; ++j) {
+      // level_j * log2(e) in one float factor (exact: level_j is a power of two)
+      const T e = j == kLevels - 1 ? (T)1
+                                   : (T)__builtin_amdgcn_exp2f((float)d2 *
+                                                               (h_levels[j] * 1.4426950408889634f));
+      acc += (e * rl[j]) * q[j];
+    }
+    if (mrow != nullptr && k < n) mrow[(size_t)li * n] = acc;
+    csum = fmaT<T>(d2, acc, csum);
+  }
+  const T t = block_sum(k < n ? csum : (T)0, red);
+  if (threadIdx.x == 0) part[((size_t)bb * gridDim.y + lb) * gridDim.x + kb] = t;
 }
 
 // grad1 partials: lanes over k, l split S ways: part[s][(bb*n + k)*3 + x].
@@ -313,7 +369,9 @@ size_t emd_ws_elems(int b, int n, int m) {
   // the region starts at 12 (bn + bm) elements: 16-B aligned for f32, 32-B for f64
   const size_t part = std::max({(size_t)S * b * std::max(n, m) * 3,
                                 (size_t)b * S * ceil_div(std::max(n, 1), kThreads),
-                                4 * (bn + 2 * bm)});
+                                4 * (bn + 2 * bm) +
+                                    (size_t)b * ceil_div(std::max(m, 1), kMatchL) *
+                                        ceil_div(std::max(n, 1), kThreads)});
   return 2 * (bn + bm) + kLevels * (bn + bm) + part;
 }
 
@@ -360,13 +418,20 @@ inline dim3 grid1d(size_t total, int threads = 256) {
 // ---------------------------------------------------------------------------
 constexpr int kRowWaves = 16;  // column splits per block, one wave each
 
-// A point with the coefficient it carries into a pass, 16 (f32) / 32 (f64)
-// bytes: a wave-uniform column read is one scalar load of point + coefficient
-// (the compiler merges consecutive columns into s_load_dwordx8/x16).
+// A point with the coefficient it carries into a pass (x, y, z, w = coef),
+// float4 / double4: a native vector type, so copies stay in registers.
 template <typename T>
-struct alignas(4 * sizeof(T)) Col4 {
-  T x, y, z, c;
+struct Vec4Of;
+template <>
+struct Vec4Of<float> {
+  using type = float4;
 };
+template <>
+struct Vec4Of<double> {
+  using type = double4;
+};
+template <typename T>
+using Col4 = typename Vec4Of<T>::type;
 
 // packK[b, k] = {xyz1, ratL};  packL0[b, l] = {xyz2, remR};  packL1[b, l] = {xyz2, ratR}
 template <typename T>
@@ -385,24 +450,56 @@ __global__ void emd_pack_kernel(const T* __restrict__ xyz1, size_t bn, T multiL,
                                 EmdRowState<T> s) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < bn) {
-    s.packK[i] = Col4<T>{xyz1[3 * i], xyz1[3 * i + 1], xyz1[3 * i + 2], (T)0};
+    s.packK[i] = Col4<T>(xyz1[3 * i], xyz1[3 * i + 1], xyz1[3 * i + 2], (T)0);
     s.remL[i] = multiL;
   }
   if (i < bm) {
     const T x = xyz2[3 * i], y = xyz2[3 * i + 1], z = xyz2[3 * i + 2];
-    s.packL0[i] = Col4<T>{x, y, z, multiR};
-    s.packL1[i] = Col4<T>{x, y, z, (T)0};
+    s.packL0[i] = Col4<T>(x, y, z, multiR);
+    s.packL1[i] = Col4<T>(x, y, z, (T)0);
   }
 }
 
 // PH 0: rows k (packK), cols packL0 (coef remR);  suml -> ratL = remL / (1e-9 + suml)  (:57-81)
 // PH 1: rows l (packL0), cols packK (coef ratL);  sumr -> ratR, levR[lvl], remR (fin2) (:86-116)
 // PH 2: rows k (packK, row scale ratL), cols packL1 (coef ratR);  -> remL, levL[lvl]   (:119-151)
-// grid = (ceil(nr / 64), b), 1024 threads.
+// grid = (ceil(nr / 64), b), 1024 threads.  Each wave stages its column slice
+// through a wave-private LDS chunk (one 16-B load per lane and column pair,
+// the next chunk's loads in flight while this one is used); the column loop
+// then reads a column as one broadcast ds_read, whose in-order completion
+// lets the compiler keep several in flight (scalar loads of the columns
+// complete out of order, so every use waited for all of them: 13.8 us/pass).
+constexpr int kColChunk = 128;  // columns per wave per LDS chunk
+
+template <typename T, int PH>
+__device__ __forceinline__ T rowpass_chunk(const Col4<T>* __restrict__ st, int cnt, T x1, T y1,
+                                           T z1, T rl, T lvl2, T acc) {
+  if (lvl2 == (T)0) {  // level 0: exp(0 * d2) = 1 exactly
+#pragma unroll 8
+    for (int c = 0; c < cnt; ++c) acc = fmaT<T>(PH == 2 ? rl : (T)1, st[c].w, acc);
+    return acc;
+  }
+#pragma unroll 8
+  for (int c = 0; c < cnt; ++c) {
+    const Col4<T> q = st[c];
+    const T d2 = sqdist3(q.x - x1, q.y - y1, q.z - z1);
+    // level * log2(e) folded into one float factor: level is -4^j, a power of
+    // two, so d2 * (level * log2 e) rounds exactly as emd_exp's (level * d2) * log2 e
+    const T e = (T)__builtin_amdgcn_exp2f((float)d2 * (float)lvl2);
+    if constexpr (PH == 2) {
+      acc = fmaT<T>(e * rl, q.w, acc);
+    } else {
+      acc = fmaT<T>(e, q.w, acc);
+    }
+  }
+  return acc;
+}
+
 template <typename T, int PH>
 __global__ void __launch_bounds__(64 * kRowWaves)
-    emd_rowpass_kernel(int nr, int ncol, T level, int lvl, EmdRowState<T> s) {
+    emd_rowpass_kernel(int nr, int ncol, T lvl2, int lvl, EmdRowState<T> s) {
   __shared__ T red[kRowWaves][64];
+  __shared__ Col4<T> stage[kRowWaves][kColChunk];
   Col4<T>* rows = PH == 1 ? s.packL0 : s.packK;
   const Col4<T>* __restrict__ cols = PH == 0 ? s.packL0 : (PH == 1 ? s.packK : s.packL1);
   const int bb = blockIdx.y, lane = threadIdx.x & 63;
@@ -410,21 +507,23 @@ __global__ void __launch_bounds__(64 * kRowWaves)
   const int i = blockIdx.x * 64 + lane;
   const int ii = i < nr ? i : nr - 1;
   const Col4<T> rp = rows[(size_t)bb * nr + ii];
-  const T rl = rp.c;  // PH 2: ratL of the row
+  const T rl = rp.w;  // PH 2: ratL of the row
   const int c0 = (int)(((long long)ncol * w) / kRowWaves);
   const int c1 = (int)(((long long)ncol * (w + 1)) / kRowWaves);
   const Col4<T>* __restrict__ cb = cols + (size_t)bb * ncol;
+  Col4<T>* st = stage[w];
   T acc = 0;
-#pragma unroll 8
-  for (int c = c0; c < c1; ++c) {
-    const Col4<T> q = cb[c];
-    const T d2 = sqdist3(q.x - rp.x, q.y - rp.y, q.z - rp.z);
-    const T e = emd_exp<T>(level * d2);
-    if constexpr (PH == 2) {
-      acc = fmaT<T>(e * rl, q.c, acc);
-    } else {
-      acc = fmaT<T>(e, q.c, acc);
-    }
+  // unconditional loads (index clamped to the batch element's last column; the
+  // extra columns are never read): no branch around a load in flight
+  const int cl = ncol - 1;
+  Col4<T> n0 = cb[min(c0 + lane, cl)], n1 = cb[min(c0 + 64 + lane, cl)];
+  for (int base = c0; base < c1; base += kColChunk) {
+    st[lane] = n0;
+    st[64 + lane] = n1;
+    const int nb = base + kColChunk;
+    n0 = cb[min(nb + lane, cl)];
+    n1 = cb[min(nb + 64 + lane, cl)];
+    acc = rowpass_chunk<T, PH>(st, min(kColChunk, c1 - base), rp.x, rp.y, rp.z, rl, lvl2, acc);
   }
   red[w][lane] = acc;
   __syncthreads();
@@ -435,15 +534,15 @@ __global__ void __launch_bounds__(64 * kRowWaves)
   const size_t idx = (size_t)bb * nr + i;
   const size_t lv = (size_t)lvl * gridDim.y * nr + idx;
   if constexpr (PH == 0) {
-    rows[idx].c = s.remL[idx] / ((T)1e-9f + t);
+    rows[idx].w = s.remL[idx] / ((T)1e-9f + t);
   } else if constexpr (PH == 1) {
-    const T r = rp.c;
+    const T r = rp.w;
     const T sumr = t * r;
     const T cons = (T)fminf((float)(r / (sumr + (T)1e-9f)), 1.0f);
     const T rat = cons * r;
-    s.packL1[idx].c = rat;
+    s.packL1[idx].w = rat;
     s.levR[lv] = rat;
-    rows[idx].c = (T)fmaxf(0.0f, (float)(r - sumr));
+    rows[idx].w = (T)fmaxf(0.0f, (float)(r - sumr));
   } else {
     s.remL[idx] = (T)fmaxf(0.0f, (float)(s.remL[idx] - t));
     s.levL[lv] = rl;
@@ -457,9 +556,10 @@ bool emd_split_form() {
   return e != nullptr && e[0] == 's';
 }
 
+// match (when non-null) and, when cost is non-null, the fused matchcost.
 template <typename T>
-int approxmatch_rowpass(const T* xyz1, const T* xyz2, int b, int n, int m, T* match, EmdWs<T> w,
-                        hipStream_t st) {
+int approxmatch_rowpass(const T* xyz1, const T* xyz2, int b, int n, int m, T* match, T* cost,
+                        EmdWs<T> w, hipStream_t st) {
   const size_t bn = (size_t)b * n, bm = (size_t)b * m;
   Col4<T>* pk = reinterpret_cast<Col4<T>*>(w.part);  // 16/32-B aligned: see emd_ws_elems
   EmdRowState<T> s{pk, pk + bn, pk + bn + bm, w.remL, w.levL, w.levR};
@@ -469,14 +569,18 @@ int approxmatch_rowpass(const T* xyz1, const T* xyz2, int b, int n, int m, T* ma
                      multiL, xyz2, bm, multiR, s);
   const dim3 gL(ceil_div(n, 64), b), gR(ceil_div(m, 64), b), blk(64 * kRowWaves);
   for (int j = 0; j < kLevels; ++j) {
-    const T level = (T)h_levels[j];
-    hipLaunchKernelGGL((emd_rowpass_kernel<T, 0>), gL, blk, 0, st, n, m, level, j, s);
-    hipLaunchKernelGGL((emd_rowpass_kernel<T, 1>), gR, blk, 0, st, m, n, level, j, s);
-    hipLaunchKernelGGL((emd_rowpass_kernel<T, 2>), gL, blk, 0, st, n, m, level, j, s);
+    const T lvl2 = (T)(h_levels[j] * 1.4426950408889634f);  // exact: level_j is a power of 2
+    hipLaunchKernelGGL((emd_rowpass_kernel<T, 0>), gL, blk, 0, st, n, m, lvl2, j, s);
+    hipLaunchKernelGGL((emd_rowpass_kernel<T, 1>), gR, blk, 0, st, m, n, lvl2, j, s);
+    hipLaunchKernelGGL((emd_rowpass_kernel<T, 2>), gL, blk, 0, st, n, m, lvl2, j, s);
   }
-  dim3 gm(ceil_div(n, kThreads), ceil_div(m, kLPer), b);
-  hipLaunchKernelGGL(emd_match_kernel<T>, gm, dim3(kThreads), 0, st, xyz1, xyz2, b, n, m, w.levL,
-                     w.levR, match);
+  const dim3 gm(ceil_div(n, kThreads), ceil_div(m, kMatchL), b);
+  T* cpart = w.part + 4 * (bn + 2 * bm);  // after the packs (emd_ws_elems)
+  hipLaunchKernelGGL(emd_match_cost_kernel<T>, gm, dim3(kThreads), 0, st, xyz1, xyz2, b, n, m,
+                     (const T*)w.levL, (const T*)w.levR, match, cpart);
+  if (cost != nullptr)
+    hipLaunchKernelGGL(emd_cost_fin_kernel<T>, dim3(b), dim3(64), 0, st, (const T*)cpart,
+                       (int)(gm.x * gm.y), cost);
   return check_launch("approxmatch");
 }
 
@@ -489,7 +593,7 @@ int approxmatch(const T* xyz1, const T* xyz2, int b, int n, int m, T* match, voi
                  emd_ws_elems(b, n, m) * sizeof(T));
   if (b == 0 || n == 0 || m == 0) return PCFM_OK;
   EmdWs<T> w = carve<T>(ws, b, n, m);
-  if (!emd_split_form()) return approxmatch_rowpass(xyz1, xyz2, b, n, m, match, w, st);
+  if (!emd_split_form()) return approxmatch_rowpass(xyz1, xyz2, b, n, m, match, (T*)nullptr, w, st);
   const int S = emd_splits(b, n, m);
   // multiL/multiR: integer ratio of the cloud sizes (:27-33)
   const T multiL = n >= m ? (T)1 : (T)(m / n);
@@ -522,6 +626,30 @@ int approxmatch(const T* xyz1, const T* xyz2, int b, int n, int m, T* match, voi
   return check_launch("approxmatch");
 }
 
+// approxmatch + matchcost in one call (row-pass form; the cost from the match
+// kernel's partials).  match may be null: the cost alone, match not written.
+template <typename T>
+int approxmatch_cost(const T* xyz1, const T* xyz2, int b, int n, int m, T* match, T* cost,
+                     void* ws, size_t ws_bytes, hipStream_t st) {
+  PCFM_CHECK_ARG(b >= 0 && n >= 0 && m >= 0, "approxmatch_cost: negative size");
+  PCFM_CHECK_ARG(cost != nullptr, "approxmatch_cost: cost is required");
+  PCFM_CHECK_ARG(ws_bytes >= emd_ws_elems(b, n, m) * sizeof(T),
+                 "approxmatch_cost: workspace %zu < %zu bytes", ws_bytes,
+                 emd_ws_elems(b, n, m) * sizeof(T));
+  if (b == 0) return PCFM_OK;
+  if (n == 0 || m == 0) {
+    hipError_t e = hipMemsetAsync(cost, 0, (size_t)b * sizeof(T), st);
+    if (e == hipSuccess && match != nullptr)
+      e = hipMemsetAsync(match, 0, (size_t)b * n * m * sizeof(T), st);
+    if (e != hipSuccess) {
+      set_error("approxmatch_cost: hipMemsetAsync: %s", hipGetErrorString(e));
+      return (int)e;
+    }
+    return PCFM_OK;
+  }
+  return approxmatch_rowpass(xyz1, xyz2, b, n, m, match, cost, carve<T>(ws, b, n, m), st);
+}
+
 template <typename T>
 int matchcost(const T* xyz1, const T* xyz2, const T* match, int b, int n, int m, T* cost,
               void* ws, size_t ws_bytes, hipStream_t st) {
@@ -544,7 +672,7 @@ int matchcost(const T* xyz1, const T* xyz2, const T* match, int b, int n, int m,
   hipLaunchKernelGGL(emd_cost_kernel<T>, g, dim3(kThreads), 0, st, xyz1, xyz2, match, b, n, m, S,
                      w.part);
   const int per_b = S * (int)g.x;
-  hipLaunchKernelGGL(emd_cost_fin_kernel<T>, grid1d(b, 64), dim3(64), 0, st, w.part, per_b, b,
+  hipLaunchKernelGGL(emd_cost_fin_kernel<T>, dim3(b), dim3(64), 0, st, (const T*)w.part, per_b,
                      cost);
   return check_launch("matchcost");
 }
@@ -596,6 +724,18 @@ extern "C" int pcfm_emd_approxmatch_f64(const double* xyz1, const double* xyz2, 
                                         int m, double* match, void* ws, size_t ws_bytes,
                                         void* stream) {
   return approxmatch<double>(xyz1, xyz2, b, n, m, match, ws, ws_bytes, (hipStream_t)stream);
+}
+extern "C" int pcfm_emd_approxmatch_cost_f32(const float* xyz1, const float* xyz2, int b, int n,
+                                             int m, float* match, float* cost, void* ws,
+                                             size_t ws_bytes, void* stream) {
+  return approxmatch_cost<float>(xyz1, xyz2, b, n, m, match, cost, ws, ws_bytes,
+                                 (hipStream_t)stream);
+}
+extern "C" int pcfm_emd_approxmatch_cost_f64(const double* xyz1, const double* xyz2, int b, int n,
+                                             int m, double* match, double* cost, void* ws,
+                                             size_t ws_bytes, void* stream) {
+  return approxmatch_cost<double>(xyz1, xyz2, b, n, m, match, cost, ws, ws_bytes,
+                                  (hipStream_t)stream);
 }
 extern "C" int pcfm_emd_matchcost_f32(const float* xyz1, const float* xyz2, const float* match,
                                       int b, int n, int m, float* cost, void* ws,

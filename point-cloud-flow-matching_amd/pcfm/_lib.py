@@ -44,6 +44,8 @@ SIGNATURES = {
     "pcfm_emd_workspace_bytes": (_Z, [_I, _I, _I, _I]),
     "pcfm_emd_approxmatch_f32": (_I, [_P, _P, _I, _I, _I, _P, _P, _Z, _P]),
     "pcfm_emd_approxmatch_f64": (_I, [_P, _P, _I, _I, _I, _P, _P, _Z, _P]),
+    "pcfm_emd_approxmatch_cost_f32": (_I, [_P, _P, _I, _I, _I, _P, _P, _P, _Z, _P]),
+    "pcfm_emd_approxmatch_cost_f64": (_I, [_P, _P, _I, _I, _I, _P, _P, _P, _Z, _P]),
     "pcfm_emd_matchcost_f32": (_I, [_P, _P, _P, _I, _I, _I, _P, _P, _Z, _P]),
     "pcfm_emd_matchcost_f64": (_I, [_P, _P, _P, _I, _I, _I, _P, _P, _Z, _P]),
     "pcfm_emd_matchcost_bwd_f32": (_I, [_P, _P, _P, _P, _I, _I, _I, _P, _P, _P, _Z, _P]),
@@ -129,7 +131,7 @@ SIGNATURES = {
     "pcfm_adamw_ema_step": (_I, [_P, _P, _I, _P, _P, _I, _DP, _DP, _D, _D, _D, _D, _P]),
 }
 
-ABI_VERSION = 17
+ABI_VERSION = 18
 
 _lock = threading.Lock()
 _lib = None

@@ -615,6 +615,25 @@ def matchcost_forward(xyz1: torch.Tensor, xyz2: torch.Tensor, match: torch.Tenso
     return cost
 
 
+def approxmatch_cost_forward(xyz1: torch.Tensor, xyz2: torch.Tensor, want_match: bool = True):
+    """approxmatch_forward + matchcost_forward in one native call (the forward
+    of PyTorchEMD/emd.py:14-19): -> (match (B, M, N) or None, cost (B,)).  The
+    cost is summed from the match kernel's own values; want_match=False skips
+    writing match (a forward whose inputs need no gradient)."""
+    xyz1, xyz2 = xyz1.contiguous(), xyz2.contiguous()
+    if _host(xyz1, xyz2):
+        _emd_check(xyz1, xyz2)
+        match = cpu_ops.approxmatch_forward(xyz1, xyz2)
+        return (match if want_match else None), cpu_ops.matchcost_forward(xyz1, xyz2, match)
+    sfx, b, n, m, ws = _emd_args(xyz1, xyz2)
+    match = torch.empty((b, m, n), dtype=xyz1.dtype, device=xyz1.device) if want_match else None
+    cost = torch.empty((b,), dtype=xyz1.dtype, device=xyz1.device)
+    _lib.call(f"pcfm_emd_approxmatch_cost_{sfx}", _ptr(xyz1), _ptr(xyz2), b, n, m,
+              _ptr(match) if match is not None else None, _ptr(cost), _ptr(ws), ws.numel(),
+              _stream(xyz1))
+    return match, cost
+
+
 def matchcost_backward(grad_cost: torch.Tensor, xyz1: torch.Tensor, xyz2: torch.Tensor,
                        match: torch.Tensor):
     """emd_kernel.cu:371-396: -> [grad1 (B,N,3), grad2 (B,M,3)]"""

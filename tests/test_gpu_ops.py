@@ -385,6 +385,25 @@ def test_emd_vs_oracle(dtype, b, n, m):
     np.testing.assert_allclose(np_(g2), e2, rtol=1e-4, atol=1e-5)
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+@pytest.mark.parametrize("b,n,m", [(2, 64, 64), (3, 100, 37), (2, 37, 700), (8, 2048, 2048)])
+def test_emd_fused_cost_matches_two_calls(dtype, b, n, m):
+    """pcfm_emd_approxmatch_cost (the product forward of emd.py): the match
+    it writes is bit-identical to approxmatch_forward's, its cost equals
+    matchcost_forward on that match to summation order, and the cost-only form
+    (no match written) returns the same bits (emd_kernel.cu:169-277)."""
+    from pcfm import ops
+    g = torch.Generator(device=DEV).manual_seed(n + m)
+    a = torch.rand(b, n, 3, device=DEV, generator=g, dtype=dtype)
+    c = torch.rand(b, m, 3, device=DEV, generator=g, dtype=dtype)
+    match, cost = ops.approxmatch_cost_forward(a, c)
+    assert torch.equal(match, ops.approxmatch_forward(a, c))
+    ref = ops.matchcost_forward(a, c, match)
+    torch.testing.assert_close(cost, ref, rtol=1e-5 if dtype == torch.float32 else 1e-12, atol=0)
+    none, cost2 = ops.approxmatch_cost_forward(a, c, want_match=False)
+    assert none is None and torch.equal(cost, cost2)
+
+
 def test_emd_known_answer(golden):
     from PyTorchEMD.emd import earth_mover_distance
     g = golden("emd_known.npz")
