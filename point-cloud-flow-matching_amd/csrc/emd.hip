@@ -10,7 +10,8 @@
 //     included: a block owns 64 rows (lanes), its 16 waves split the column
 //     range (wave-uniform, so the column points arrive through scalar loads),
 //     the wave sums of a row are added in a fixed order in LDS and the row's
-//     finalize runs in the same block (31 launches per approxmatch);
+//     finalize runs in the same block; a level's third pass and the next
+//     level's first share one launch (21 launches per approxmatch);
 //   * match is NOT accumulated level by level.  Each level only needs the
 //     vectors ratioL (n) and ratioR (m), which are kept per level (10 x (n+m));
 //     match is written once at the end as
@@ -406,7 +407,9 @@ inline dim3 grid1d(size_t total, int threads = 256) {
 // and splits the column range over its 16 waves; the 16 wave sums of a row
 // are added in wave order in LDS and the row's finalize (fin1 / fin2 / fin3
 // of the split form) runs right there, so the next pass reads finished
-// coefficients.  31 launches per approxmatch (init + 30) plus the match write.
+// coefficients.  A level's third pass and the next level's first pass walk
+// the same (row k, column l) pairs, so they share one launch and one d2 per
+// pair: 21 pass launches + the pack + the match write (with the cost fused).
 // Measured history (B = 8, N = 2048, MI355X): the split form below (6 launches
 // per level, S-way partials reduced by separate finalize kernels) 0.67 ms; a
 // form with the finalizes folded into the next pass, each block re-reducing
@@ -414,7 +417,8 @@ inline dim3 grid1d(size_t total, int threads = 256) {
 // of every pass); the round-3 cooperative one-launch form with
 // cooperative_groups grid barriers 4.45 ms (a grid.sync() costs ~0.1 us per
 // block on ROCm 7.2, ~100 us at 1024 blocks, against ~1.7 us for a kernel
-// boundary).
+// boundary); this form with 30 separate pass launches and scalar-loaded
+// columns 0.51 ms, with LDS-staged columns and the fused cost 0.39 ms.
 // ---------------------------------------------------------------------------
 constexpr int kRowWaves = 16;  // column splits per block, one wave each
 
@@ -469,7 +473,7 @@ __global__ void emd_pack_kernel(const T* __restrict__ xyz1, size_t bn, T multiL,
 // then reads a column as one broadcast ds_read, whose in-order completion
 // lets the compiler keep several in flight (scalar loads of the columns
 // complete out of order, so every use waited for all of them: 13.8 us/pass).
-constexpr int kColChunk = 128;  // columns per wave per LDS chunk
+constexpr int kColChunk = 128;  // columns per wave per LDS chunk (64 for PH 3: two packs)
 
 template <typename T, int PH>
 __device__ __forceinline__ T rowpass_chunk(const Col4<T>* __restrict__ st, int cnt, T x1, T y1,
@@ -495,10 +499,41 @@ __device__ __forceinline__ T rowpass_chunk(const Col4<T>* __restrict__ st, int c
   return acc;
 }
 
+// PH 3 = PH 2 of level j fused with PH 0 of level j+1 (same rows k, same
+// columns l, one d2 per pair): st[c] = {xyz2, ratR_j}, st[64 + c].w = remR_{j+1}
+template <typename T>
+__device__ __forceinline__ void rowpass_pair(const Col4<T>* __restrict__ st, int cnt, T x1, T y1,
+                                             T z1, T rl, T lvl2, T lvl2b, T& acc2, T& acc0) {
+#pragma unroll 8
+  for (int c = 0; c < cnt; ++c) {
+    const Col4<T> q = st[c];
+    const T rr = st[64 + c].w;
+    const float d2 = (float)sqdist3(q.x - x1, q.y - y1, q.z - z1);
+    const T e2 = (T)__builtin_amdgcn_exp2f(d2 * (float)lvl2);
+    const T e0 = (T)__builtin_amdgcn_exp2f(d2 * (float)lvl2b);
+    acc2 = fmaT<T>(e2 * rl, q.w, acc2);
+    acc0 = fmaT<T>(e0, rr, acc0);
+  }
+}
+
+// PH 0: rows k (packK), cols packL0 (coef remR);  suml -> ratL = remL / (1e-9 + suml)  (:57-81)
+// PH 1: rows l (packL0), cols packK (coef ratL);  sumr -> ratR, levR[lvl], remR (fin2) (:86-116)
+// PH 2: rows k (packK, row scale ratL), cols packL1 (coef ratR);  -> remL, levL[lvl]   (:119-151)
+// PH 3: PH 2 of level lvl then PH 0 of level lvl+1 (lvl2b), one launch: the
+//       column sums of both are taken in the same order as the two launches,
+//       so the result is bit-identical (PCFM_EMD_FORM=unfused runs them apart).
+// grid = (ceil(nr / 64), b), 1024 threads.  Each wave stages its column slice
+// through a wave-private LDS chunk (16-B loads, the next chunk's loads in
+// flight while this one is used); the column loop then reads a column as one
+// broadcast ds_read, whose in-order completion lets the compiler keep several
+// in flight (scalar loads of the columns complete out of order, so every use
+// waited for all of them: 13.8 us/pass).
 template <typename T, int PH>
 __global__ void __launch_bounds__(64 * kRowWaves)
-    emd_rowpass_kernel(int nr, int ncol, T lvl2, int lvl, EmdRowState<T> s) {
+    emd_rowpass_kernel(int nr, int ncol, T lvl2, T lvl2b, int lvl, EmdRowState<T> s) {
+  constexpr int CH = PH == 3 ? 64 : kColChunk;
   __shared__ T red[kRowWaves][64];
+  __shared__ T red2[PH == 3 ? kRowWaves : 1][64];
   __shared__ Col4<T> stage[kRowWaves][kColChunk];
   Col4<T>* rows = PH == 1 ? s.packL0 : s.packK;
   const Col4<T>* __restrict__ cols = PH == 0 ? s.packL0 : (PH == 1 ? s.packK : s.packL1);
@@ -507,30 +542,43 @@ __global__ void __launch_bounds__(64 * kRowWaves)
   const int i = blockIdx.x * 64 + lane;
   const int ii = i < nr ? i : nr - 1;
   const Col4<T> rp = rows[(size_t)bb * nr + ii];
-  const T rl = rp.w;  // PH 2: ratL of the row
+  const T rl = rp.w;  // PH 2 / 3: ratL of the row
   const int c0 = (int)(((long long)ncol * w) / kRowWaves);
   const int c1 = (int)(((long long)ncol * (w + 1)) / kRowWaves);
   const Col4<T>* __restrict__ cb = cols + (size_t)bb * ncol;
+  const Col4<T>* __restrict__ cb2 = s.packL0 + (size_t)bb * ncol;  // PH 3's remR_{lvl+1}
   Col4<T>* st = stage[w];
-  T acc = 0;
+  T acc = 0, acc2 = 0;
   // unconditional loads (index clamped to the batch element's last column; the
   // extra columns are never read): no branch around a load in flight
   const int cl = ncol - 1;
-  Col4<T> n0 = cb[min(c0 + lane, cl)], n1 = cb[min(c0 + 64 + lane, cl)];
-  for (int base = c0; base < c1; base += kColChunk) {
+  Col4<T> n0, n1;
+  auto fetch = [&](int base) {
+    n0 = cb[min(base + lane, cl)];
+    n1 = PH == 3 ? cb2[min(base + lane, cl)] : cb[min(base + 64 + lane, cl)];
+  };
+  fetch(c0);
+  for (int base = c0; base < c1; base += CH) {
     st[lane] = n0;
     st[64 + lane] = n1;
-    const int nb = base + kColChunk;
-    n0 = cb[min(nb + lane, cl)];
-    n1 = cb[min(nb + 64 + lane, cl)];
-    acc = rowpass_chunk<T, PH>(st, min(kColChunk, c1 - base), rp.x, rp.y, rp.z, rl, lvl2, acc);
+    fetch(base + CH);
+    const int cnt = min(CH, c1 - base);
+    if constexpr (PH == 3) {
+      rowpass_pair<T>(st, cnt, rp.x, rp.y, rp.z, rl, lvl2, lvl2b, acc2, acc);
+    } else {
+      acc = rowpass_chunk<T, PH>(st, cnt, rp.x, rp.y, rp.z, rl, lvl2, acc);
+    }
   }
   red[w][lane] = acc;
+  if constexpr (PH == 3) red2[w][lane] = acc2;
   __syncthreads();
   if (w != 0 || i >= nr) return;
-  T t = 0;
+  T t = 0, t2 = 0;
 #pragma unroll
-  for (int q = 0; q < kRowWaves; ++q) t += red[q][lane];
+  for (int q = 0; q < kRowWaves; ++q) {
+    t += red[q][lane];
+    if constexpr (PH == 3) t2 += red2[q][lane];
+  }
   const size_t idx = (size_t)bb * nr + i;
   const size_t lv = (size_t)lvl * gridDim.y * nr + idx;
   if constexpr (PH == 0) {
@@ -543,17 +591,27 @@ __global__ void __launch_bounds__(64 * kRowWaves)
     s.packL1[idx].w = rat;
     s.levR[lv] = rat;
     rows[idx].w = (T)fmaxf(0.0f, (float)(r - sumr));
-  } else {
+  } else if constexpr (PH == 2) {
     s.remL[idx] = (T)fmaxf(0.0f, (float)(s.remL[idx] - t));
     s.levL[lv] = rl;
+  } else {
+    const T rem = (T)fmaxf(0.0f, (float)(s.remL[idx] - t2));  // level lvl's fin3
+    s.remL[idx] = rem;
+    s.levL[lv] = rl;
+    rows[idx].w = rem / ((T)1e-9f + t);  // level lvl+1's ratL
   }
 }
 
 // PCFM_EMD_FORM=split: every pass and finalize its own launch, S-way partials
-// (measurement / the cross-form test); default: the row-pass form
+// (measurement / the cross-form test); =unfused: the row-pass form with PH 2
+// and the next level's PH 0 as separate launches; default: the fused row-pass form
 bool emd_split_form() {
   const char* e = std::getenv("PCFM_EMD_FORM");
   return e != nullptr && e[0] == 's';
+}
+bool emd_unfused_form() {
+  const char* e = std::getenv("PCFM_EMD_FORM");
+  return e != nullptr && e[0] == 'u';
 }
 
 // match (when non-null) and, when cost is non-null, the fused matchcost.
@@ -568,11 +626,21 @@ int approxmatch_rowpass(const T* xyz1, const T* xyz2, int b, int n, int m, T* ma
   hipLaunchKernelGGL(emd_pack_kernel<T>, grid1d(std::max(bn, bm)), dim3(256), 0, st, xyz1, bn,
                      multiL, xyz2, bm, multiR, s);
   const dim3 gL(ceil_div(n, 64), b), gR(ceil_div(m, 64), b), blk(64 * kRowWaves);
+  // level_j * log2(e), exact in float: level_j is a power of two
+  auto lv2 = [](int j) { return (T)(h_levels[j] * 1.4426950408889634f); };
+  const bool fused = !emd_unfused_form();
+  hipLaunchKernelGGL((emd_rowpass_kernel<T, 0>), gL, blk, 0, st, n, m, lv2(0), (T)0, 0, s);
   for (int j = 0; j < kLevels; ++j) {
-    const T lvl2 = (T)(h_levels[j] * 1.4426950408889634f);  // exact: level_j is a power of 2
-    hipLaunchKernelGGL((emd_rowpass_kernel<T, 0>), gL, blk, 0, st, n, m, lvl2, j, s);
-    hipLaunchKernelGGL((emd_rowpass_kernel<T, 1>), gR, blk, 0, st, m, n, lvl2, j, s);
-    hipLaunchKernelGGL((emd_rowpass_kernel<T, 2>), gL, blk, 0, st, n, m, lvl2, j, s);
+    hipLaunchKernelGGL((emd_rowpass_kernel<T, 1>), gR, blk, 0, st, m, n, lv2(j), (T)0, j, s);
+    if (fused && j + 1 < kLevels) {
+      hipLaunchKernelGGL((emd_rowpass_kernel<T, 3>), gL, blk, 0, st, n, m, lv2(j), lv2(j + 1), j,
+                         s);
+    } else {
+      hipLaunchKernelGGL((emd_rowpass_kernel<T, 2>), gL, blk, 0, st, n, m, lv2(j), (T)0, j, s);
+      if (j + 1 < kLevels)
+        hipLaunchKernelGGL((emd_rowpass_kernel<T, 0>), gL, blk, 0, st, n, m, lv2(j + 1), (T)0,
+                           j + 1, s);
+    }
   }
   const dim3 gm(ceil_div(n, kThreads), ceil_div(m, kMatchL), b);
   T* cpart = w.part + 4 * (bn + 2 * bm);  // after the packs (emd_ws_elems)

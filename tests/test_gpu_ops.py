@@ -443,7 +443,8 @@ def test_chamfer_c2_product_path(tmp_path, report):
 def test_emd_rowpass_form_matches_split_form(tmp_path, report):
     """approxmatch's row-pass form (one launch per pass of each level, the
     finalize in the same block, the 16 column slices of a row summed in a fixed
-    order: 31 launches) against the split form (every pass and finalize its own
+    order; a level's third pass and the next level's first share one launch:
+    21 launches; bit-identical to the unfused 31) against the split form (every pass and finalize its own
     launch, S-way partial sums: 62): the same matches to fp32 round-off over
     f32/f64, n >< m and ragged sizes (tests/helpers/emd_forms.py;
     emd_kernel.cu:24-156) -- the two differ only in the order of the column
@@ -454,13 +455,16 @@ def test_emd_rowpass_form_matches_split_form(tmp_path, report):
     import sys
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     res = {}
-    for form in ("split", "rowpass"):
+    for form in ("split", "rowpass", "unfused"):
         env = dict(os.environ, PCFM_EMD_FORM=form)
         subprocess.run([sys.executable, os.path.join(repo, "tests", "helpers", "emd_forms.py"),
                         str(tmp_path / f"m{form}.npz"), str(tmp_path / f"t{form}.json")],
                        check=True, timeout=120, env=env, cwd=repo)
         res[form] = json.load(open(tmp_path / f"t{form}.json"))
     a, b = np.load(tmp_path / "msplit.npz"), np.load(tmp_path / "mrowpass.npz")
+    u = np.load(tmp_path / "munfused.npz")
+    for k in b.files:  # level j's third pass fused with level j+1's first: same sums, same order
+        np.testing.assert_array_equal(b[k], u[k], err_msg=k)
     worst = 0.0
     for k in a.files:
         x, y = a[k], b[k]
@@ -472,4 +476,5 @@ def test_emd_rowpass_form_matches_split_form(tmp_path, report):
         np.testing.assert_allclose(x.sum(axis=(1, 2)), y.sum(axis=(1, 2)), rtol=tol * 10, err_msg=k)
     report("emd_forms", {"split_ms": res["split"]["approxmatch_ms_b8_n2048"],
                          "rowpass_ms": res["rowpass"]["approxmatch_ms_b8_n2048"],
+                         "rowpass_unfused_ms": res["unfused"]["approxmatch_ms_b8_n2048"],
                          "max_rel_diff_f32": worst})
