@@ -46,7 +46,7 @@ extern "C" {
  * voxel convolution entry points; 14: voxel-list form of the voxel convolution;
  * 15: the head FiLM backward takes shift and recomputes u; 16: devoxelization
  * self-check entry point; 17: BatchNorm statistics from the pointwise GEMM's
- * epilogue; 18: fused EMD approxmatch + matchcost). */
+ * epilogue; 18: fused EMD approxmatch + matchcost, SE3d MLP kernels). */
 int pcfm_abi_version(void);
 /* Thread-local text of the last non-zero return code. */
 const char* pcfm_last_error(void);
@@ -111,6 +111,16 @@ int pcfm_debug_devox_verify(const float* coords, const float* feat, const float*
                             const float* add, const float* out, const int* inds,
                             const float* wgts, int b, int c, int n, int r, int* rec,
                             void* stream);
+
+/* SE3d's channel MLP (modules/se.py over pvconv.py:35-39; se.py:9-19):
+ *   hid [b][h] = relu(m [b][c] . W1^T), W1 [h][c];  s [b][c] = sigmoid(hid . W2^T), W2 [c][h]
+ * and its backward from ds [b][c]: dm [b][c] (times dm_scale), dW1 [h][c], dW2 [c][h].
+ * One single-block launch each; b * (c + h) <= 16384 (else PCFM_EINVAL). */
+int pcfm_se_mlp_fwd(const float* m, const float* w1, const float* w2, int b, int c, int h,
+                    float* hid, float* s, void* stream);
+int pcfm_se_mlp_bwd(const float* m, const float* hid, const float* s, const float* ds,
+                    const float* w1, const float* w2, int b, int c, int h, float dm_scale,
+                    float* dm, float* dw1, float* dw2, void* stream);
 
 /* out[r] = scale * sum_v a[r][v] * b[r][v] (b NULL: plain row sum), rows of
  * `len` floats; deterministic.  (SE3d pooling and its scale gradient.) */

@@ -347,6 +347,103 @@ extern "C" int pcfm_trilinear_devoxelize_bwd_planned(const float* grad_y, const 
   return e ? e : check_launch("trilinear_devoxelize_bwd_planned");
 }
 
+// ---------------------------------------------------------------------------
+// SE3d's channel MLP (modules/se.py: s = sigmoid(W2 relu(W1 m)), m the pooled
+// grid, bias-free Linears) and its backward, each ONE single-block launch: the
+// products are B x C x C/r multiply-adds (8 x 256 x 32 at C2), which as torch
+// ops were ~12 launches of a few microseconds per PVConv.  Fixed summation
+// order (deterministic); fp32 like the module.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(1024)
+    se_mlp_fwd_kernel(const float* __restrict__ m, const float* __restrict__ w1,
+                      const float* __restrict__ w2, int b, int c, int h, float* __restrict__ hid,
+                      float* __restrict__ s) {
+  extern __shared__ float sh[];  // hid [b][h]
+  for (int e = threadIdx.x; e < b * h; e += blockDim.x) {
+    const int bi = e / h, j = e - bi * h;
+    const float* mr = m + (size_t)bi * c;
+    const float* wr = w1 + (size_t)j * c;
+    float acc = 0.0f;
+    for (int k = 0; k < c; ++k) acc = __builtin_fmaf(mr[k], wr[k], acc);
+    const float v = fmaxf(acc, 0.0f);
+    sh[e] = v;
+    hid[e] = v;
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < b * c; e += blockDim.x) {
+    const int bi = e / c, k = e - bi * c;
+    const float* hr = sh + bi * h;
+    const float* wr = w2 + (size_t)k * h;
+    float acc = 0.0f;
+    for (int j = 0; j < h; ++j) acc = __builtin_fmaf(hr[j], wr[j], acc);
+    s[e] = 1.0f / (1.0f + expf(-acc));
+  }
+}
+
+// ds -> dm (scaled by dm_scale: the pooling's 1/V folded in), dW1, dW2.
+__global__ void __launch_bounds__(1024)
+    se_mlp_bwd_kernel(const float* __restrict__ m, const float* __restrict__ hid,
+                      const float* __restrict__ s, const float* __restrict__ ds,
+                      const float* __restrict__ w1, const float* __restrict__ w2, int b, int c,
+                      int h, float dm_scale, float* __restrict__ dm, float* __restrict__ dw1,
+                      float* __restrict__ dw2) {
+  extern __shared__ float sh[];  // dz2 [b][c], dz1 [b][h]
+  float* dz2 = sh;
+  float* dz1 = sh + b * c;
+  for (int e = threadIdx.x; e < b * c; e += blockDim.x) {
+    const float sv = s[e];
+    dz2[e] = ds[e] * (1.0f - sv) * sv;  // torch's sigmoid backward expression
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < c * h; e += blockDim.x) {  // dW2 [c][h]
+    const int k = e / h, j = e - k * h;
+    float acc = 0.0f;
+    for (int bi = 0; bi < b; ++bi) acc = __builtin_fmaf(dz2[bi * c + k], hid[bi * h + j], acc);
+    dw2[e] = acc;
+  }
+  for (int e = threadIdx.x; e < b * h; e += blockDim.x) {  // dh -> relu backward
+    const int bi = e / h, j = e - bi * h;
+    float acc = 0.0f;
+    for (int k = 0; k < c; ++k) acc = __builtin_fmaf(dz2[bi * c + k], w2[(size_t)k * h + j], acc);
+    dz1[e] = hid[e] > 0.0f ? acc : 0.0f;
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < h * c; e += blockDim.x) {  // dW1 [h][c]
+    const int j = e / c, k = e - j * c;
+    float acc = 0.0f;
+    for (int bi = 0; bi < b; ++bi) acc = __builtin_fmaf(dz1[bi * h + j], m[(size_t)bi * c + k], acc);
+    dw1[e] = acc;
+  }
+  for (int e = threadIdx.x; e < b * c; e += blockDim.x) {  // dm [b][c]
+    const int bi = e / c, k = e - bi * c;
+    float acc = 0.0f;
+    for (int j = 0; j < h; ++j) acc = __builtin_fmaf(dz1[bi * h + j], w1[(size_t)j * c + k], acc);
+    dm[e] = acc * dm_scale;
+  }
+}
+
+static bool se_mlp_ok(int b, int c, int h) {
+  return b > 0 && c > 0 && h > 0 && (long long)b * c + (long long)b * h <= 16384;
+}
+
+extern "C" int pcfm_se_mlp_fwd(const float* m, const float* w1, const float* w2, int b, int c,
+                               int h, float* hid, float* s, void* stream) {
+  PCFM_CHECK_ARG(se_mlp_ok(b, c, h), "se_mlp_fwd: unsupported size b=%d c=%d h=%d", b, c, h);
+  hipLaunchKernelGGL(se_mlp_fwd_kernel, dim3(1), dim3(1024), (size_t)b * h * sizeof(float),
+                     (hipStream_t)stream, m, w1, w2, b, c, h, hid, s);
+  return check_launch("se_mlp_fwd");
+}
+
+extern "C" int pcfm_se_mlp_bwd(const float* m, const float* hid, const float* s, const float* ds,
+                               const float* w1, const float* w2, int b, int c, int h,
+                               float dm_scale, float* dm, float* dw1, float* dw2, void* stream) {
+  PCFM_CHECK_ARG(se_mlp_ok(b, c, h), "se_mlp_bwd: unsupported size b=%d c=%d h=%d", b, c, h);
+  hipLaunchKernelGGL(se_mlp_bwd_kernel, dim3(1), dim3(1024),
+                     ((size_t)b * c + (size_t)b * h) * sizeof(float), (hipStream_t)stream, m, hid,
+                     s, ds, w1, w2, b, c, h, dm_scale, dm, dw1, dw2);
+  return check_launch("se_mlp_bwd");
+}
+
 extern "C" int pcfm_rows_dot(const float* a, const float* b, long long rows, int len, float scale,
                              float* out, void* stream) {
   PCFM_CHECK_ARG(rows >= 0 && rows < (1LL << 31) && len >= 0, "rows_dot: bad size %lld x %d",

@@ -30,6 +30,10 @@ def _conv_bn_lrelu(cin, cout, kernel_size):
     ]
 
 
+# SE3d's MLP as one kernel each way (PCFM_SE_FUSED=0: torch ops, A/B knob)
+_SE_FUSED = __import__("os").environ.get("PCFM_SE_FUSED", "1") != "0"
+
+
 def _se_scale(m, w1, w2):
     return torch.sigmoid(TF.linear(TF.relu(TF.linear(m, w1)), w2))
 
@@ -49,7 +53,13 @@ class _SEDevoxAdd(torch.autograd.Function):
         v = grid[0, 0].numel()
         rows = grid.contiguous().view(b * c, v)
         m = ops.rows_dot(rows, None, 1.0 / v).view(b, c)
-        s = _se_scale(m, w1, w2).contiguous()
+        w1, w2 = w1.contiguous(), w2.contiguous()
+        # the SE MLP as one kernel each way (pcfm_se_mlp_*), torch ops beyond its size
+        fused = _SE_FUSED and ops.se_mlp_ok(m, w1)
+        if fused:
+            s, hid = ops.se_mlp_forward(m, w1, w2)
+        else:
+            s, hid = _se_scale(m, w1, w2).contiguous(), m.new_empty(0)
         # the corner indices / weights depend on the points only: the second
         # block of a stage reuses the first one's (pcfm.plans) and skips writing
         shared = plans.devox_corners(coords, r) if training else None
@@ -60,8 +70,8 @@ class _SEDevoxAdd(torch.autograd.Function):
         elif training:
             plans.put_devox_corners(coords, r, inds, wgts)
         if training:
-            ctx.save_for_backward(rows, inds, wgts, m, s, w1, w2)
-            ctx.r, ctx.shape = r, grid.shape
+            ctx.save_for_backward(rows, inds, wgts, m, s, w1, w2, hid)
+            ctx.r, ctx.shape, ctx.fused = r, grid.shape, fused
             ctx.points = coords  # key of the shared backward plan (pcfm.plans)
         return out
 
@@ -69,7 +79,7 @@ class _SEDevoxAdd(torch.autograd.Function):
     def backward(ctx, dout):
         from pcfm import ops
         from pcfm import plans
-        rows, inds, wgts, m, s, w1, w2 = ctx.saved_tensors
+        rows, inds, wgts, m, s, w1, w2, hid = ctx.saved_tensors
         dout = dout.contiguous()
         if plans.ENABLED:
             plan = plans.devox_bwd_plan(ctx.points, inds, wgts, ctx.r)
@@ -77,12 +87,16 @@ class _SEDevoxAdd(torch.autograd.Function):
         else:
             g = ops.trilinear_devoxelize_backward(dout, inds, wgts, ctx.r).view_as(rows)
         ds = ops.rows_dot(rows, g, 1.0).view_as(s)
-        with torch.enable_grad():
-            m_ = m.detach().requires_grad_(True)
-            w1_ = w1.detach().requires_grad_(True)
-            w2_ = w2.detach().requires_grad_(True)
-            dm, dw1, dw2 = torch.autograd.grad(_se_scale(m_, w1_, w2_), [m_, w1_, w2_], ds)
-        ops.rows_affine_(g, s.view(-1), (dm / rows.shape[1]).contiguous().view(-1))
+        if ctx.fused:  # d mean / V straight out of the MLP backward
+            dmv, dw1, dw2 = ops.se_mlp_backward(m, hid, s, ds, w1, w2, 1.0 / rows.shape[1])
+        else:
+            with torch.enable_grad():
+                m_ = m.detach().requires_grad_(True)
+                w1_ = w1.detach().requires_grad_(True)
+                w2_ = w2.detach().requires_grad_(True)
+                dm, dw1, dw2 = torch.autograd.grad(_se_scale(m_, w1_, w2_), [m_, w1_, w2_], ds)
+            dmv = (dm / rows.shape[1]).contiguous()
+        ops.rows_affine_(g, s.view(-1), dmv.view(-1))
         return g.view(ctx.shape), None, dout, dw1, dw2, None, None
 
 

@@ -78,6 +78,8 @@ SIGNATURES = {
     "pcfm_trilinear_devoxelize_scale_add_fwd": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P,
                                                      _P, _P]),
     "pcfm_debug_devox_verify": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _P]),
+    "pcfm_se_mlp_fwd": (_I, [_P, _P, _P, _I, _I, _I, _P, _P, _P]),
+    "pcfm_se_mlp_bwd": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _F, _P, _P, _P, _P]),
     "pcfm_rows_dot": (_I, [_P, _P, _L, _I, _F, _P, _P]),
     "pcfm_rows_affine": (_I, [_P, _P, _P, _L, _I, _P]),
     "pcfm_rows_colsum_workspace_bytes": (_Z, [_I, _L, _I]),

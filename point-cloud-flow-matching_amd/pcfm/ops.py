@@ -402,6 +402,40 @@ def rows_dot(a: torch.Tensor, b, scale: float = 1.0) -> torch.Tensor:
     return out
 
 
+def se_mlp_ok(m: torch.Tensor, w1: torch.Tensor) -> bool:
+    b, c = m.shape
+    return b * (c + w1.shape[0]) <= 16384
+
+
+def se_mlp_forward(m: torch.Tensor, w1: torch.Tensor, w2: torch.Tensor):
+    """SE3d's MLP (se.py:9-19): (s = sigmoid(W2 relu(W1 m)), hid = relu(W1 m))."""
+    for t, n in ((m, "m"), (w1, "w1"), (w2, "w2")):
+        _check(t, n, "f")
+    b, c = m.shape
+    h = w1.shape[0]
+    if w1.shape != (h, c) or w2.shape != (c, h):
+        raise ValueError("se_mlp_forward: weight shapes")
+    hid = torch.empty((b, h), dtype=torch.float32, device=m.device)
+    s = torch.empty((b, c), dtype=torch.float32, device=m.device)
+    _lib.call("pcfm_se_mlp_fwd", _ptr(m), _ptr(w1), _ptr(w2), b, c, h, _ptr(hid), _ptr(s),
+              _stream(m))
+    return s, hid
+
+
+def se_mlp_backward(m, hid, s, ds, w1, w2, dm_scale: float = 1.0):
+    """-> (dm * dm_scale, dW1, dW2) of se_mlp_forward for the output gradient ds."""
+    for t, n in ((m, "m"), (hid, "hid"), (s, "s"), (ds, "ds"), (w1, "w1"), (w2, "w2")):
+        _check(t, n, "f")
+    b, c = m.shape
+    h = w1.shape[0]
+    dm = torch.empty_like(m)
+    dw1 = torch.empty_like(w1)
+    dw2 = torch.empty_like(w2)
+    _lib.call("pcfm_se_mlp_bwd", _ptr(m), _ptr(hid), _ptr(s), _ptr(ds), _ptr(w1), _ptr(w2), b, c,
+              h, float(dm_scale), _ptr(dm), _ptr(dw1), _ptr(dw2), _stream(m))
+    return dm, dw1, dw2
+
+
 def rows_affine_(x: torch.Tensor, s: torch.Tensor, t) -> torch.Tensor:
     """x[r, :] = s[r] * x[r, :] + t[r] in place, x (rows, len) with len % 4 == 0."""
     _check(x, "x", "f")

@@ -34,6 +34,30 @@ def test_rows_dot_and_affine(ops):
     assert torch.allclose(x, s[:, None] * a + t[:, None], atol=1e-6, rtol=1e-6)
 
 
+@pytest.mark.parametrize("b,c,h", [(8, 256, 32), (8, 128, 16), (3, 64, 8), (1, 7, 3)])
+def test_se_mlp_kernels_match_torch(ops, b, c, h):
+    """pcfm_se_mlp_fwd / _bwd (SE3d's MLP, se.py:9-19, one launch each way)
+    against torch autograd over sigmoid(W2 relu(W1 m)) in fp32: outputs and all
+    three gradients (dm with the pooling's 1/V folded in) to fp32 round-off."""
+    g = torch.Generator(device="cuda").manual_seed(c)
+    m = torch.randn(b, c, device="cuda", generator=g)
+    w1 = torch.randn(h, c, device="cuda", generator=g) * c ** -0.5
+    w2 = torch.randn(c, h, device="cuda", generator=g) * h ** -0.5
+    ds = torch.randn(b, c, device="cuda", generator=g)
+    assert ops.se_mlp_ok(m, w1)
+    s, hid = ops.se_mlp_forward(m, w1, w2)
+    dm, dw1, dw2 = ops.se_mlp_backward(m, hid, s, ds, w1, w2, 0.25)
+    mr, w1r, w2r = (t.clone().requires_grad_(True) for t in (m, w1, w2))
+    sr = torch.sigmoid(torch.relu(mr @ w1r.t()) @ w2r.t())
+    sr.backward(ds)
+    torch.testing.assert_close(s, sr.detach(), rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(hid, torch.relu(m @ w1.t()), rtol=1e-5, atol=1e-6)
+    for a, r_ in ((dm, 0.25 * mr.grad), (dw1, w1r.grad), (dw2, w2r.grad)):
+        torch.testing.assert_close(a, r_, rtol=1e-5, atol=1e-6 * max(1.0, r_.abs().max().item()))
+    s2, _ = ops.se_mlp_forward(m, w1, w2)
+    assert torch.equal(s, s2)  # deterministic
+
+
 @pytest.mark.parametrize("cin,cout,r,n", [(64, 128, 8, 3000), (128, 128, 16, 5000)])
 def test_pvconv_se_devox_fused_matches_modules(ops, monkeypatch, cin, cout, r, n):
     import modules.pvconv as pv
