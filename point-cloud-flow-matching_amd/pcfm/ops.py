@@ -404,7 +404,8 @@ def rows_dot(a: torch.Tensor, b, scale: float = 1.0) -> torch.Tensor:
 
 def se_mlp_ok(m: torch.Tensor, w1: torch.Tensor) -> bool:
     b, c = m.shape
-    return b * (c + w1.shape[0]) <= 16384
+    h = w1.shape[0]
+    return (b + h) * c + b * h <= 24576
 
 
 def se_mlp_forward(m: torch.Tensor, w1: torch.Tensor, w2: torch.Tensor):
