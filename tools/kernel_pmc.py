@@ -8,8 +8,9 @@ north_star's "MFMA-busy counters against gfx950 peak" and SURVEY.md 8d
     python tools/kernel_pmc.py summarize OUT/<pass> ... > profiles/rNN_kernel_pmc.json
 
 Workload (B = 8, N = 20000 where it applies -- the C2 train step's shapes):
-  conv3d fwd / bwd-data / wgrad at C128 R32 and C256 R16 (split operands, as the
-  step runs them), Chamfer forward at C2 (8 x 20000 x 20000), ball query at C5
+  conv3d fwd / bwd-data / wgrad at C128 R32, C256 R16 and C256 R8 (split
+  operands, as the step runs them), the devoxelization forward, the pointwise
+  GEMMs, the EMD forward, Chamfer forward at C2 (8 x 20000 x 20000), ball query at C5
   (4 x 100000 points, 4096 centers, U = 32).
 Derived per kernel: MFMA-pipe busy fraction = SQ_VALU_MFMA_BUSY_CYCLES / (1024
 SIMDs x GRBM_GUI_ACTIVE / 8) (GRBM_GUI_ACTIVE is summed over the 8 XCDs;
@@ -36,7 +37,7 @@ def run():
     from pcfm import ops
     g = torch.Generator(device="cuda").manual_seed(0)
     b = 8
-    for c, r in ((128, 32), (256, 16)):
+    for c, r in ((128, 32), (256, 16), (256, 8)):
         x = torch.randn(b, c, r, r, r, device="cuda", generator=g)
         w = torch.randn(c, c, 3, 3, 3, device="cuda", generator=g) * (1.0 / (27 * c) ** 0.5)
         xs, gys = ops.conv3d_split(x), ops.conv3d_split(x * 0.5)
@@ -54,6 +55,20 @@ def run():
         for _ in range(K):
             ops.trilinear_devoxelize_scale_add(r, True, x, grid, sc, pf)
         torch.cuda.synchronize()
+    for ci, co in ((256, 256), (128, 256)):  # SharedMLP 1x1 convs, fwd / bwd-data / wgrad
+        x = torch.randn(b, ci, 20000, device="cuda", generator=g)
+        w = torch.randn(co, ci, 1, device="cuda", generator=g) * ci ** -0.5
+        dy = torch.randn(b, co, 20000, device="cuda", generator=g)
+        for _ in range(K):
+            ops.pointwise_forward(x, w, None)
+            ops.pointwise_backward_data(dy, w)
+            ops.pointwise_backward_weight(x, dy)
+        torch.cuda.synchronize()
+    e1 = torch.rand(8, 2048, 3, device="cuda", generator=g)
+    e2 = torch.rand(8, 2048, 3, device="cuda", generator=g)
+    for _ in range(K):  # EMD forward at the bench size (exp-bound VALU)
+        ops.approxmatch_cost_forward(e1, e2)
+    torch.cuda.synchronize()
     a = torch.randn(8, 20000, 3, device="cuda", generator=g)
     p = torch.randn(8, 20000, 3, device="cuda", generator=g)
     d1, d2 = torch.empty(8, 20000, device="cuda"), torch.empty(8, 20000, device="cuda")
@@ -99,8 +114,10 @@ def summarize(dirs):
         if "SQ_LDS_BANK_CONFLICT" in avg and avg.get("SQ_LDS_IDX_ACTIVE"):
             entry["lds_conflict_frac"] = avg["SQ_LDS_BANK_CONFLICT"] / avg["SQ_LDS_IDX_ACTIVE"]
         out[short] = entry
-    return {"workload": "tools/kernel_pmc.py run (conv3d C128R32/C256R16 B=8 split operands; "
-                        "Chamfer fwd 8x20000x20000; ball query 4x100000, M=4096, U=32)",
+    return {"workload": "tools/kernel_pmc.py run (conv3d C128R32/C256R16/C256R8 B=8 split "
+                        "operands; devox fwd C128R32/C256R16; pointwise 256->256 / 128->256 at "
+                        "B=8 N=20000; EMD fwd B=8 N=2048; Chamfer fwd 8x20000x20000; ball query "
+                        "4x100000, M=4096, U=32)",
             "derivation": "mfma_busy_frac = SQ_VALU_MFMA_BUSY_CYCLES / (1024 * GRBM_GUI_ACTIVE / 8)",
             "kernels": out}
 
