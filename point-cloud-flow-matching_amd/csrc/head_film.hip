@@ -36,6 +36,15 @@
 namespace pcfm {
 namespace {
 
+// waves-per-SIMD bound of the FiLM backward (measurement knob; 0: none)
+#ifndef PCFM_FILM_BWD_WPE
+#define PCFM_FILM_BWD_WPE 0
+#endif
+#if PCFM_FILM_BWD_WPE > 0
+#define FILM_BWD_ATTR __attribute__((amdgpu_waves_per_eu(PCFM_FILM_BWD_WPE)))
+#else
+#define FILM_BWD_ATTR
+#endif
 constexpr int kRowsPerBlock = 256;  // 4 waves x 64 rows, one batch element
 constexpr int kSums = 5;            // d sp1, d shift, d gamma, d beta, d bias_prev
 
@@ -197,7 +206,7 @@ __global__ void __launch_bounds__(256)
 
 // grid = (chunks = ceil(n / 256), B), 256 threads.  part[B * chunks][5][W].
 template <int NV, bool FILM>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256) FILM_BWD_ATTR
     film_bwd_kernel(const float* __restrict__ dhn, const uint16_t* __restrict__ da16,
                     const float* __restrict__ u, const uint16_t* __restrict__ h16,
                     const float* __restrict__ uprev, const uint16_t* __restrict__ gprev,
