@@ -115,7 +115,7 @@ int pcfm_debug_devox_verify(const float* coords, const float* feat, const float*
 /* SE3d's channel MLP (modules/se.py over pvconv.py:35-39; se.py:9-19):
  *   hid [b][h] = relu(m [b][c] . W1^T), W1 [h][c];  s [b][c] = sigmoid(hid . W2^T), W2 [c][h]
  * and its backward from ds [b][c]: dm [b][c] (times dm_scale), dW1 [h][c], dW2 [c][h].
- * One single-block launch each; (b + h) * c + b * h <= 24576 (else PCFM_EINVAL). */
+ * One single-block launch each; 2 (b + h) c + 2 b h <= 32768 (else PCFM_EINVAL). */
 int pcfm_se_mlp_fwd(const float* m, const float* w1, const float* w2, int b, int c, int h,
                     float* hid, float* s, void* stream);
 int pcfm_se_mlp_bwd(const float* m, const float* hid, const float* s, const float* ds,

@@ -354,11 +354,11 @@ extern "C" int pcfm_trilinear_devoxelize_bwd_planned(const float* grad_y, const 
 // ops were ~12 launches of a few microseconds per PVConv.  Fixed summation
 // order (deterministic); fp32 like the module.
 // ---------------------------------------------------------------------------
-// Long reductions (over c) are one 16-lane group per output with the lanes
-// splitting c (a fixed xor tree); short ones (over h or b) one thread per
-// output.  W2 is staged transposed in LDS (w2t [h][c]) so that both its uses
-// read consecutive channels across lanes.
-// 16-lane groups: four outputs per wave at a time
+// Every operand is staged in LDS first (coalesced loads by the whole block;
+// read straight from global memory, the dependent loads of the reduction loops
+// took 17-20 us per launch); W2 transposed (w2t [h][c]).  Long reductions
+// (over c) are one 16-lane group per output with the lanes splitting c (a fixed
+// xor tree); short ones (over h or b) one thread per output.
 __device__ __forceinline__ float se_group_sum(float v) {
 #pragma unroll
   for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -369,20 +369,24 @@ __global__ void __launch_bounds__(1024)
     se_mlp_fwd_kernel(const float* __restrict__ m, const float* __restrict__ w1,
                       const float* __restrict__ w2, int b, int c, int h, float* __restrict__ hid,
                       float* __restrict__ s) {
-  extern __shared__ float sh[];  // hid [b][h], w2t [h][c]
-  float* hs = sh;
-  float* w2t = sh + b * h;
+  extern __shared__ float sh[];  // m [b][c], w1 [h][c], w2t [h][c], hid [b][h]
+  float* ms = sh;
+  float* w1s = ms + b * c;
+  float* w2t = w1s + h * c;
+  float* hs = w2t + h * c;
   const int l16 = threadIdx.x & 15, grp = threadIdx.x >> 4, ng = blockDim.x >> 4;
-  for (int e = threadIdx.x; e < c * h; e += blockDim.x) {
+  for (int e = threadIdx.x; e < b * c; e += blockDim.x) ms[e] = m[e];
+  for (int e = threadIdx.x; e < h * c; e += blockDim.x) {
+    w1s[e] = w1[e];
     const int k = e / h, j = e - k * h;
     w2t[j * c + k] = w2[e];
   }
+  __syncthreads();
   for (int e0 = 0; e0 < b * h; e0 += ng) {  // hid = relu(m . W1^T): 16 lanes over c
     const int e = e0 + grp, ec = min(e, b * h - 1);
     const int bi = ec / h, j = ec - bi * h;
     float acc = 0.0f;
-    for (int k = l16; k < c; k += 16)
-      acc = __builtin_fmaf(m[(size_t)bi * c + k], w1[(size_t)j * c + k], acc);
+    for (int k = l16; k < c; k += 16) acc = __builtin_fmaf(ms[bi * c + k], w1s[j * c + k], acc);
     const float v = fmaxf(se_group_sum(acc), 0.0f);
     if (l16 == 0 && e < b * h) {
       hs[e] = v;
@@ -405,24 +409,31 @@ __global__ void __launch_bounds__(1024)
                       const float* __restrict__ w1, const float* __restrict__ w2, int b, int c,
                       int h, float dm_scale, float* __restrict__ dm, float* __restrict__ dw1,
                       float* __restrict__ dw2) {
-  extern __shared__ float sh[];  // dz2 [b][c], dz1 [b][h], w2t [h][c]
+  // dz2 [b][c], m [b][c], w1 [h][c], w2t [h][c], hid [b][h], dz1 [b][h]
+  extern __shared__ float sh[];
   float* dz2 = sh;
-  float* dz1 = sh + b * c;
-  float* w2t = dz1 + b * h;
+  float* ms = dz2 + b * c;
+  float* w1s = ms + b * c;
+  float* w2t = w1s + h * c;
+  float* hs = w2t + h * c;
+  float* dz1 = hs + b * h;
   const int l16 = threadIdx.x & 15, grp = threadIdx.x >> 4, ng = blockDim.x >> 4;
   for (int e = threadIdx.x; e < b * c; e += blockDim.x) {
     const float sv = s[e];
     dz2[e] = ds[e] * (1.0f - sv) * sv;  // torch's sigmoid backward expression
+    ms[e] = m[e];
   }
-  for (int e = threadIdx.x; e < c * h; e += blockDim.x) {
+  for (int e = threadIdx.x; e < h * c; e += blockDim.x) {
+    w1s[e] = w1[e];
     const int k = e / h, j = e - k * h;
     w2t[j * c + k] = w2[e];
   }
+  for (int e = threadIdx.x; e < b * h; e += blockDim.x) hs[e] = hid[e];
   __syncthreads();
   for (int e = threadIdx.x; e < c * h; e += blockDim.x) {  // dW2 [c][h]: over b
     const int k = e / h, j = e - k * h;
     float acc = 0.0f;
-    for (int bi = 0; bi < b; ++bi) acc = __builtin_fmaf(dz2[bi * c + k], hid[bi * h + j], acc);
+    for (int bi = 0; bi < b; ++bi) acc = __builtin_fmaf(dz2[bi * c + k], hs[bi * h + j], acc);
     dw2[e] = acc;
   }
   for (int e0 = 0; e0 < b * h; e0 += ng) {  // dh = dz2 . W2, relu backward: 16 lanes over c
@@ -431,31 +442,31 @@ __global__ void __launch_bounds__(1024)
     float acc = 0.0f;
     for (int k = l16; k < c; k += 16) acc = __builtin_fmaf(dz2[bi * c + k], w2t[j * c + k], acc);
     acc = se_group_sum(acc);
-    if (l16 == 0 && e < b * h) dz1[e] = hid[e] > 0.0f ? acc : 0.0f;
+    if (l16 == 0 && e < b * h) dz1[e] = hs[e] > 0.0f ? acc : 0.0f;
   }
   __syncthreads();
   for (int e = threadIdx.x; e < h * c; e += blockDim.x) {  // dW1 [h][c]: over b
     const int j = e / c, k = e - j * c;
     float acc = 0.0f;
-    for (int bi = 0; bi < b; ++bi) acc = __builtin_fmaf(dz1[bi * h + j], m[(size_t)bi * c + k], acc);
+    for (int bi = 0; bi < b; ++bi) acc = __builtin_fmaf(dz1[bi * h + j], ms[bi * c + k], acc);
     dw1[e] = acc;
   }
   for (int e = threadIdx.x; e < b * c; e += blockDim.x) {  // dm [b][c]: over h
     const int bi = e / c, k = e - bi * c;
     float acc = 0.0f;
-    for (int j = 0; j < h; ++j) acc = __builtin_fmaf(dz1[bi * h + j], w1[(size_t)j * c + k], acc);
+    for (int j = 0; j < h; ++j) acc = __builtin_fmaf(dz1[bi * h + j], w1s[j * c + k], acc);
     dm[e] = acc * dm_scale;
   }
 }
 
-static bool se_mlp_ok(int b, int c, int h) {  // LDS: (b + h) c + b h floats <= 96 KiB
-  return b > 0 && c > 0 && h > 0 && ((long long)b + h) * c + (long long)b * h <= 24576;
+static bool se_mlp_ok(int b, int c, int h) {  // LDS: 2 (b + h) c + 2 b h floats <= 128 KiB
+  return b > 0 && c > 0 && h > 0 && 2 * ((long long)b + h) * c + 2LL * b * h <= 32768;
 }
 
 extern "C" int pcfm_se_mlp_fwd(const float* m, const float* w1, const float* w2, int b, int c,
                                int h, float* hid, float* s, void* stream) {
   PCFM_CHECK_ARG(se_mlp_ok(b, c, h), "se_mlp_fwd: unsupported size b=%d c=%d h=%d", b, c, h);
-  const size_t lds = ((size_t)b * h + (size_t)h * c) * sizeof(float);
+  const size_t lds = ((size_t)b * c + 2 * (size_t)h * c + (size_t)b * h) * sizeof(float);
   int e = allow_big_lds((const void*)se_mlp_fwd_kernel);
   if (e) return e;
   hipLaunchKernelGGL(se_mlp_fwd_kernel, dim3(1), dim3(1024), lds, (hipStream_t)stream, m, w1, w2,
@@ -467,7 +478,7 @@ extern "C" int pcfm_se_mlp_bwd(const float* m, const float* hid, const float* s,
                                const float* w1, const float* w2, int b, int c, int h,
                                float dm_scale, float* dm, float* dw1, float* dw2, void* stream) {
   PCFM_CHECK_ARG(se_mlp_ok(b, c, h), "se_mlp_bwd: unsupported size b=%d c=%d h=%d", b, c, h);
-  const size_t lds = ((size_t)b * c + (size_t)b * h + (size_t)h * c) * sizeof(float);
+  const size_t lds = (2 * (size_t)b * c + 2 * (size_t)h * c + 2 * (size_t)b * h) * sizeof(float);
   int e = allow_big_lds((const void*)se_mlp_bwd_kernel);
   if (e) return e;
   hipLaunchKernelGGL(se_mlp_bwd_kernel, dim3(1), dim3(1024), lds, (hipStream_t)stream, m, hid, s,

@@ -405,7 +405,7 @@ def rows_dot(a: torch.Tensor, b, scale: float = 1.0) -> torch.Tensor:
 def se_mlp_ok(m: torch.Tensor, w1: torch.Tensor) -> bool:
     b, c = m.shape
     h = w1.shape[0]
-    return (b + h) * c + b * h <= 24576
+    return 2 * (b + h) * c + 2 * b * h <= 32768
 
 
 def se_mlp_forward(m: torch.Tensor, w1: torch.Tensor, w2: torch.Tensor):
