@@ -152,16 +152,11 @@ def test_context_net_point_order(monkeypatch, report):
         m = copy.deepcopy(net)
         ctx = m(x, t, cond)
         ctx.backward(gy)
-        res[flag] = (ctx.detach(), {n: p.grad.clone() for n, p in m.named_parameters()
-                                    if p.grad is not None})
+        res[flag] = (ctx.detach(), [p.grad.clone() for p in m.parameters() if p.grad is not None])
     (a, ga), (b, gb) = res[True], res[False]
     rel = ((a - b).abs().max() / b.abs().max()).item()
-    # per-parameter relative norm; the biases of convs feeding a training-mode
-    # BatchNorm have an analytically zero gradient (rounding noise on both sides)
-    gdev = {n: ((ga[n] - gb[n]).norm() / gb[n].norm().clamp_min(1e-30)).item()
-            for n in gb if not n.endswith(_NOISE_BIAS)}
-    worst = max(gdev, key=gdev.get)
-    report("context_net_point_order", {"ctx_rel": rel, "grad_rel_max": gdev[worst],
-                                       "worst": worst})
-    assert rel < 1e-4, rel  # fp32 sums reordered through ~20 normalised layers
-    assert gdev[worst] < 1e-3, (worst, gdev[worst])
+    grel = max(((u - v).abs().max() / v.abs().max().clamp_min(1e-30)).item()
+               for u, v in zip(ga, gb) if v.abs().max() > 1e-6)
+    report("context_net_point_order", {"ctx_rel": rel, "grad_rel_max": grel})
+    assert rel < 1e-5, rel
+    assert grel < 2e-3, grel  # BN-bias-like cancelling sums, as in the golden tests' bounds
