@@ -53,20 +53,6 @@ def timestep_embedding(t: torch.Tensor, dim: int, max_period: float = 10000.0) -
 _BATCH_FP32 = os.environ.get("PCFM_BATCH_FP32", "1") != "0"
 # ContextNet's PV-block FiLM affines as batched products (A/B knob, dev)
 _FILM_GROUPS = os.environ.get("PCFM_FILM_GROUPS", "1") != "0"
-# ContextNet runs on its points in a spatial order (PCFM_SORT_POINTS=0: input order)
-_SORT_POINTS = os.environ.get("PCFM_SORT_POINTS", "1") != "0"
-
-
-def _spatial_order(xyz: torch.Tensor) -> torch.Tensor:
-    """(B, N, 3) -> (B, N) permutation sorting each cloud by its cell on a 32^3
-    grid over the cloud's bounding box, row-major (x, y, z): the voxel scatters
-    and gathers then see neighbouring points in neighbouring lanes (coherent LDS
-    corner reads) and write the sorted channels-last rows almost in order."""
-    lo = xyz.amin(dim=1, keepdim=True)
-    ext = (xyz.amax(dim=1, keepdim=True) - lo).clamp_min(1e-12)
-    q = ((xyz - lo) * (32.0 / ext)).long().clamp_(0, 31)
-    key = (q[..., 0] * 32 + q[..., 1]) * 32 + q[..., 2]
-    return torch.argsort(key, dim=1, stable=True)
 
 
 def _batch_fp32(ref: torch.Tensor):
@@ -561,22 +547,6 @@ class ContextNet(_TimeCondEmbed):
         return pre(torch.cat(scales, dim=1))
 
     def forward(self, x: torch.Tensor, t: torch.Tensor, cond: Optional[torch.Tensor]):
-        """The pyramid is permutation-equivariant over the points (per-point
-        layers, voxel scatter / gather, batch-wide norms and max pooling), so on
-        the GPU it runs on the points in a spatial order and the per-point
-        context is put back in input order: the same result up to fp32 summation
-        order (tests/test_gpu_model.py::test_context_net_point_order)."""
-        b, n, _ = x.shape
-        if not (_SORT_POINTS and x.is_cuda and n > 1):
-            return self._forward(x, t, cond)
-        perm = _spatial_order(x[..., :3].detach())
-        xs = torch.gather(x, 1, perm[..., None].expand_as(x))
-        ctx = self._forward(xs, t, cond)
-        inv = torch.empty_like(perm).scatter_(
-            1, perm, torch.arange(n, device=x.device).expand(b, n).contiguous())
-        return torch.gather(ctx, 1, inv[..., None].expand_as(ctx))
-
-    def _forward(self, x: torch.Tensor, t: torch.Tensor, cond: Optional[torch.Tensor]):
         b, n, d = x.shape
         coords = x[..., :3].permute(0, 2, 1).contiguous()
         emb = self._embed_t(t, x.dtype) + self._c_emb(x, cond)

@@ -128,35 +128,3 @@ def test_train_step_gpu_small():
     for ep in (1, 201):
         out = tr.step(batch, epoch=ep)
         assert math.isfinite(out["loss_point"].item()) and math.isfinite(out["loss_latent"].item())
-
-
-def test_context_net_point_order(monkeypatch, report):
-    """ContextNet on its points in spatial order (the GPU default,
-    pcfm.models._spatial_order) vs input order: the pyramid is
-    permutation-equivariant, so the context and every parameter gradient agree
-    to fp32 summation order (BatchNorm / GroupNorm sums, voxel averages)."""
-    import copy
-    import pcfm.models as M
-    torch.manual_seed(5)
-    net = M.ContextNet(in_point_dim=6, cond_dim=129).to(DEV).train()
-    with torch.no_grad():
-        for p in net.head_out.parameters():  # zero-init: let the context see the pyramid
-            p.normal_(0.0, 0.05)
-    x = torch.rand(2, 4096, 6, device=DEV) * 2 - 1
-    t = torch.rand(2, device=DEV)
-    cond = torch.randn(2, 129, device=DEV)
-    gy = torch.randn(2, 4096, net.ctx_dim, device=DEV)
-    res = {}
-    for flag in (True, False):
-        monkeypatch.setattr(M, "_SORT_POINTS", flag)
-        m = copy.deepcopy(net)
-        ctx = m(x, t, cond)
-        ctx.backward(gy)
-        res[flag] = (ctx.detach(), [p.grad.clone() for p in m.parameters() if p.grad is not None])
-    (a, ga), (b, gb) = res[True], res[False]
-    rel = ((a - b).abs().max() / b.abs().max()).item()
-    grel = max(((u - v).abs().max() / v.abs().max().clamp_min(1e-30)).item()
-               for u, v in zip(ga, gb) if v.abs().max() > 1e-6)
-    report("context_net_point_order", {"ctx_rel": rel, "grad_rel_max": grel})
-    assert rel < 1e-5, rel
-    assert grel < 2e-3, grel  # BN-bias-like cancelling sums, as in the golden tests' bounds
