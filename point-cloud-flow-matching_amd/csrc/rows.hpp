@@ -256,6 +256,80 @@ __global__ void __launch_bounds__(1024)
   }
 }
 
+// The 4-channel form of gather_rows_kernel (cpb == 4, the r = 16 / 8 devox
+// forward and voxelization backward): the four rows are staged interleaved,
+// lds4[v] = (row c0 .. c0+3 at v), so a tap of an item reads its four channels
+// with one ds_read_b128 instead of four ds_read_b32 (the random corner reads
+// are what the gather waits on: LDS bank conflicts were 0.7 of its LDS cycles).
+// Per channel the same products and fma order: bit-identical.
+template <int T>
+__device__ __forceinline__ float4 tap_sum4(const float4* __restrict__ s, const int (&id)[T],
+                                           const float (&w)[T]) {
+  if constexpr (T == 1) {
+    const float4 v = s[id[0]];
+    return make_float4(v.x * w[0], v.y * w[0], v.z * w[0], v.w * w[0]);
+  } else {
+    const float4 v1 = s[id[1]], v0 = s[id[0]];
+    float4 a = make_float4(w[1] * v1.x, w[1] * v1.y, w[1] * v1.z, w[1] * v1.w);
+    a.x = __builtin_fmaf(w[0], v0.x, a.x);
+    a.y = __builtin_fmaf(w[0], v0.y, a.y);
+    a.z = __builtin_fmaf(w[0], v0.z, a.z);
+    a.w = __builtin_fmaf(w[0], v0.w, a.w);
+#pragma unroll
+    for (int k = 2; k < T; ++k) {
+      const float4 v = s[id[k]];
+      a.x = __builtin_fmaf(w[k], v.x, a.x);
+      a.y = __builtin_fmaf(w[k], v.y, a.y);
+      a.z = __builtin_fmaf(w[k], v.z, a.z);
+      a.w = __builtin_fmaf(w[k], v.w, a.w);
+    }
+    return a;
+  }
+}
+
+// grid = (item splits, C / 4, b); C % 4 == 0.
+template <class Prov>
+__global__ void __launch_bounds__(512)
+    gather_rows4_kernel(const float* __restrict__ rows, float* __restrict__ out, int C, int V,
+                        int NI, Prov prov, GatherEpi epi) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float4* lds4 = reinterpret_cast<float4*>(lds);
+  constexpr int T = Prov::TAPS;
+  const int b = blockIdx.z;
+  const int c0 = blockIdx.y * 4;
+  const float* __restrict__ rb = rows + ((size_t)b * C + c0) * V;
+  for (int v = threadIdx.x; v < V; v += blockDim.x)
+    lds4[v] = make_float4(rb[v], rb[(size_t)V + v], rb[2 * (size_t)V + v], rb[3 * (size_t)V + v]);
+  __syncthreads();
+  float* __restrict__ ob = out + ((size_t)b * C + c0) * NI;
+  const float* __restrict__ ab = epi.add != nullptr ? epi.add + ((size_t)b * C + c0) * NI : nullptr;
+  float sc[4] = {1.0f, 1.0f, 1.0f, 1.0f};
+  if (epi.scale != nullptr) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) sc[k] = epi.scale[(size_t)b * C + c0 + k];
+  }
+  const bool primary = blockIdx.y == 0;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < NI; i += gridDim.x * blockDim.x) {
+    float ad[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    if (ab != nullptr) {  // issued before the taps: their latency overlaps the index math
+#pragma unroll
+      for (int k = 0; k < 4; ++k) ad[k] = nt_ld(ab + (size_t)k * NI + i);
+    }
+    int id[T];
+    float w[T];
+    prov.get(b, i, primary, id, w);
+    const float4 a = tap_sum4<T>(lds4, id, w);
+    const float r[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float acc = r[k];
+      if (epi.scale != nullptr) acc *= sc[k];
+      if (ab != nullptr) acc += ad[k];
+      ob[(size_t)k * NI + i] = acc;
+    }
+  }
+}
+
 // grid = (cell chunks * item splits, channel groups, b).  The block's row
 // segments [v0, v0 + vlen) of `cpb` channels accumulate in LDS (ds_add_f32),
 // then go to HBM once: plain stores when the block owns the whole item range
@@ -339,6 +413,15 @@ inline long long gather_target_blocks() {
   return t;
 }
 
+// PCFM_GATHER4=0: the per-channel form for cpb == 4 too (A/B knob)
+inline bool gather4_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("PCFM_GATHER4");
+    return !(e != nullptr && e[0] == '0');
+  }();
+  return on;
+}
+
 inline RowPlan plan_gather(int B, int C, int V, int NI) {
   RowPlan p;
   const long long target = gather_target_blocks();
@@ -414,7 +497,12 @@ inline int launch_gather(const float* rows, float* out, int B, int C, int V, int
   }
   RowPlan p = plan_gather(B, C, V, NI);
   dim3 grid(p.psplit, p.groups, B);
-  if (p.use_lds) {
+  if (p.use_lds && p.cpb == 4 && C % 4 == 0 && p.threads == 512 && gather4_enabled()) {
+    int e = allow_big_lds((const void*)gather_rows4_kernel<Prov>);
+    if (e) return e;
+    hipLaunchKernelGGL((gather_rows4_kernel<Prov>), grid, dim3(512), p.lds_bytes, st, rows, out, C,
+                       V, NI, prov, epi);
+  } else if (p.use_lds) {
     int e = allow_big_lds((const void*)gather_rows_kernel<Prov, true>);
     if (e) return e;
     hipLaunchKernelGGL((gather_rows_kernel<Prov, true>), grid, dim3(p.threads), p.lds_bytes, st,
