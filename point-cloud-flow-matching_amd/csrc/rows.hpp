@@ -330,60 +330,6 @@ __global__ void __launch_bounds__(512)
   }
 }
 
-// Voxelization backward with the 1/cnt weight folded into the staging:
-// lds[v] = row[v] * (float)(1.0 / (double)cnt[v]) -- the product ProvVoxBwd's
-// tap forms per item, formed once per voxel from a coalesced cnt read -- so an
-// item reads one staged value: no random cnt gather and no fp64 reciprocal per
-// item and channel group (each item was visited by every channel group's
-// block).  Bit-identical to gather_rows_kernel<ProvVoxBwd>.  CPB = 1 (r = 32,
-// 1024 threads) or 4 (rows interleaved as in gather_rows4_kernel, 512 threads).
-// grid = (item splits, C / CPB, b).
-template <int CPB>
-__global__ void __launch_bounds__(CPB == 4 ? 512 : 1024)
-    vox_bwd_gather_kernel(const float* __restrict__ rows, const int* __restrict__ ind,
-                          const int* __restrict__ cnt, const float* __restrict__ add, int C,
-                          int V, int NI, float* __restrict__ out) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-  const int b = blockIdx.z;
-  const int c0 = blockIdx.y * CPB;
-  const float* __restrict__ rb = rows + ((size_t)b * C + c0) * V;
-  const int* __restrict__ cb = cnt + (size_t)b * V;
-  for (int v = threadIdx.x; v < V; v += blockDim.x) {
-    const int cv = cb[v];
-    const float w = cv > 0 ? (float)(1.0 / (double)cv) : 0.0f;
-    if constexpr (CPB == 4) {
-      reinterpret_cast<float4*>(lds)[v] =
-          make_float4(rb[v] * w, rb[(size_t)V + v] * w, rb[2 * (size_t)V + v] * w,
-                      rb[3 * (size_t)V + v] * w);
-    } else {
-      lds[v] = rb[v] * w;
-    }
-  }
-  __syncthreads();
-  float* __restrict__ ob = out + ((size_t)b * C + c0) * NI;
-  const float* __restrict__ ab = add != nullptr ? add + ((size_t)b * C + c0) * NI : nullptr;
-  const int* __restrict__ ib = ind + (size_t)b * NI;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < NI; i += gridDim.x * blockDim.x) {
-    float ad[CPB];
-#pragma unroll
-    for (int k = 0; k < CPB; ++k) ad[k] = ab != nullptr ? nt_ld(ab + (size_t)k * NI + i) : 0.0f;
-    const int v = ib[i];
-    const bool ok = (unsigned)v < (unsigned)V;
-    float r[CPB];
-    if constexpr (CPB == 4) {
-      const float4 q = ok ? reinterpret_cast<const float4*>(lds)[v] : make_float4(0.f, 0.f, 0.f, 0.f);
-      r[0] = q.x;
-      r[1] = q.y;
-      r[2] = q.z;
-      r[3] = q.w;
-    } else {
-      r[0] = ok ? lds[v] : 0.0f;
-    }
-#pragma unroll
-    for (int k = 0; k < CPB; ++k) ob[(size_t)k * NI + i] = ab != nullptr ? r[k] + ad[k] : r[k];
-  }
-}
-
 // grid = (cell chunks * item splits, channel groups, b).  The block's row
 // segments [v0, v0 + vlen) of `cpb` channels accumulate in LDS (ds_add_f32),
 // then go to HBM once: plain stores when the block owns the whole item range
@@ -564,39 +510,6 @@ inline int launch_gather(const float* rows, float* out, int B, int C, int V, int
   } else {
     hipLaunchKernelGGL((gather_rows_kernel<Prov, false>), grid, dim3(p.threads), 0, st, rows,
                        out, C, V, NI, p.cpb, prov, epi);
-  }
-  return check_launch(what);
-}
-
-// avg_voxelize backward (+ add): vox_bwd_gather_kernel when the rows fit LDS in
-// the 1- or 4-channel form, else the generic gather (PCFM_VOXBWD_STAGED=0: always)
-inline int launch_vox_bwd(const float* rows, const int* ind, const int* cnt, const float* add,
-                          float* out, int B, int C, int V, int NI, hipStream_t st,
-                          const char* what) {
-  if (B == 0 || NI == 0) return PCFM_OK;
-  static const bool staged = [] {
-    const char* e = std::getenv("PCFM_VOXBWD_STAGED");
-    return !(e != nullptr && e[0] == '0');
-  }();
-  const RowPlan p = plan_gather(B, C, V, NI);
-  const bool k4 = p.use_lds && p.cpb == 4 && C % 4 == 0 && p.threads == 512;
-  const bool k1 = p.use_lds && p.cpb == 1 && p.threads == 1024;
-  if (!staged || V == 0 || !(k4 || k1)) {
-    GatherEpi epi;
-    epi.add = add;
-    return launch_gather(rows, out, B, C, V, NI, ProvVoxBwd{ind, cnt, NI, V}, st, what, epi);
-  }
-  const dim3 grid(p.psplit, p.groups, B);
-  if (k4) {
-    int e = allow_big_lds((const void*)vox_bwd_gather_kernel<4>);
-    if (e) return e;
-    hipLaunchKernelGGL(vox_bwd_gather_kernel<4>, grid, dim3(512), p.lds_bytes, st, rows, ind, cnt,
-                       add, C, V, NI, out);
-  } else {
-    int e = allow_big_lds((const void*)vox_bwd_gather_kernel<1>);
-    if (e) return e;
-    hipLaunchKernelGGL(vox_bwd_gather_kernel<1>, grid, dim3(1024), p.lds_bytes, st, rows, ind,
-                       cnt, add, C, V, NI, out);
   }
   return check_launch(what);
 }

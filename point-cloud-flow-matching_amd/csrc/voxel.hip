@@ -190,8 +190,8 @@ extern "C" int pcfm_avg_voxelize_bwd(const float* grad_y, const int* ind, const 
   PCFM_CHECK_ARG(b >= 0 && c >= 0 && n >= 0 && s >= 0,
                  "avg_voxelize_bwd: negative size b=%d c=%d n=%d s=%d", b, c, n, s);
   if (c == 0) return PCFM_OK;
-  return launch_vox_bwd(grad_y, ind, cnt, nullptr, grad_x, b, c, s, n, (hipStream_t)stream,
-                        "avg_voxelize_bwd");
+  return launch_gather(grad_y, grad_x, b, c, s, n, ProvVoxBwd{ind, cnt, n, s},
+                       (hipStream_t)stream, "avg_voxelize_bwd");
 }
 
 // grad_x = avg_voxelize_bwd(grad_y) + add: the voxelization's input gradient
@@ -202,8 +202,10 @@ extern "C" int pcfm_avg_voxelize_bwd_add(const float* grad_y, const int* ind, co
   PCFM_CHECK_ARG(b >= 0 && c >= 0 && n >= 0 && s > 0,
                  "avg_voxelize_bwd_add: bad size b=%d c=%d n=%d s=%d", b, c, n, s);
   if (c == 0) return PCFM_OK;
-  return launch_vox_bwd(grad_y, ind, cnt, add, grad_x, b, c, s, n, (hipStream_t)stream,
-                        "avg_voxelize_bwd_add");
+  GatherEpi epi;
+  epi.add = add;
+  return launch_gather(grad_y, grad_x, b, c, s, n, ProvVoxBwd{ind, cnt, n, s},
+                       (hipStream_t)stream, "avg_voxelize_bwd_add", epi);
 }
 
 extern "C" int pcfm_trilinear_devoxelize_fwd(const float* coords, const float* feat, int b, int c,
