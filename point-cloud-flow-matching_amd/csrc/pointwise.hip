@@ -408,52 +408,38 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
     pw_gemm256ws_kernel(const Parts x, const uint16_t* __restrict__ wh,
                         const uint16_t* __restrict__ wl, const float* __restrict__ bias,
                         int bias_bstride, const Parts y, int K, int M, int N, int Kpad,
-                        int nbatch, float2* __restrict__ stats, int* __restrict__ fault) {
+                        float2* __restrict__ stats, int* __restrict__ fault) {
   constexpr int TM = 256, TN = 128;
   constexpr int A_ELEMS = TM * kLDR, B_ELEMS = TN * kLDR;
   constexpr int STAGE = 2 * A_ELEMS + 2 * B_ELEMS;  // uint16 elements
   static_assert(STAGE * 2 == 61440, "stage bytes (launcher)");
   extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
   __shared__ int full[kWsStages], empty[kWsStages];
+  const int b = blockIdx.z, m0 = blockIdx.y * TM, p0 = blockIdx.x * TN;
   const int t = threadIdx.x, lane = t & 63;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   const int nsteps = Kpad / kKT;
-  // persistent over tiles (point tile fastest, then m tile, then batch element);
-  // the global step gs = k * nsteps + s of the block's k-th tile runs through
-  // the stages and counters without a break at tile boundaries, so the next
-  // tile's loads and fills overlap the previous tile's MFMAs and stores
-  const int ntp = (N + TN - 1) / TN, ntm = (M + TM - 1) / TM, ntiles = ntp * ntm * nbatch;
-  const int mytiles = ntiles > (int)blockIdx.x ? (ntiles - 1 - (int)blockIdx.x) / (int)gridDim.x + 1 : 0;
-  const int G = mytiles * nsteps;
-  auto tile_of = [&](int gs, int& b, int& m0, int& p0) {
-    const int tl = (int)blockIdx.x + (gs / nsteps) * (int)gridDim.x;
-    p0 = (tl % ntp) * TN;
-    m0 = ((tl / ntp) % ntm) * TM;
-    b = tl / (ntp * ntm);
-  };
   if (t < kWsStages) {
     full[t] = 0;
     empty[t] = 0;
   }
-  __syncthreads();  // the only block barrier
+  __syncthreads();  // the only block barrier before the epilogue
 
   if (w >= 4) {
     // ---------------- producers: 256 threads ----------------
     const int pt_ = t - 256;
     const int sp = pt_ % TN, ch = __builtin_amdgcn_readfirstlane((pt_ / TN) * 16);  // 0 / 16
+    const int pt = p0 + sp;
+    const bool pok = pt < N;
+    const int voff = (pok ? pt : N - 1) * 4;
     const int arow = pt_;  // one weight row (32 channels hi | lo) per thread
     const __amdgpu_buffer_rsrc_t rwh = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint16_t*>(wh), (short)0, 0x7FFFFFF0, 0x00020000);
     const __amdgpu_buffer_rsrc_t rwl = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<uint16_t*>(wl), (short)0, 0x7FFFFFF0, 0x00020000);
-    const int gl = G > 0 ? G - 1 : 0;
-    auto load_b = [&](int gs, float (&v)[16]) {
-      gs = min(gs, gl);  // past the end: re-read the last step (never filled)
-      int b, m0, p0;
-      tile_of(gs, b, m0, p0);
-      const int pt = p0 + sp;
-      const int voff = (pt < N ? pt : N - 1) * 4;
-      const int c0 = (gs % nsteps) * kKT;
+    const int aoff = (m0 + arow) * Kpad * 2;
+    auto load_b = [&](int s, float (&v)[16]) {
+      const int c0 = s * kKT;
       const int cb = __builtin_amdgcn_readfirstlane(min(c0 + ch, K - 1));
       const float* xr = x.row(b, cb, N);
       const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
@@ -465,12 +451,9 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
             float, __builtin_amdgcn_raw_buffer_load_b32(rs, voff, (c < K ? c - cb : 0) * N * 4, 0));
       }
     };
-    auto load_a = [&](int gs, uint4 (&ra)[8]) {
-      gs = min(gs, gl);
-      int b, m0, p0;
-      tile_of(gs, b, m0, p0);
-      const int aoff = (m0 + arow) * Kpad * 2;
-      const int so = (gs % nsteps) * kKT * 2;
+    uint4 ra[8];
+    auto load_a = [&](int s) {
+      const int so = s * kKT * 2;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         ra[q] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rwh, aoff, so + 16 * q, 0));
@@ -478,12 +461,8 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
             __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rwl, aoff, so + 16 * q, 0));
       }
     };
-    auto fill = [&](int gs, float (&v)[16], const uint4 (&ra)[8]) {  // -> stage gs % 2
-      int b, m0, p0;
-      tile_of(gs, b, m0, p0);
-      const bool pok = p0 + sp < N;
-      const int s = gs % nsteps;
-      uint16_t* st = lds + (size_t)(gs % kWsStages) * STAGE;
+    auto fill = [&](int s, float (&v)[16]) {  // step s -> stage s % 2
+      uint16_t* st = lds + (size_t)(s % kWsStages) * STAGE;
       uint16_t* dh = st + arow * kLDR;
       uint16_t* dl = st + A_ELEMS + arow * kLDR;
 #pragma unroll
@@ -497,31 +476,26 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
       store_split<16>(v, bh, bh + B_ELEMS);
     };
     float x0[16], x1[16], x2[16];
-    uint4 a0[8], a1[8];
+    const int last = nsteps - 1;
     load_b(0, x0);
-    load_b(1, x1);
-    load_b(2, x2);
-    load_a(0, a0);
-    load_a(1, a1);
+    load_b(min(1, last), x1);
+    load_b(min(2, last), x2);
+    load_a(0);
     bool ok = true;
-    // step gs uses x0 / a0; x1, x2 hold gs+1, gs+2 and a1 gs+1; then rotate and
-    // refill x2 with gs+3, a1 with gs+2
-    for (int gs = 0; gs < G; ++gs) {
-      const int stage = gs % kWsStages;
-      if (gs >= kWsStages) ok = ok && ws_wait(&empty[stage], 4 * (gs / kWsStages));
-      fill(gs, x0, a0);
+    // step s uses x0; x1, x2 hold s+1, s+2; x0 is refilled with s+3 (rotated)
+    for (int s = 0; s < nsteps; ++s) {
+      const int stage = s % kWsStages;
+      if (s >= kWsStages) ok = ok && ws_wait(&empty[stage], 4 * (s / kWsStages));
+      fill(s, x0);
       __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's stage writes done
-      if (lane == 0)
-        __hip_atomic_fetch_add(&full[stage], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (lane == 0) __hip_atomic_fetch_add(&full[stage], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (s + 1 < nsteps) load_a(s + 1);
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         x0[q] = x1[q];
         x1[q] = x2[q];
       }
-#pragma unroll
-      for (int q = 0; q < 8; ++q) a0[q] = a1[q];
-      load_a(gs + 2, a1);
-      load_b(gs + 3, x2);
+      load_b(min(s + 3, last), x2);
     }
     if (!ok && lane == 0) atomicAdd(fault, 1);
     return;
@@ -530,18 +504,16 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
   // ---------------- consumers: waves 0..3, rows 64 w .. 64 w + 63 ----------------
   const int r = lane & 31, h = lane >> 5;
   f32x16 acc[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
   bool ok = true;
-  for (int gs = 0; gs < G; ++gs) {
-    const int stage = gs % kWsStages, s = gs % nsteps;
-    if (s == 0) {
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-          for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
-    }
-    ok = ok && ws_wait(&full[stage], 4 * (gs / kWsStages + 1));
+  for (int s = 0; s < nsteps; ++s) {
+    const int stage = s % kWsStages;
+    ok = ok && ws_wait(&full[stage], 4 * (s / kWsStages + 1));
     const uint16_t* st = lds + (size_t)stage * STAGE;
 #pragma unroll
     for (int kk = 0; kk < kKT / 16; ++kk) {
@@ -567,67 +539,62 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2))
       }
     }
     __builtin_amdgcn_s_waitcnt(0xC07F);  // this wave's reads of the stage are done
-    if (lane == 0)
-      __hip_atomic_fetch_add(&empty[stage], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    if (s != nsteps - 1) continue;
-    // ---- epilogue of the tile (the producers already fill the next tile's stages)
-    int b, m0, p0;
-    tile_of(gs, b, m0, p0);
-    const int bo = b * bias_bstride;
+    if (lane == 0) __hip_atomic_fetch_add(&empty[stage], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+  if (!ok && lane == 0) atomicAdd(fault, 1);
+  const int bo = b * bias_bstride;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int mg = m0 + w * 64 + i * 32;
-      float* __restrict__ yr = y.row(b, min(mg, M - 1), N);
-      float bv[16];
-      load_bias16(bias != nullptr ? bias + bo : nullptr, mg, h, M, bv);
+  for (int i = 0; i < 2; ++i) {
+    const int mg = m0 + w * 64 + i * 32;
+    float* __restrict__ yr = y.row(b, min(mg, M - 1), N);
+    float bv[16];
+    load_bias16(bias != nullptr ? bias + bo : nullptr, mg, h, M, bv);
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int dm = (e & 3) + 8 * (e >> 2) + 4 * h;
+        const int m = mg + dm;
+        const int p = p0 + j * 32 + r;
+        if (m < M && p < N) out_store(yr + (size_t)dm * N + p, acc[i][j][e] + bv[e]);
+      }
+    if (stats != nullptr) {
+#pragma unroll
+      for (int g = 0; g < 2; ++g) {  // 64-point groups: point tiles 2 g, 2 g + 1
+        const int pw0 = p0 + 64 * g;
+        if (pw0 >= N) continue;
+        const int nv = min(64, N - pw0);
+        const int ngroups = (N + 63) / 64, P = (int)gridDim.z * ngroups;
+        const bool ok0 = pw0 + r < N, ok1 = pw0 + 32 + r < N;
+        float v[32], sr = 0.0f;
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
-          const int dm = (e & 3) + 8 * (e >> 2) + 4 * h;
-          const int m = mg + dm;
-          const int p = p0 + j * 32 + r;
-          if (m < M && p < N) out_store(yr + (size_t)dm * N + p, acc[i][j][e] + bv[e]);
+          const float v0 = acc[i][2 * g][e] + bv[e], v1 = acc[i][2 * g + 1][e] + bv[e];
+          const float s0 = __builtin_bit_cast(
+              float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v0), 0));
+          const float s1 = __builtin_bit_cast(
+              float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v0), 32));
+          const float shv = h ? s1 : s0;
+          sr = r == e ? shv : sr;
+          const float d0 = ok0 ? v0 - shv : 0.0f, d1 = ok1 ? v1 - shv : 0.0f;
+          v[e] = d0 + d1;
+          v[16 + e] = __builtin_fmaf(d1, d1, d0 * d0);
         }
-      if (stats != nullptr) {
-#pragma unroll
-        for (int g = 0; g < 2; ++g) {  // 64-point groups: point tiles 2 g, 2 g + 1
-          const int pw0 = p0 + 64 * g;
-          if (pw0 >= N) continue;
-          const int nv = min(64, N - pw0);
-          const int ngroups = (N + 63) / 64, P = nbatch * ngroups;
-          const bool ok0 = pw0 + r < N, ok1 = pw0 + 32 + r < N;
-          float v[32], sr = 0.0f;
-#pragma unroll
-          for (int e = 0; e < 16; ++e) {
-            const float v0 = acc[i][2 * g][e] + bv[e], v1 = acc[i][2 * g + 1][e] + bv[e];
-            const float s0 = __builtin_bit_cast(
-                float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v0), 0));
-            const float s1 = __builtin_bit_cast(
-                float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v0), 32));
-            const float shv = h ? s1 : s0;
-            sr = r == e ? shv : sr;
-            const float d0 = ok0 ? v0 - shv : 0.0f, d1 = ok1 ? v1 - shv : 0.0f;
-            v[e] = d0 + d1;
-            v[16 + e] = __builtin_fmaf(d1, d1, d0 * d0);
-          }
-          xpose_reduce_stage<32, 16>(v, r & 16);
-          xpose_reduce_stage<16, 8>(v, r & 8);
-          xpose_reduce_stage<8, 4>(v, r & 4);
-          xpose_reduce_stage<4, 2>(v, r & 2);
-          xpose_reduce_stage<2, 1>(v, r & 1);
-          const float q = swz_xor<16>(v[0]);
-          const int m = mg + (r & 3) + 8 * ((r >> 2) & 3) + 4 * h;
-          if (r < 16 && m < M) {
-            const float a = v[0], mu_s = a / (float)nv;
-            stats[(size_t)m * P + b * ngroups + pw0 / 64] =
-                make_float2(sr + mu_s, fmaxf(__builtin_fmaf(-a, mu_s, q), 0.0f));
-          }
+        xpose_reduce_stage<32, 16>(v, r & 16);
+        xpose_reduce_stage<16, 8>(v, r & 8);
+        xpose_reduce_stage<8, 4>(v, r & 4);
+        xpose_reduce_stage<4, 2>(v, r & 2);
+        xpose_reduce_stage<2, 1>(v, r & 1);
+        const float q = swz_xor<16>(v[0]);
+        const int m = mg + (r & 3) + 8 * ((r >> 2) & 3) + 4 * h;
+        if (r < 16 && m < M) {
+          const float a = v[0], mu_s = a / (float)nv;
+          stats[(size_t)m * P + b * ngroups + pw0 / 64] =
+              make_float2(sr + mu_s, fmaxf(__builtin_fmaf(-a, mu_s, q), 0.0f));
         }
       }
     }
   }
-  if (!ok && lane == 0) atomicAdd(fault, 1);
 }
 
 // Streaming form for M <= 128, K <= 256, both multiples of 32 (SharedMLP 128 -> 128 layers and
@@ -1273,11 +1240,8 @@ static int pw_gemm_launch(const Parts& x, const void* wsplit, const float* bias,
         set_error("pointwise_gemm: fault counter");
         return PCFM_EINVAL;
       }
-      // persistent: one block per CU (120 KiB of LDS), tiles dealt round-robin
-      const int ntiles = (int)(g256.x * g256.y * g256.z);
-      hipLaunchKernelGGL(pw_gemm256ws_kernel, dim3(std::min(ntiles, kCUs)), dim3(512),
-                         (size_t)kWsStages * 61440, st, x, wh, wh + total, bias, bias_bstride, y,
-                         cin, cout, n, Kpad, b, stats, fault);
+      hipLaunchKernelGGL(pw_gemm256ws_kernel, g256, dim3(512), (size_t)kWsStages * 61440, st, x,
+                         wh, wh + total, bias, bias_bstride, y, cin, cout, n, Kpad, stats, fault);
     } else {
       hipLaunchKernelGGL(pw_gemm256_kernel, g256, dim3(512), 0, st, x, wh, wh + total, bias,
                          bias_bstride, y, cin, cout, n, Kpad, stats);
