@@ -122,10 +122,6 @@ int pcfm_se_mlp_bwd(const float* m, const float* hid, const float* s, const floa
                     const float* w1, const float* w2, int b, int c, int h, float dm_scale,
                     float* dm, float* dw1, float* dw2, void* stream);
 
-/* Diagnosis only (not a reference interface): waits of the warp-specialised
- * pointwise GEMM (PCFM_PW_WS=1) that gave up since the library was loaded. */
-int pcfm_debug_pw_ws_faults(void);
-
 /* out[r] = scale * sum_v a[r][v] * b[r][v] (b NULL: plain row sum), rows of
  * `len` floats; deterministic.  (SE3d pooling and its scale gradient.) */
 int pcfm_rows_dot(const float* a, const float* b, long long rows, int len, float scale,

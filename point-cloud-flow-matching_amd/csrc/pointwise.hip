@@ -381,222 +381,6 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))
   }
 }
 
-// Warp-specialised form of pw_gemm256_kernel (same tile, operands, products
-// and K order: bit-identical).  The 8 waves split into 4 consumers, each
-// running a 64 (m) x 128 (point) accumulator over the whole K, and 4
-// producers that hold x three K-steps ahead in registers, split it into
-// bf16 hi / lo, and fill a two-stage LDS ring with it and the weight slice.
-// The two sides meet at per-stage LDS counters instead of block barriers, so
-// the MFMA stream of a consumer never waits for another wave's loads to be
-// converted (in pw_gemm256_kernel the block's load, split, MFMA and store
-// phases run one after the other between its two barriers per step).
-// Every wait is bounded (kWsSpin polls, then the wave gives up and flags
-// `fault`, so a protocol error ends the launch instead of hanging it).
-constexpr int kWsStages = 2;
-constexpr int kWsSpin = 1 << 22;
-__device__ int g_pw_ws_fault;  // waits that gave up (pcfm_debug_pw_ws_faults)
-__device__ __forceinline__ bool ws_wait(int* ctr, int target) {
-  for (int it = 0; it < kWsSpin; ++it) {
-    if (__hip_atomic_load(ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= target)
-      return true;
-    __builtin_amdgcn_s_sleep(1);
-  }
-  return false;
-}
-
-__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2)))
-    pw_gemm256ws_kernel(const Parts x, const uint16_t* __restrict__ wh,
-                        const uint16_t* __restrict__ wl, const float* __restrict__ bias,
-                        int bias_bstride, const Parts y, int K, int M, int N, int Kpad,
-                        float2* __restrict__ stats, int* __restrict__ fault) {
-  constexpr int TM = 256, TN = 128;
-  constexpr int A_ELEMS = TM * kLDR, B_ELEMS = TN * kLDR;
-  constexpr int STAGE = 2 * A_ELEMS + 2 * B_ELEMS;  // uint16 elements
-  static_assert(STAGE * 2 == 61440, "stage bytes (launcher)");
-  extern __shared__ __attribute__((aligned(16))) uint16_t lds[];
-  __shared__ int full[kWsStages], empty[kWsStages];
-  const int b = blockIdx.z, m0 = blockIdx.y * TM, p0 = blockIdx.x * TN;
-  const int t = threadIdx.x, lane = t & 63;
-  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int nsteps = Kpad / kKT;
-  if (t < kWsStages) {
-    full[t] = 0;
-    empty[t] = 0;
-  }
-  __syncthreads();  // the only block barrier before the epilogue
-
-  if (w >= 4) {
-    // ---------------- producers: 256 threads ----------------
-    const int pt_ = t - 256;
-    const int sp = pt_ % TN, ch = __builtin_amdgcn_readfirstlane((pt_ / TN) * 16);  // 0 / 16
-    const int pt = p0 + sp;
-    const bool pok = pt < N;
-    const int voff = (pok ? pt : N - 1) * 4;
-    const int arow = pt_;  // one weight row (32 channels hi | lo) per thread
-    const __amdgpu_buffer_rsrc_t rwh = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint16_t*>(wh), (short)0, 0x7FFFFFF0, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rwl = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint16_t*>(wl), (short)0, 0x7FFFFFF0, 0x00020000);
-    const int aoff = (m0 + arow) * Kpad * 2;
-    auto load_b = [&](int s, float (&v)[16]) {
-      const int c0 = s * kKT;
-      const int cb = __builtin_amdgcn_readfirstlane(min(c0 + ch, K - 1));
-      const float* xr = x.row(b, cb, N);
-      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-          const_cast<float*>(xr), (short)0, 0x7FFFFFF0, 0x00020000);
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int c = c0 + ch + q;
-        v[q] = __builtin_bit_cast(
-            float, __builtin_amdgcn_raw_buffer_load_b32(rs, voff, (c < K ? c - cb : 0) * N * 4, 0));
-      }
-    };
-    uint4 ra[8];
-    auto load_a = [&](int s) {
-      const int so = s * kKT * 2;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        ra[q] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rwh, aoff, so + 16 * q, 0));
-        ra[4 + q] =
-            __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rwl, aoff, so + 16 * q, 0));
-      }
-    };
-    auto fill = [&](int s, float (&v)[16]) {  // step s -> stage s % 2
-      uint16_t* st = lds + (size_t)(s % kWsStages) * STAGE;
-      uint16_t* dh = st + arow * kLDR;
-      uint16_t* dl = st + A_ELEMS + arow * kLDR;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        *reinterpret_cast<uint4*>(dh + 8 * q) = ra[q];
-        *reinterpret_cast<uint4*>(dl + 8 * q) = ra[4 + q];
-      }
-#pragma unroll
-      for (int q = 0; q < 16; ++q) v[q] = pok && s * kKT + ch + q < K ? v[q] : 0.0f;
-      uint16_t* bh = st + 2 * A_ELEMS + sp * kLDR + ch;
-      store_split<16>(v, bh, bh + B_ELEMS);
-    };
-    float x0[16], x1[16], x2[16];
-    const int last = nsteps - 1;
-    load_b(0, x0);
-    load_b(min(1, last), x1);
-    load_b(min(2, last), x2);
-    load_a(0);
-    bool ok = true;
-    // step s uses x0; x1, x2 hold s+1, s+2; x0 is refilled with s+3 (rotated)
-    for (int s = 0; s < nsteps; ++s) {
-      const int stage = s % kWsStages;
-      if (s >= kWsStages) ok = ok && ws_wait(&empty[stage], 4 * (s / kWsStages));
-      fill(s, x0);
-      __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's stage writes done
-      if (lane == 0) __hip_atomic_fetch_add(&full[stage], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-      if (s + 1 < nsteps) load_a(s + 1);
-#pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        x0[q] = x1[q];
-        x1[q] = x2[q];
-      }
-      load_b(min(s + 3, last), x2);
-    }
-    if (!ok && lane == 0) atomicAdd(fault, 1);
-    return;
-  }
-
-  // ---------------- consumers: waves 0..3, rows 64 w .. 64 w + 63 ----------------
-  const int r = lane & 31, h = lane >> 5;
-  f32x16 acc[2][4];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
-  bool ok = true;
-  for (int s = 0; s < nsteps; ++s) {
-    const int stage = s % kWsStages;
-    ok = ok && ws_wait(&full[stage], 4 * (s / kWsStages + 1));
-    const uint16_t* st = lds + (size_t)stage * STAGE;
-#pragma unroll
-    for (int kk = 0; kk < kKT / 16; ++kk) {
-      bf16x8 ah[2], al[2];
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int o = (w * 64 + i * 32 + r) * kLDR + kk * 16 + 8 * h;
-        ah[i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(st + o));
-        al[i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(st + A_ELEMS + o));
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int o = 2 * A_ELEMS + (j * 32 + r) * kLDR + kk * 16 + 8 * h;
-        const bf16x8 bh = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(st + o));
-        const bf16x8 bl =
-            __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(st + B_ELEMS + o));
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh, acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl, acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh, acc[i][j], 0, 0, 0);
-        }
-      }
-    }
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // this wave's reads of the stage are done
-    if (lane == 0) __hip_atomic_fetch_add(&empty[stage], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-  }
-  if (!ok && lane == 0) atomicAdd(fault, 1);
-  const int bo = b * bias_bstride;
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int mg = m0 + w * 64 + i * 32;
-    float* __restrict__ yr = y.row(b, min(mg, M - 1), N);
-    float bv[16];
-    load_bias16(bias != nullptr ? bias + bo : nullptr, mg, h, M, bv);
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int dm = (e & 3) + 8 * (e >> 2) + 4 * h;
-        const int m = mg + dm;
-        const int p = p0 + j * 32 + r;
-        if (m < M && p < N) out_store(yr + (size_t)dm * N + p, acc[i][j][e] + bv[e]);
-      }
-    if (stats != nullptr) {
-#pragma unroll
-      for (int g = 0; g < 2; ++g) {  // 64-point groups: point tiles 2 g, 2 g + 1
-        const int pw0 = p0 + 64 * g;
-        if (pw0 >= N) continue;
-        const int nv = min(64, N - pw0);
-        const int ngroups = (N + 63) / 64, P = (int)gridDim.z * ngroups;
-        const bool ok0 = pw0 + r < N, ok1 = pw0 + 32 + r < N;
-        float v[32], sr = 0.0f;
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const float v0 = acc[i][2 * g][e] + bv[e], v1 = acc[i][2 * g + 1][e] + bv[e];
-          const float s0 = __builtin_bit_cast(
-              float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v0), 0));
-          const float s1 = __builtin_bit_cast(
-              float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v0), 32));
-          const float shv = h ? s1 : s0;
-          sr = r == e ? shv : sr;
-          const float d0 = ok0 ? v0 - shv : 0.0f, d1 = ok1 ? v1 - shv : 0.0f;
-          v[e] = d0 + d1;
-          v[16 + e] = __builtin_fmaf(d1, d1, d0 * d0);
-        }
-        xpose_reduce_stage<32, 16>(v, r & 16);
-        xpose_reduce_stage<16, 8>(v, r & 8);
-        xpose_reduce_stage<8, 4>(v, r & 4);
-        xpose_reduce_stage<4, 2>(v, r & 2);
-        xpose_reduce_stage<2, 1>(v, r & 1);
-        const float q = swz_xor<16>(v[0]);
-        const int m = mg + (r & 3) + 8 * ((r >> 2) & 3) + 4 * h;
-        if (r < 16 && m < M) {
-          const float a = v[0], mu_s = a / (float)nv;
-          stats[(size_t)m * P + b * ngroups + pw0 / 64] =
-              make_float2(sr + mu_s, fmaxf(__builtin_fmaf(-a, mu_s, q), 0.0f));
-        }
-      }
-    }
-  }
-}
-
 // Streaming form for M <= 128, K <= 256, both multiples of 32 (SharedMLP 128 -> 128 layers and
 // their backward-data, stage-2 proj backward-data): a skinny GEMM that is
 // HBM-bound (x in, y out once), so no point tile is staged through LDS.  The
@@ -1171,12 +955,6 @@ extern "C" int pcfm_pointwise_prep_weight(const float* w, int cout, int cin, int
 
 // Does pw_gemm_launch take the 256-row tile (the one with the BatchNorm
 // statistics epilogue) for this shape?
-// PCFM_PW_WS=1: the warp-specialised 256-row GEMM (A/B knob)
-static bool pw_ws() {
-  const char* e = std::getenv("PCFM_PW_WS");
-  return e != nullptr && e[0] == '1';
-}
-
 static bool pw_takes_256(int b, int cin, int cout, int n) {
   const int Mpad = pw_mpad(cout), Kpad = pad_to(cin, kKT);
   const long long big = (long long)ceil_div(n, 128) * (Mpad / 128) * b;
@@ -1232,20 +1010,8 @@ static int pw_gemm_launch(const Parts& x, const void* wsplit, const float* bias,
 #ifndef PCFM_PW_NO256
   if (Mpad % 256 == 0 && big / 2 >= 2 * kCUs) {
     const dim3 g256(ceil_div(n, 128), Mpad / 256, b);
-    if (pw_ws()) {
-      int e = allow_big_lds((const void*)pw_gemm256ws_kernel);
-      if (e) return e;
-      int* fault = nullptr;
-      if (hipGetSymbolAddress((void**)&fault, HIP_SYMBOL(g_pw_ws_fault)) != hipSuccess) {
-        set_error("pointwise_gemm: fault counter");
-        return PCFM_EINVAL;
-      }
-      hipLaunchKernelGGL(pw_gemm256ws_kernel, g256, dim3(512), (size_t)kWsStages * 61440, st, x,
-                         wh, wh + total, bias, bias_bstride, y, cin, cout, n, Kpad, stats, fault);
-    } else {
-      hipLaunchKernelGGL(pw_gemm256_kernel, g256, dim3(512), 0, st, x, wh, wh + total, bias,
-                         bias_bstride, y, cin, cout, n, Kpad, stats);
-    }
+    hipLaunchKernelGGL(pw_gemm256_kernel, g256, dim3(512), 0, st, x, wh, wh + total, bias,
+                       bias_bstride, y, cin, cout, n, Kpad, stats);
     return check_launch("pointwise_gemm");
   }
 #endif
@@ -1378,12 +1144,4 @@ extern "C" int pcfm_pointwise_wgrad_parts(int nx, const float* const* x, const i
   PCFM_CHECK_ARG(ws_bytes >= need, "pointwise_wgrad_parts: workspace %zu < %zu bytes", ws_bytes,
                  need);
   return pw_wgrad_launch(px, grad_y, b, cin, cout, n, grad_w, ws, (hipStream_t)stream);
-}
-
-// Diagnosis only: waits of the warp-specialised GEMM that gave up since load.
-extern "C" int pcfm_debug_pw_ws_faults(void) {
-  int v = 0;
-  if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(pcfm::g_pw_ws_fault), sizeof(int)) != hipSuccess)
-    return -1;
-  return v;
 }

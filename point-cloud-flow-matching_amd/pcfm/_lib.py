@@ -78,7 +78,6 @@ SIGNATURES = {
     "pcfm_trilinear_devoxelize_scale_add_fwd": (_I, [_P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _P,
                                                      _P, _P]),
     "pcfm_debug_devox_verify": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _P]),
-    "pcfm_debug_pw_ws_faults": (_I, []),
     "pcfm_se_mlp_fwd": (_I, [_P, _P, _P, _I, _I, _I, _P, _P, _P]),
     "pcfm_se_mlp_bwd": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _F, _P, _P, _P, _P]),
     "pcfm_rows_dot": (_I, [_P, _P, _L, _I, _F, _P, _P]),
