@@ -256,6 +256,58 @@ __global__ void __launch_bounds__(1024)
   }
 }
 
+// The one-channel form (cpb == 1: the r = 32 rows of 32768 voxels, 128 KiB, one
+// 1024-thread block per CU): IPT items per thread per round, every item's
+// loads (coordinates / indices, the epilogue's add) issued before any of them
+// is used -- the plain loop had one item's load chain in flight per thread
+// (its store may alias the next item's loads as far as the compiler knows),
+// which held the gather to ~2 TB/s.  Same expressions: bit-identical.
+template <class Prov, int IPT>
+__global__ void __launch_bounds__(1024)
+    gather_rows1_kernel(const float* __restrict__ rows, float* __restrict__ out, int C, int V,
+                        int NI, Prov prov, GatherEpi epi) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  constexpr int T = Prov::TAPS;
+  const int b = blockIdx.z;
+  const int c0 = blockIdx.y;
+  const float* __restrict__ rb = rows + ((size_t)b * C + c0) * V;
+  if ((((uintptr_t)rb) & 15) == 0 && (V & 3) == 0) {
+    const float4* __restrict__ s4 = reinterpret_cast<const float4*>(rb);
+    float4* d4 = reinterpret_cast<float4*>(lds);
+    for (int e = threadIdx.x; e < (V >> 2); e += blockDim.x) d4[e] = s4[e];
+  } else {
+    for (int e = threadIdx.x; e < V; e += blockDim.x) lds[e] = rb[e];
+  }
+  __syncthreads();
+  float* __restrict__ ob = out + ((size_t)b * C + c0) * NI;
+  const float* __restrict__ ab = epi.add != nullptr ? epi.add + ((size_t)b * C + c0) * NI : nullptr;
+  const float sc = epi.scale != nullptr ? epi.scale[(size_t)b * C + c0] : 1.0f;
+  const bool primary = blockIdx.y == 0;
+  const int stride = gridDim.x * blockDim.x;
+  for (int i0 = blockIdx.x * blockDim.x + threadIdx.x; i0 < NI; i0 += IPT * stride) {
+    int id[IPT][T];
+    float w[IPT][T], ad[IPT];
+#pragma unroll
+    for (int u = 0; u < IPT; ++u) {
+      const int i = i0 + u * stride;
+      const bool ok = i < NI;
+      const int iu = ok ? i : i0;
+      ad[u] = ab != nullptr ? nt_ld(ab + iu) : 0.0f;
+      prov.get(b, iu, primary && ok, id[u], w[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < IPT; ++u) {
+      const int i = i0 + u * stride;
+      if (i < NI) {
+        float acc = tap_sum<T>(lds, id[u], w[u]);
+        if (epi.scale != nullptr) acc *= sc;
+        if (ab != nullptr) acc += ad[u];
+        ob[i] = acc;
+      }
+    }
+  }
+}
+
 // The 4-channel form of gather_rows_kernel (cpb == 4, the r = 16 / 8 devox
 // forward and voxelization backward): the four rows are staged interleaved,
 // lds4[v] = (row c0 .. c0+3 at v), so a tap of an item reads its four channels
@@ -422,6 +474,16 @@ inline bool gather4_enabled() {
   return on;
 }
 
+// items per thread per round of the one-channel gather (PCFM_GATHER1_IPT: 1 =
+// the generic loop; A/B knob)
+inline int gather1_ipt() {
+  static const int v = [] {
+    const char* e = std::getenv("PCFM_GATHER1_IPT");
+    return e != nullptr ? std::max(1, std::atoi(e)) : 2;
+  }();
+  return v;
+}
+
 inline RowPlan plan_gather(int B, int C, int V, int NI) {
   RowPlan p;
   const long long target = gather_target_blocks();
@@ -502,6 +564,17 @@ inline int launch_gather(const float* rows, float* out, int B, int C, int V, int
     if (e) return e;
     hipLaunchKernelGGL((gather_rows4_kernel<Prov>), grid, dim3(512), p.lds_bytes, st, rows, out, C,
                        V, NI, prov, epi);
+  } else if (p.use_lds && p.cpb == 1 && p.threads == 1024 && gather1_ipt() > 1) {
+    int e = allow_big_lds((const void*)gather_rows1_kernel<Prov, 2>);
+    if (e) return e;
+    e = allow_big_lds((const void*)gather_rows1_kernel<Prov, 4>);
+    if (e) return e;
+    if (gather1_ipt() >= 4)
+      hipLaunchKernelGGL((gather_rows1_kernel<Prov, 4>), grid, dim3(1024), p.lds_bytes, st, rows,
+                         out, C, V, NI, prov, epi);
+    else
+      hipLaunchKernelGGL((gather_rows1_kernel<Prov, 2>), grid, dim3(1024), p.lds_bytes, st, rows,
+                         out, C, V, NI, prov, epi);
   } else if (p.use_lds) {
     int e = allow_big_lds((const void*)gather_rows_kernel<Prov, true>);
     if (e) return e;
