@@ -23,6 +23,21 @@ for p in (REPO, PKG):
 os.environ.setdefault("PCFM_CHAMFER_CULL_PAIRS", str(16 << 20))
 
 
+@pytest.fixture(autouse=True)
+def _restore_torch_backend_flags():
+    """Trainer(miopen_find=True) switches torch.backends.cudnn.benchmark on for
+    the process; MIOpen's timed solver search then picks per-run algorithms
+    (different summation orders) in every later test.  Each test starts from
+    the flags the session started with."""
+    import torch
+    b = torch.backends
+    old = (b.cudnn.benchmark, b.cudnn.deterministic, b.cudnn.allow_tf32,
+           b.cuda.matmul.allow_tf32)
+    yield
+    (b.cudnn.benchmark, b.cudnn.deterministic, b.cudnn.allow_tf32,
+     b.cuda.matmul.allow_tf32) = old
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a HIP GPU (MI355X); run with -m gpu")
 
