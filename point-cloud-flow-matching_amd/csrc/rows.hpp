@@ -1,4 +1,4 @@
-// Row gather / row scatter engines shared by the voxel ops and grouping.
+// Row gather engine shared by the voxel ops and grouping.
 //
 // Every PVConv scatter/gather in the reference is, for one (batch, channel),
 // a 1-D problem between a "row" of V cells (voxels r^3, or points n) and a list
@@ -11,11 +11,10 @@
 // The reference launches one block per batch element and walks points with a
 // channel loop inside (vox.cu:48-72, trilinear_devox.cu:21-162,
 // grouping.cu:18-77): 8 blocks on a 256-CU part, random 4-byte global gathers
-// and float atomics into HBM.  Here one block owns (batch, channel group,
-// cell chunk): the row segment lives in LDS (<= 128 KiB per block), so every
-// random access is an LDS access (ds_read / ds_add_f32), while HBM only sees
-// coalesced streams -- the item stream in, and the whole row out exactly once
-// (no torch::zeros pre-pass, no global atomics unless a row is split).
+// and float atomics into HBM.  Gathers here: one block owns (batch, channel
+// group), its row lives in LDS (<= 128 KiB per block), so every random access
+// is an LDS read while HBM only sees coalesced streams.  Scatters run on the
+// sorted segment engine (segsum.hpp: fixed summation order, no float atomics).
 #pragma once
 
 #include <algorithm>
@@ -382,60 +381,6 @@ __global__ void __launch_bounds__(512)
   }
 }
 
-// grid = (cell chunks * item splits, channel groups, b).  The block's row
-// segments [v0, v0 + vlen) of `cpb` channels accumulate in LDS (ds_add_f32),
-// then go to HBM once: plain stores when the block owns the whole item range
-// (psplit == 1), global atomics into a zeroed row otherwise.
-template <class Prov>
-__global__ void __launch_bounds__(1024)
-    scatter_rows_kernel(const float* __restrict__ in, float* __restrict__ rows, int C, int V,
-                        int NI, int cpb, int vchunk, int nvchunk, int psplit, Prov prov) {
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-  constexpr int T = Prov::TAPS;
-  const int b = blockIdx.z;
-  const int c0 = blockIdx.y * cpb;
-  const int nc = min(cpb, C - c0);
-  const int vc = blockIdx.x % nvchunk;
-  const int ps = blockIdx.x / nvchunk;
-  const int v0 = vc * vchunk;
-  const int vlen = min(vchunk, V - v0);
-  for (int e = threadIdx.x; e < nc * vchunk; e += blockDim.x) lds[e] = 0.0f;
-  __syncthreads();
-  const int i0 = (int)(((long long)NI * ps) / psplit);
-  const int i1 = (int)(((long long)NI * (ps + 1)) / psplit);
-  const float* __restrict__ ib = in + ((size_t)b * C + c0) * NI;
-  for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
-    int id[T];
-    float w[T];
-    prov.get(b, i, false, id, w);
-    unsigned rel[T];
-#pragma unroll
-    for (int k = 0; k < T; ++k) rel[k] = (unsigned)(id[k] - v0);
-    for (int cc = 0; cc < nc; ++cc) {
-      const float g = ib[(size_t)cc * NI + i];
-      float* lrow = lds + cc * vchunk;
-#pragma unroll
-      for (int k = 0; k < T; ++k) {
-        if (rel[k] < (unsigned)vlen) atomicAdd(lrow + rel[k], w[k] * g);
-      }
-    }
-  }
-  __syncthreads();
-  float* __restrict__ ob = rows + ((size_t)b * C + c0) * V + v0;
-  for (int cc = 0; cc < nc; ++cc) {
-    const float* lrow = lds + cc * vchunk;
-    float* orow = ob + (size_t)cc * V;
-    if (psplit == 1) {
-      for (int o = threadIdx.x; o < vlen; o += blockDim.x) orow[o] = lrow[o];
-    } else {
-      for (int o = threadIdx.x; o < vlen; o += blockDim.x) {
-        const float val = lrow[o];
-        if (val != 0.0f) atomicAdd(orow + o, val);
-      }
-    }
-  }
-}
-
 // ---------------------------------------------------------------------------
 // Launch planning
 // ---------------------------------------------------------------------------
@@ -444,14 +389,11 @@ struct RowPlan {
   int threads = 512;
   int cpb = 1;       // channels per block
   int groups = 1;    // ceil(C / cpb), at least 1
-  int vchunk = 0;    // scatter: LDS row segment length
-  int nvchunk = 1;   // scatter: segments per row
   int psplit = 1;    // item splits (grid.x multiplier)
   bool use_lds = true;
   size_t lds_bytes = 0;
 };
 
-constexpr int kTargetBlocks = 1024;         // 4 per CU
 constexpr int kLdsFloatsSmall = 16 * 1024;  // 64 KiB: 2 blocks of 512 threads per CU
 constexpr int kLdsFloatsBig = 32 * 1024;    // 128 KiB: 1 block of 1024 threads per CU
 
@@ -511,36 +453,6 @@ inline RowPlan plan_gather(int B, int C, int V, int NI) {
   return p;
 }
 
-inline RowPlan plan_scatter(int B, int C, int V, int NI) {
-  RowPlan p;
-  if ((long long)V <= kLdsFloatsSmall) {
-    p.threads = 512;
-    p.vchunk = std::max(V, 1);
-    p.cpb = std::max(1, std::min(C, kLdsFloatsSmall / p.vchunk));
-  } else if ((long long)V <= kLdsFloatsBig) {
-    p.threads = 1024;
-    p.vchunk = V;
-    p.cpb = 1;
-  } else {
-    p.threads = 1024;
-    p.vchunk = kLdsFloatsBig;
-    p.cpb = 1;
-  }
-  p.nvchunk = std::max(1, ceil_div(V, p.vchunk));
-  auto groups = [&](int cpb) { return std::max(1, ceil_div(C, cpb)); };
-  while (p.cpb > 1 && (long long)groups(p.cpb) * p.nvchunk * B < kTargetBlocks)
-    p.cpb = (p.cpb + 1) / 2;
-  p.groups = groups(p.cpb);
-  const long long blocks = (long long)p.groups * p.nvchunk * B;
-  if (blocks < kTargetBlocks) {
-    const int want = ceil_div(kTargetBlocks, blocks);
-    const int cap = std::max(1, NI / 2048);
-    p.psplit = std::min(want, cap);
-  }
-  p.lds_bytes = (size_t)p.cpb * p.vchunk * sizeof(float);
-  return p;
-}
-
 template <class Prov>
 inline bool prov_has_side_outputs(const Prov&) { return false; }
 inline bool prov_has_side_outputs(const ProvDevox& p) { return p.inds_out != nullptr; }
@@ -584,26 +496,6 @@ inline int launch_gather(const float* rows, float* out, int B, int C, int V, int
     hipLaunchKernelGGL((gather_rows_kernel<Prov, false>), grid, dim3(p.threads), 0, st, rows,
                        out, C, V, NI, p.cpb, prov, epi);
   }
-  return check_launch(what);
-}
-
-template <class Prov>
-inline int launch_scatter(const float* in, float* rows, int B, int C, int V, int NI, Prov prov,
-                          hipStream_t st, const char* what) {
-  if (B == 0 || C == 0 || V == 0) return PCFM_OK;
-  RowPlan p = plan_scatter(B, C, V, NI);
-  if (p.psplit > 1) {
-    hipError_t e = hipMemsetAsync(rows, 0, (size_t)B * C * V * sizeof(float), st);
-    if (e != hipSuccess) {
-      set_error("%s: hipMemsetAsync: %s", what, hipGetErrorString(e));
-      return (int)e;
-    }
-  }
-  int e = allow_big_lds((const void*)scatter_rows_kernel<Prov>);
-  if (e) return e;
-  dim3 grid(p.nvchunk * p.psplit, p.groups, B);
-  hipLaunchKernelGGL((scatter_rows_kernel<Prov>), grid, dim3(p.threads), p.lds_bytes, st, in,
-                     rows, C, V, NI, p.cpb, p.vchunk, p.nvchunk, p.psplit, prov);
   return check_launch(what);
 }
 
