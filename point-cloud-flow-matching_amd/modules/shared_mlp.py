@@ -37,7 +37,10 @@ class _PointwiseX3(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             gw = ops.pointwise_backward_weight(x, gy).view_as(weight)
         if ctx.has_bias and ctx.needs_input_grad[2]:
-            gb = gy.sum(dim=(0, 2))
+            # row sums on the rows kernel (torch's sum over dims (0, 2) of a
+            # (8, 64, 20000) gradient ran at 0.8 TB/s), then over the batch
+            bb, cc, nn_ = gy.shape
+            gb = ops.rows_dot(gy.view(bb * cc, nn_), None, 1.0).view(bb, cc).sum(0)
         return gx, gw, gb
 
 

@@ -392,6 +392,28 @@ class _PointwiseParts(torch.autograd.Function):
         return (gw, gb, *gxs)
 
 
+class _MaxTee(torch.autograd.Function):
+    """(f, max of f over the points) with f passed through: f's gradient from
+    its other consumer gets the max's gradient added at the argmax in place, a
+    (B, C) scatter, instead of torch's dense zero-filled max gradient and the
+    autograd add of two (B, C, N) gradients (models.py:523-524 global_mlp)."""
+
+    @staticmethod
+    def forward(ctx, f):
+        m, idx = f.max(dim=-1)
+        ctx.save_for_backward(idx)
+        ctx.shape = f.shape
+        return f.view_as(f), m
+
+    @staticmethod
+    def backward(ctx, df, dm):
+        (idx,) = ctx.saved_tensors
+        if dm is None:
+            return df
+        df = dm.new_zeros(ctx.shape) if df is None else df.contiguous()
+        return df.scatter_add_(2, idx.unsqueeze(-1), dm.unsqueeze(-1))
+
+
 class _TGate(torch.autograd.Function):
     """ctx (B, N, C) = a[b] * head (B, C, N)^T + (1 - a[b]) * glb[b] (models.py:533-541);
     the gate a depends on t only (no gradient)."""
@@ -571,7 +593,14 @@ class ContextNet(_TimeCondEmbed):
             for stage, gb in zip(self.stages[1:], gbs[1:]):
                 f, c = stage(f, c, emb32, gb)
                 scales.append(f)
-            g = self.global_mlp(f.max(dim=-1).values) if self.with_global else None
+            g = None
+            if self.with_global:
+                if f.is_cuda and f.requires_grad:
+                    f, fmax = _MaxTee.apply(f)
+                    scales[-1] = f
+                else:
+                    fmax = f.max(dim=-1).values
+                g = self.global_mlp(fmax)
             pre = self._head_pre(scales, g)
             if isinstance(self.head_norm, nn.GroupNorm) and isinstance(self.head_act, nn.SiLU):
                 h = gn_silu(pre, self.head_norm)  # one fused pass pair on the GPU

@@ -13,6 +13,9 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [REPO, os.path.join(REPO, "point-cloud-flow-matching_amd")]
 
 
+_OURS = ("point-cloud-flow-matching_amd", "pcfm/", "modules/", "PyTorchEMD/", "chamfer3D/")
+
+
 def main():
     from pcfm import _lib
     from pcfm.train import TrainConfig, Trainer, synthetic_batch
@@ -27,7 +30,9 @@ def main():
         tr.step(batch, epoch)
     torch.cuda.synchronize(dev)
     acts = [torch.profiler.ProfilerActivity.CPU, torch.profiler.ProfilerActivity.CUDA]
-    with torch.profiler.profile(activities=acts, record_shapes=True, with_stack=True) as prof:
+    cfgx = torch._C._profiler._ExperimentalConfig(verbose=True)  # populates e.stack
+    with torch.profiler.profile(activities=acts, record_shapes=True, with_stack=True,
+                                experimental_config=cfgx) as prof:
         tr.step(batch, epoch)
         torch.cuda.synchronize(dev)
     agg = defaultdict(lambda: {"calls": 0, "dev_us": 0.0})
@@ -37,9 +42,16 @@ def main():
         dev_us = sum(k.duration for k in e.kernels) if e.kernels else 0.0
         if dev_us <= 0:
             continue
-        frames = [f for f in (e.stack or []) if REPO in f and "torch_ops.py" not in f]
-        key = (e.name, str(e.input_shapes)[:120], " <- ".join(f.replace(REPO + "/", "")
-                                                             for f in frames[:3]))
+        # the box runs a snapshot whose path differs from REPO: keep the package's frames
+        frames = [f for f in (e.stack or []) if any(m in f for m in _OURS)
+                  and "torch_ops.py" not in f and "site-packages" not in f]
+        where = " <- ".join(f.split("/")[-1] for f in frames[:3])
+        if not where:  # backward ops run on the autograd thread: name the node instead
+            p = e.cpu_parent
+            while p is not None and not p.name.startswith("autograd::engine"):
+                p = p.cpu_parent
+            where = p.name.split(": ")[-1] if p is not None else ""
+        key = (e.name, str(e.input_shapes)[:120], where)
         agg[key]["calls"] += 1
         agg[key]["dev_us"] += dev_us
     rows = sorted(agg.items(), key=lambda kv: -kv[1]["dev_us"])
