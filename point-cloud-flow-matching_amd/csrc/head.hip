@@ -406,19 +406,34 @@ __global__ void __launch_bounds__(256)
   const long long r0 = rows * p / P, r1 = rows * (p + 1) / P;
   __shared__ float red[256 * 2];
   float s0 = 0.0f, s1 = 0.0f;
+  auto ld = [&](long long r) {
+    const size_t o = ((size_t)b * rows + r) * C + 2 * cp;
+    if constexpr (BF16) {
+      const uint32_t q = *reinterpret_cast<const uint32_t*>(
+          reinterpret_cast<const uint16_t*>(x) + o);
+      return make_float2(__uint_as_float(q << 16), __uint_as_float(q & 0xFFFF0000u));
+    } else {
+      return *reinterpret_cast<const float2*>(reinterpret_cast<const float*>(x) + o);
+    }
+  };
   if (rl < rstep) {
-    for (long long r = r0 + rl; r < r1; r += rstep) {
-      const size_t o = ((size_t)b * rows + r) * C + 2 * cp;
-      if constexpr (BF16) {
-        const uint32_t q = *reinterpret_cast<const uint32_t*>(
-            reinterpret_cast<const uint16_t*>(x) + o);
-        s0 += __uint_as_float(q << 16);
-        s1 += __uint_as_float(q & 0xFFFF0000u);
-      } else {
-        const float2 q = *reinterpret_cast<const float2*>(reinterpret_cast<const float*>(x) + o);
-        s0 += q.x;
-        s1 += q.y;
+    long long r = r0 + rl;
+    // 8 rows' loads in flight before they are added, in the same row order (one
+    // dependent load per add kept a thread latency-bound: 0.84 TB/s)
+    for (; r + 7 * rstep < r1; r += 8 * rstep) {
+      float2 q[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) q[u] = ld(r + u * rstep);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        s0 += q[u].x;
+        s1 += q[u].y;
       }
+    }
+    for (; r < r1; r += rstep) {
+      const float2 q = ld(r);
+      s0 += q.x;
+      s1 += q.y;
     }
   }
   red[2 * threadIdx.x] = s0;
