@@ -28,7 +28,7 @@ from __future__ import annotations
 import math
 import os
 import random
-from dataclasses import dataclass, field
+from dataclasses import asdict, dataclass, field
 from typing import Dict, List, Optional
 
 import torch
@@ -402,6 +402,62 @@ class Trainer:
             self.scaler.step(self.opt)
             self.scaler.update()
         self.opt.zero_grad(set_to_none=True)
+
+    # -- checkpoint / resume (train.py:681-699 save, :470-520 resume) ---------
+    def checkpoint(self, epoch: int) -> Dict:
+        """The reference's checkpoint dict: epoch, the three models' state dicts,
+        the EMA shadows, args, cond_dim, optimizer (torch AdamW layout) and AMP
+        scaler state, global step.  torch.save-able with weights_only loads."""
+        cfg = self.cfg
+        args = {k: (list(v) if isinstance(v, tuple) else v) for k, v in asdict(cfg).items()}
+        args.update(enc_in_channels=cfg.enc_in_ch, pf_point_dim=cfg.pf_point_dim)
+        return {
+            "epoch": int(epoch),
+            "encoder": self.enc.state_dict(),
+            "pf": self.pf.state_dict(),
+            "lf": self.lf.state_dict(),
+            "ema_pf": {k: v.detach().clone() for k, v in self.ema_pf.shadow.items()},
+            "ema_lf": {k: v.detach().clone() for k, v in self.ema_lf.shadow.items()},
+            "args": args,
+            "cond_dim": cfg.cond_dim,
+            "opt": self.opt.state_dict(),
+            "scaler": self.scaler.state_dict() if cfg.amp else None,
+            "global_step": int(self.global_step),
+        }
+
+    def load_checkpoint(self, ckpt: Dict) -> int:
+        """Resume from a `checkpoint()` dict (or the reference's): encoder strict,
+        pf (or the old key "model") and lf non-strict, EMA shadow entries present
+        in the file copied in place (the fused update holds these tensors), the
+        optimizer and AMP scaler state when present.  Returns the epoch to run
+        next (the saved epoch + 1), as the reference's auto-resume does."""
+        if "encoder" in ckpt:
+            self.enc.load_state_dict(ckpt["encoder"], strict=True)
+        if "pf" in ckpt:
+            self.pf.load_state_dict(ckpt["pf"], strict=False)
+        elif "model" in ckpt:
+            self.pf.load_state_dict(ckpt["model"], strict=False)
+        if "lf" in ckpt:
+            self.lf.load_state_dict(ckpt["lf"], strict=False)
+        with torch.no_grad():
+            for ema, key in ((self.ema_pf, "ema_pf"), (self.ema_lf, "ema_lf")):
+                src = ckpt.get(key)
+                if not isinstance(src, dict):
+                    continue
+                for k, cur in ema.shadow.items():
+                    v = src.get(k)
+                    if torch.is_tensor(v) and v.dtype.is_floating_point:
+                        if tuple(v.shape) != tuple(cur.shape):
+                            raise ValueError(f"load_checkpoint: {key}[{k}] shape "
+                                             f"{tuple(v.shape)} != {tuple(cur.shape)}")
+                        cur.copy_(v.to(device=cur.device, dtype=cur.dtype))
+        opt_sd = ckpt.get("opt", ckpt.get("opt_main"))
+        if opt_sd is not None:
+            self.opt.load_state_dict(opt_sd)
+        if self.cfg.amp and ckpt.get("scaler") is not None:
+            self.scaler.load_state_dict(ckpt["scaler"])
+        self.global_step = int(ckpt.get("global_step", self.global_step))
+        return int(ckpt.get("epoch", 0)) + 1
 
     # -- one iteration ------------------------------------------------------
     def step(self, batch: Dict[str, torch.Tensor], epoch: int,
