@@ -94,6 +94,32 @@ __global__ void __launch_bounds__(256)
   }
 }
 
+// s = sum of part[2p], q = sum of part[2p + 1] over p < P, added in p order;
+// 8 partials' loads in flight at a time (the serial form kept the thread that
+// derives a block's statistics waiting on one load per partial)
+__device__ __forceinline__ void sum_parts2(const float* __restrict__ part, int P, float& s,
+                                           float& q) {
+  const float2* __restrict__ p2 = reinterpret_cast<const float2*>(part);
+  s = 0.0f;
+  q = 0.0f;
+  int p = 0;
+  for (; p + 8 <= P; p += 8) {
+    float2 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = p2[p + u];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      s += v[u].x;
+      q += v[u].y;
+    }
+  }
+  for (; p < P; ++p) {
+    const float2 v = p2[p];
+    s += v.x;
+    q += v.y;
+  }
+}
+
 // one thread per channel: mean, invstd (biased variance, as BN normalises) and
 // the running-stat update with the unbiased variance (torch's batch_norm).
 __global__ void __launch_bounds__(256)
@@ -103,11 +129,8 @@ __global__ void __launch_bounds__(256)
                        float* __restrict__ invstd) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
-  float s = 0.0f, q = 0.0f;
-  for (int p = 0; p < P; ++p) {
-    s += part[((size_t)c * P + p) * 2];
-    q += part[((size_t)c * P + p) * 2 + 1];
-  }
+  float s, q;
+  sum_parts2(part + (size_t)c * P * 2, P, s, q);
   const double n = (double)B * S;
   const float K = x[(size_t)c * S];
   const float md = (float)(s / n);
@@ -134,11 +157,8 @@ struct BnFwdFin {
   long long* nbt;  // BatchNorm num_batches_tracked (+1 by channel 0's publisher), or NULL
   __device__ __forceinline__ void get(const float* x, int c, float& m, float& is, float& var,
                                       double& n) const {
-    float s = 0.0f, q = 0.0f;
-    for (int p = 0; p < P; ++p) {
-      s += part[((size_t)c * P + p) * 2];
-      q += part[((size_t)c * P + p) * 2 + 1];
-    }
+    float s, q;
+    sum_parts2(part + (size_t)c * P * 2, P, s, q);
     n = (double)B * S;
     const float K = x[(size_t)c * S];
     const float md = (float)(s / n);
@@ -159,30 +179,54 @@ struct BnFwdFin {
 };
 __device__ __forceinline__ void bn_bwd_fin(const float* part, int P, int c, float& sg,
                                            float& sgx) {
-  sg = 0.0f;
-  sgx = 0.0f;
-  for (int p = 0; p < P; ++p) {
-    sg += part[((size_t)c * P + p) * 2];
-    sgx += part[((size_t)c * P + p) * 2 + 1];
-  }
+  sum_parts2(part + (size_t)c * P * 2, P, sg, sgx);
 }
 
 // Statistics from a producer's epilogue (pw_gemm256_kernel with stats): part
 // float2 [C][P], the (mean, centred sum of squares) of P groups of up to 64
 // values, group p holding min(64, S - (p % G) 64) values (G = ceil(S / 64)).
-// One wave per channel: lane l combines groups l, l + 64, ... in order (Chan's
-// update, fp64), then a fixed xor tree; lane 0 publishes mean / invstd and the
-// running statistics exactly as BnFwdFin::publish.  Deterministic.
-__global__ void __launch_bounds__(64)
+// Four waves per channel: thread t combines groups t, t + 256, ... in order
+// (Chan's update, fp64; 4 groups' loads in flight at a time), then a fixed xor
+// tree per wave and the 4 wave results in wave order; thread 0 publishes mean /
+// invstd and the running statistics exactly as BnFwdFin::publish.
+// Deterministic.  (One wave per channel walked ~40 dependent loads per lane:
+// 17 us per launch at P = 2504.)
+__device__ __forceinline__ void chan_merge(double& n, double& mu, double& m2, double nb, double mb,
+                                           double qb) {
+  const double nn = n + nb;
+  if (nn > 0.0) {
+    const double d = mb - mu;
+    mu += d * nb / nn;
+    m2 += qb + d * d * n * nb / nn;
+  }
+  n = nn;
+}
+
+__global__ void __launch_bounds__(256)
     bn_fin_parts_kernel(const float2* __restrict__ part, int P, int S, float eps, float momentum,
                         float* __restrict__ rmean, float* __restrict__ rvar,
                         long long* __restrict__ nbt, float* __restrict__ mean,
                         float* __restrict__ invstd) {
-  const int c = blockIdx.x, l = threadIdx.x;
+  const int c = blockIdx.x, t = threadIdx.x, l = t & 63, w = t >> 6;
   const int G = (S + 63) / 64;
   double n = 0.0, mu = 0.0, m2 = 0.0;
-  for (int p = l; p < P; p += 64) {
-    const float2 v = part[(size_t)c * P + p];
+  const float2* __restrict__ pc = part + (size_t)c * P;
+  int p = t;
+  for (; p + 3 * 256 < P; p += 4 * 256) {
+    float2 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = pc[p + u * 256];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const double nb = (double)min(64, S - ((p + u * 256) % G) * 64);
+      const double nn = n + nb, d = (double)v[u].x - mu;
+      mu += d * nb / nn;
+      m2 += (double)v[u].y + d * d * n * nb / nn;
+      n = nn;
+    }
+  }
+  for (; p < P; p += 256) {
+    const float2 v = pc[p];
     const double nb = (double)min(64, S - (p % G) * 64);
     const double nn = n + nb, d = (double)v.x - mu;
     mu += d * nb / nn;
@@ -190,18 +234,22 @@ __global__ void __launch_bounds__(64)
     n = nn;
   }
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const double nb = __shfl_xor(n, o, 64), mb = __shfl_xor(mu, o, 64),
-                 qb = __shfl_xor(m2, o, 64);
-    const double nn = n + nb;
-    if (nn > 0.0) {
-      const double d = mb - mu;
-      mu += d * nb / nn;
-      m2 += qb + d * d * n * nb / nn;
-    }
-    n = nn;
-  }
+  for (int o = 32; o > 0; o >>= 1)
+    chan_merge(n, mu, m2, __shfl_xor(n, o, 64), __shfl_xor(mu, o, 64), __shfl_xor(m2, o, 64));
+  __shared__ double wr[4][3];
   if (l == 0) {
+    wr[w][0] = n;
+    wr[w][1] = mu;
+    wr[w][2] = m2;
+  }
+  __syncthreads();
+  if (t == 0) {
+    n = wr[0][0];
+    mu = wr[0][1];
+    m2 = wr[0][2];
+    for (int k = 1; k < 4; ++k) chan_merge(n, mu, m2, wr[k][0], wr[k][1], wr[k][2]);
+  }
+  if (t == 0) {
     const float var = fmaxf((float)(m2 / n), 0.0f);
     const float m = (float)mu;
     mean[c] = m;
@@ -334,11 +382,8 @@ __global__ void __launch_bounds__(256)
                            float* __restrict__ dbeta) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
-  float sg = 0.0f, sgx = 0.0f;
-  for (int p = 0; p < P; ++p) {
-    sg += part[((size_t)c * P + p) * 2];
-    sgx += part[((size_t)c * P + p) * 2 + 1];
-  }
+  float sg, sgx;
+  sum_parts2(part + (size_t)c * P * 2, P, sg, sgx);
   dbeta[c] = sg;
   dgamma[c] = sgx;
 }
@@ -874,7 +919,7 @@ extern "C" int pcfm_bn_act_fwd_parts(const float* x, const float* part, int P, c
   PCFM_CHECK_ARG((running_mean == nullptr) == (running_var == nullptr),
                  "bn_act_fwd_parts: running_mean and running_var must both be given or both NULL");
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(bn_fin_parts_kernel, dim3(c), dim3(64), 0, st,
+  hipLaunchKernelGGL(bn_fin_parts_kernel, dim3(c), dim3(256), 0, st,
                      reinterpret_cast<const float2*>(part), P, s, eps, momentum, running_mean,
                      running_var, num_batches_tracked, mean, invstd);
   const BnFwdFin fin{nullptr, b, s, 0, eps, momentum, running_mean, running_var, nullptr};
