@@ -972,13 +972,10 @@ static int pw_gemm_launch(const Parts& x, const void* wsplit, const float* bias,
   const uint16_t* wh = (const uint16_t*)wsplit;
   const long long big = (long long)ceil_div(n, 128) * (Mpad / 128) * b;
 #ifndef PCFM_PW_NOSTREAM
-  // M > 128 in 128-row slices: opt-in (PCFM_PW_STREAM_M=1) until measured
-  static const bool stream_m = [] {
-    const char* e = getenv("PCFM_PW_STREAM_M");
-    return e != nullptr && e[0] == '1';
-  }();
-  if ((Mpad == 128 || (stream_m && Mpad % 128 == 0)) && Kpad <= 256 && cin % 32 == 0 &&
-      cout % 32 == 0) {
+  // (M > 128 in 128-row slices of this form was an opt-in experiment; measured
+  // in round 4 it failed the parity tests -- wrong and run-to-run different
+  // outputs -- and was removed)
+  if (Mpad == 128 && Kpad <= 256 && cin % 32 == 0 && cout % 32 == 0) {
     const uint16_t* wl_img = wh + total;
     const long long tiles = (long long)b * ceil_div(n, 32);
     const size_t lds = (size_t)2 * 128 * (Kpad + 8) * sizeof(uint16_t);
