@@ -43,6 +43,8 @@ for _p in (REPO, PKG):
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
+from pcfm.dist_env import pin_rccl_env  # noqa: E402
+
 METRIC = "train-step points/sec (B=8, N=20000, xyz+rgb) at 1/2/4/8 MI355X; Chamfer ms"
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 FP32_VALU_TF = 157.3            # MI355X fp32 vector peak (Chamfer / ball query: VALU-bound)
@@ -292,8 +294,11 @@ def launch_ranks(args, backend):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
            f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1", f"--master-port={port}",
            os.path.abspath(__file__), *sys.argv[1:]]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    if backend == "nccl":
+        pin_rccl_env(env)  # every rank's RCCL on the ring kernels (pcfm/dist_env.py)
     log("launching:", " ".join(cmd))
-    sys.exit(subprocess.call(cmd, env=dict(os.environ, MASTER_ADDR="127.0.0.1")))
+    sys.exit(subprocess.call(cmd, env=env))
 
 
 def main():
@@ -319,6 +324,8 @@ def main():
     ddp = world > 1
     local = local % max(1, ndev)
     if ddp:
+        if backend == "nccl":
+            pin_rccl_env()  # ranks started by the driver's torch.distributed.run too
         torch.cuda.set_device(local)
         dist.init_process_group(backend, init_method="env://")
     dev = torch.device("cuda", local)
@@ -523,7 +530,8 @@ def main():
             "kernels": kernels, "cpu_baseline": cpu, "chamfer": cham, **extra,
             "loss_point": loss_p, "loss_latent": loss_z,
             "distributed": {"backend": dist.get_backend() if ddp else None,
-                            "world_size": dist.get_world_size() if ddp else 1},
+                            "world_size": dist.get_world_size() if ddp else 1,
+                            "NCCL_ALGO": os.environ.get("NCCL_ALGO") if ddp else None},
         }
         print(json.dumps(line), flush=True)
     if ddp:

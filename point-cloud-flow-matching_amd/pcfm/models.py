@@ -396,22 +396,33 @@ class _MaxTee(torch.autograd.Function):
     """(f, max of f over the points) with f passed through: f's gradient from
     its other consumer gets the max's gradient added at the argmax in place, a
     (B, C) scatter, instead of torch's dense zero-filled max gradient and the
-    autograd add of two (B, C, N) gradients (models.py:523-524 global_mlp)."""
+    autograd add of two (B, C, N) gradients (models.py:523-524 global_mlp).
+
+    The add is in place only when the caller passes `exclusive_grad=True`,
+    asserting that f's other consumer returns a freshly allocated gradient
+    that nothing else holds (`_PointwiseParts`, whose backward allocates every
+    input gradient); otherwise the incoming gradient is cloned first."""
 
     @staticmethod
-    def forward(ctx, f):
+    def forward(ctx, f, exclusive_grad=False):
         m, idx = f.max(dim=-1)
         ctx.save_for_backward(idx)
         ctx.shape = f.shape
+        ctx.exclusive = bool(exclusive_grad)
         return f.view_as(f), m
 
     @staticmethod
     def backward(ctx, df, dm):
         (idx,) = ctx.saved_tensors
         if dm is None:
-            return df
-        df = dm.new_zeros(ctx.shape) if df is None else df.contiguous()
-        return df.scatter_add_(2, idx.unsqueeze(-1), dm.unsqueeze(-1))
+            return df, None
+        if df is None:
+            df = dm.new_zeros(ctx.shape)
+        elif ctx.exclusive and df.is_contiguous():
+            pass  # the consumer's own fresh tensor: add in place
+        else:
+            df = df.clone(memory_format=torch.contiguous_format)
+        return df.scatter_add_(2, idx.unsqueeze(-1), dm.unsqueeze(-1)), None
 
 
 class _TGate(torch.autograd.Function):
@@ -546,6 +557,13 @@ class ContextNet(_TimeCondEmbed):
                 out[si][bi] = (parts[2 * j], parts[2 * j + 1])
         return out
 
+    def _head_pre_segmented(self, scales: List[torch.Tensor]) -> bool:
+        """Whether _head_pre runs as one _PointwiseParts node over the scales."""
+        widths = [int(s.shape[1]) for s in scales]
+        return bool(self.head_pre.x3_ok(scales[-1]) and len(scales) <= 4
+                    and self.head_pre.bias is not None
+                    and all(w % 128 == 0 for w in widths[:-1]))
+
     def _head_pre(self, scales: List[torch.Tensor], g: Optional[torch.Tensor]) -> torch.Tensor:
         """head_pre(cat(scales | g broadcast over points)) (models.py:460-466).
 
@@ -554,9 +572,8 @@ class ContextNet(_TimeCondEmbed):
         weight collapse to a per-cloud bias W_g g + b (the broadcast columns
         are constant along the points)."""
         pre = self.head_pre
-        widths = [int(s.shape[1]) for s in scales]
-        if (pre.x3_ok(scales[-1]) and len(scales) <= 4 and pre.bias is not None
-                and all(w % 128 == 0 for w in widths[:-1])):
+        if self._head_pre_segmented(scales):
+            widths = [int(s.shape[1]) for s in scales]
             w = pre.weight[:, :, 0]
             cs = sum(widths)
             if g is not None:
@@ -596,7 +613,9 @@ class ContextNet(_TimeCondEmbed):
             g = None
             if self.with_global:
                 if f.is_cuda and f.requires_grad:
-                    f, fmax = _MaxTee.apply(f)
+                    # in place only when f's other consumer is _head_pre's
+                    # _PointwiseParts, whose backward returns fresh gradients
+                    f, fmax = _MaxTee.apply(f, self._head_pre_segmented(scales))
                     scales[-1] = f
                 else:
                     fmax = f.max(dim=-1).values

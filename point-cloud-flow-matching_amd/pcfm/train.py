@@ -36,6 +36,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 from torch import distributed as dist
 
+from pcfm.dist_env import pin_rccl_env
 from pcfm.models import (ConditionalLatentVelocityNet, HybridMLP, ShapeEncoder, VelocityNet)
 
 
@@ -151,6 +152,7 @@ def init_distributed(backend: Optional[str] = None):
         if backend is None:
             backend = "nccl" if torch.cuda.is_available() else "gloo"
         if backend == "nccl":
+            pin_rccl_env()  # the all-reduce on RCCL's ring kernels (pcfm/dist_env.py)
             torch.cuda.set_device(local)
         if not dist.is_initialized():
             dist.init_process_group(backend=backend, init_method="env://")
@@ -429,7 +431,8 @@ class Trainer:
         """Resume from a `checkpoint()` dict (or the reference's): encoder strict,
         pf (or the old key "model") and lf non-strict, EMA shadow entries present
         in the file copied in place (the fused update holds these tensors), the
-        optimizer and AMP scaler state when present.  Returns the epoch to run
+        optimizer and AMP scaler state when present and loadable (otherwise a
+        warning, as the reference's auto-resume).  Returns the epoch to run
         next (the saved epoch + 1), as the reference's auto-resume does."""
         if "encoder" in ckpt:
             self.enc.load_state_dict(ckpt["encoder"], strict=True)
@@ -451,11 +454,22 @@ class Trainer:
                             raise ValueError(f"load_checkpoint: {key}[{k}] shape "
                                              f"{tuple(v.shape)} != {tuple(cur.shape)}")
                         cur.copy_(v.to(device=cur.device, dtype=cur.dtype))
-        opt_sd = ckpt.get("opt", ckpt.get("opt_main"))
-        if opt_sd is not None:
-            self.opt.load_state_dict(opt_sd)
+        # optimizer / AMP scaler: a state that does not fit (groups, betas,
+        # shapes) is reported and skipped, the weights, EMA and epoch still
+        # resume -- the reference's auto-resume (train.py:498-516)
+        key = "opt" if "opt" in ckpt else ("opt_main" if "opt_main" in ckpt else None)
+        if key is not None:
+            try:
+                self.opt.load_state_dict(ckpt[key])
+            except Exception as e:  # noqa: BLE001 -- the reference's catch-all
+                if self.rank == 0:
+                    print(f"[Auto-Resume][WARN] {key} state load failed: {e}")
         if self.cfg.amp and ckpt.get("scaler") is not None:
-            self.scaler.load_state_dict(ckpt["scaler"])
+            try:
+                self.scaler.load_state_dict(ckpt["scaler"])
+            except Exception as e:  # noqa: BLE001
+                if self.rank == 0:
+                    print(f"[Auto-Resume][WARN] scaler state load failed: {e}")
         self.global_step = int(ckpt.get("global_step", self.global_step))
         return int(ckpt.get("epoch", 0)) + 1
 

@@ -59,6 +59,21 @@ def test_load_checkpoint_rejects_wrong_ema_shape(oracle_backend):
         raise AssertionError("a wrong-shape EMA entry was accepted")
 
 
+def test_unfitting_optimizer_state_warns_and_resumes(oracle_backend, capsys):
+    """An optimizer / scaler state that does not load (here: one parameter group
+    missing) is reported and skipped; weights, EMA and epoch still resume
+    (reference train.py:498-516)."""
+    a = Trainer(_cfg(0), "cpu")
+    ck = a.checkpoint(epoch=6)
+    ck["opt"]["param_groups"] = ck["opt"]["param_groups"][:2]
+    ck["scaler"] = {"scale": "not a number"}
+    b = Trainer(_cfg(123), "cpu")
+    assert b.load_checkpoint(ck) == 7
+    assert "opt state load failed" in capsys.readouterr().out
+    sa, sb = _state(a), _state(b)
+    assert all(torch.equal(sa[k], sb[k]) for k in sa)
+
+
 @__import__("pytest").mark.gpu
 def test_resume_fused_step_gpu(tmp_path):
     """Same on the GPU path: fused AdamW + EMA update (pcfm.optim), bf16 autocast
