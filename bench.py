@@ -11,7 +11,9 @@ Prints ONE JSON line on rank 0.  value = points/s of the whole job
 (world * B * N * K / max-over-ranks wall time of K steps); inputs are resident
 in HBM before the timed region.  Besides the contract fields it carries:
   roofline      the dominant hot-path kernel (by time inside the step), its
-                algorithmic bytes / its HIP-event time, vs 8 TB/s
+                algorithmic FLOPs / its HIP-event time
+  roofline_step the whole step: sum_k FLOP_k / peak_k / t_step, against
+                the bf16x3 and the fp32 peaks for the fp32 convs
   cpu_baseline  the same train step on the host CPU -- the reference's model
                 math (per-point FiLM as models.py:135/594 computes it, fp32
                 torch CPU convolutions) on this build's pure-PyTorch CPU
@@ -107,6 +109,46 @@ def scatter_gather_bytes(batch, points, stages=((128, 32), (256, 16), (256, 8)),
         db = b * (c * n * 4 + 16 * n * 4 + c * v * 4)
         tot += blocks * (vf + vb + df + db)
     return tot
+
+
+# the train step's FLOPs as the reference executes them at C2
+# (B=8, N=20000, hybrid): 1x1 convs 928.8 GFLOP (fp32), per-point head GEMMs
+# 2679.8 (bf16 autocast), encoder + latent net 32 (bf16); the Conv3d FLOPs
+# (4348.5 at C2) follow from the stage config.  Per-point terms scale with B*N,
+# the Conv3d term with B (the grids are fixed-size).
+SURVEY_C2_POINTS = 8 * 20000
+SURVEY_STEP_GFLOP = {"pointwise_fp32": 928.8, "head_bf16": 2679.8, "enc_lf_bf16": 32.0}
+
+
+def conv3d_step_flops(cfg):
+    """fwd + bwd-data + wgrad of every 3x3x3 conv of the PVConv pyramid:
+    3 x 2 B R^3 27 C^2 per conv, two convs per PVConv block."""
+    tot = 0.0
+    for c, nb, r in zip(cfg.ctx_stage_channels, cfg.ctx_stage_blocks, cfg.ctx_stage_res):
+        tot += nb * 2 * 3 * 2.0 * cfg.batch_size * r ** 3 * 27 * c * c
+    return tot
+
+
+def step_roofline(cfg, ms):
+    """SURVEY 8(d)'s train-step rate: sum_k FLOP_k / peak_k over t_step, against
+    the fp32 convs' two candidate peaks: the bf16x3 matrix-core rate this build
+    runs them at (2500 TF / 3) and the fp32 vector peak SURVEY priced them at
+    (157.3 TF); the bf16 GEMMs at 2500 TF either way."""
+    if cfg.pf_backbone != "hybrid":
+        return None
+    scale = cfg.batch_size * cfg.num_points / SURVEY_C2_POINTS
+    conv = conv3d_step_flops(cfg)
+    pw = SURVEY_STEP_GFLOP["pointwise_fp32"] * 1e9 * scale
+    bf16 = (SURVEY_STEP_GFLOP["head_bf16"] + SURVEY_STEP_GFLOP["enc_lf_bf16"]) * 1e9 * scale
+    out = {"definition": "sum_k FLOP_k / peak_k / t_step (SURVEY.md 8d, reference-as-executed "
+                         "FLOPs: Conv3d and 1x1 convs fp32, head / encoder GEMMs bf16)",
+           "gflop": {"conv3d_fp32": conv / 1e9, "pointwise_fp32": pw / 1e9,
+                     "gemm_bf16": bf16 / 1e9}, "t_step_ms": ms}
+    for key, fp32_peak in (("vs_bf16x3_peak", BF16X3_PEAK_TF), ("vs_fp32_peak", FP32_VALU_TF)):
+        floor = ((conv + pw) / (fp32_peak * 1e12) + bf16 / (BF16_DENSE_TF * 1e12)) * 1e3
+        out[key] = {"fp32_conv_peak_TF": fp32_peak, "bf16_peak_TF": BF16_DENSE_TF,
+                    "floor_ms": floor, "frac": floor / ms}
+    return out
 
 
 def committed_mfma_busy(op):
@@ -525,7 +567,8 @@ def main():
                                    "latent 128, 1 joint, stages (128,256,256)@(32,16,8)",
                        "global_batch": world * cfg.batch_size, "points_per_cloud": cfg.num_points,
                        "backbone": cfg.pf_backbone, "parallelism": f"dp{world}"},
-            "roofline": roofline, "roofline_voxel_scatter_gather": roofline_scatter,
+            "roofline": roofline, "roofline_step": step_roofline(cfg, ms),
+            "roofline_voxel_scatter_gather": roofline_scatter,
             "roofline_voxel_scatter_gather_all": roofline_sg_all,
             "kernels": kernels, "cpu_baseline": cpu, "chamfer": cham, **extra,
             "loss_point": loss_p, "loss_latent": loss_z,

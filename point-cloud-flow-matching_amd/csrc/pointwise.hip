@@ -953,16 +953,25 @@ extern "C" int pcfm_pointwise_prep_weight(const float* w, int cout, int cin, int
   return check_launch("pointwise_prep_weight");
 }
 
-// Does pw_gemm_launch take the 256-row tile (the one with the BatchNorm
-// statistics epilogue) for this shape?
-static bool pw_takes_256(int b, int cin, int cout, int n) {
+// The forward GEMM's kernel for a shape: ONE decision, used by the launcher
+// and by pcfm_pointwise_bnstats_groups(), so a caller is never told that a
+// shape writes BatchNorm statistics when the kernel that runs does not.
+enum class PwPath { Stream128, Tile256, Tile128, Tile64 };
+
+static PwPath pw_path(int b, int cin, int cout, int n) {
   const int Mpad = pw_mpad(cout), Kpad = pad_to(cin, kKT);
   const long long big = (long long)ceil_div(n, 128) * (Mpad / 128) * b;
 #ifndef PCFM_PW_NOSTREAM
-  if (Mpad == 128 && Kpad <= 256 && cin % 32 == 0 && cout % 32 == 0) return false;
+  if (Mpad == 128 && Kpad <= 256 && cin % 32 == 0 && cout % 32 == 0) return PwPath::Stream128;
 #endif
-  return Mpad % 256 == 0 && big / 2 >= 2 * kCUs;
+#ifndef PCFM_PW_NO256
+  if (Mpad % 256 == 0 && big / 2 >= 2 * kCUs) return PwPath::Tile256;
+#endif
+  return big >= 2 * kCUs ? PwPath::Tile128 : PwPath::Tile64;
 }
+
+// Only the 256-row tile has the statistics epilogue.
+static bool pw_path_has_stats(PwPath p) { return p == PwPath::Tile256; }
 
 static int pw_gemm_launch(const Parts& x, const void* wsplit, const float* bias, int bias_bstride,
                           int b, int cin, int cout, int n, const Parts& y, hipStream_t st,
@@ -970,12 +979,13 @@ static int pw_gemm_launch(const Parts& x, const void* wsplit, const float* bias,
   const int Mpad = pw_mpad(cout), Kpad = pad_to(cin, kKT);
   const size_t total = (size_t)Mpad * Kpad;
   const uint16_t* wh = (const uint16_t*)wsplit;
-  const long long big = (long long)ceil_div(n, 128) * (Mpad / 128) * b;
-#ifndef PCFM_PW_NOSTREAM
-  // (M > 128 in 128-row slices of this form was an opt-in experiment; measured
-  // in round 4 it failed the parity tests -- wrong and run-to-run different
-  // outputs -- and was removed)
-  if (Mpad == 128 && Kpad <= 256 && cin % 32 == 0 && cout % 32 == 0) {
+  const PwPath path = pw_path(b, cin, cout, n);
+  // a statistics request the chosen kernel cannot serve fails loudly (it used
+  // to be dropped, leaving the caller's stats buffer unwritten)
+  PCFM_CHECK_ARG(stats == nullptr || pw_path_has_stats(path),
+                 "pointwise_gemm: BatchNorm statistics requested for a shape whose kernel has "
+                 "no statistics epilogue (b=%d cin=%d cout=%d n=%d)", b, cin, cout, n);
+  if (path == PwPath::Stream128) {
     const uint16_t* wl_img = wh + total;
     const long long tiles = (long long)b * ceil_div(n, 32);
     const size_t lds = (size_t)2 * 128 * (Kpad + 8) * sizeof(uint16_t);
@@ -1003,16 +1013,13 @@ static int pw_gemm_launch(const Parts& x, const void* wsplit, const float* bias,
     }
     return check_launch("pointwise_gemm");
   }
-#endif
-#ifndef PCFM_PW_NO256
-  if (Mpad % 256 == 0 && big / 2 >= 2 * kCUs) {
+  if (path == PwPath::Tile256) {
     const dim3 g256(ceil_div(n, 128), Mpad / 256, b);
     hipLaunchKernelGGL(pw_gemm256_kernel, g256, dim3(512), 0, st, x, wh, wh + total, bias,
                        bias_bstride, y, cin, cout, n, Kpad, stats);
     return check_launch("pointwise_gemm");
   }
-#endif
-  if (big >= 2 * kCUs) {
+  if (path == PwPath::Tile128) {
     hipLaunchKernelGGL((pw_gemm_kernel<128, 128>), dim3(ceil_div(n, 128), Mpad / 128, b),
                        dim3(256), 0, st, x, wh, wh + total, bias, bias_bstride, y, cin, cout, n,
                        Kpad);
@@ -1055,7 +1062,8 @@ extern "C" int pcfm_pointwise_gemm(const float* x, const void* wsplit, const flo
 // group): stats float2 [cout][b * ceil(n / 64)] (mean, centred sum of squares);
 // pcfm_pointwise_bnstats_groups() > 0 for the shapes that take this path.
 extern "C" int pcfm_pointwise_bnstats_groups(int b, int cin, int cout, int n) {
-  if (!pw_ok(b, cin, cout, n) || b <= 0 || n <= 0 || !pw_takes_256(b, cin, cout, n)) return 0;
+  if (!pw_ok(b, cin, cout, n) || b <= 0 || n <= 0 || !pw_path_has_stats(pw_path(b, cin, cout, n)))
+    return 0;
   return b * ceil_div(n, 64);
 }
 

@@ -26,3 +26,50 @@ def grid_sample_devox(grid, pts, r):
     out = TF.grid_sample(g, p.reshape(b, 1, 1, -1, 3), mode="bilinear",
                          padding_mode="border", align_corners=True)
     return out.reshape(b, c, -1)
+
+
+# biases of convolutions that feed a BatchNorm: analytically zero gradient, so
+# what the reference stores for them is rounding noise (|g| ~ 1e-9)
+NOISE_BIAS = ("layers.0.bias", "voxel_layers.0.bias", "voxel_layers.3.bias")
+
+
+def grad_errors_full(module, fixture):
+    """pvconv_r8_grads.npz: {param: max |g - g_ref| / max |g_ref|} over every element."""
+    import numpy as np
+    out = {}
+    for n, p in module.named_parameters():
+        ref = fixture[f"grad/{n}"]
+        got = p.grad.detach().cpu().numpy()
+        out[n] = float(np.abs(got - ref).max() / max(float(np.abs(ref).max()), 1e-30))
+    return out
+
+
+def grad_errors_sampled(module, fixture, elements=False):
+    """model_hybrid_c1_perturbed_grads.npz: {param: max |g - g_ref| / max |g_ref|}
+    over the fixture's seeded positions, normalised by the parameter's max
+    |gradient| over all its elements (stored beside the samples).  With
+    `elements`, also the array of every sampled element's normalised error."""
+    import numpy as np
+    names = list(fixture["param_names"])
+    params = dict(module.named_parameters())
+    assert names == list(params), "parameter order differs from the reference's"
+    of, pos, ref, amax = (fixture["param_of"], fixture["flat_pos"], fixture["grad"],
+                          fixture["grad_absmax"])
+    out, el = {}, []
+    for i, n in enumerate(names):
+        sel = of == i
+        g = params[n].grad
+        flat = (g.detach().reshape(-1).cpu().numpy() if g is not None
+                else np.zeros(int(params[n].numel()), np.float32))
+        e = np.abs(flat[pos[sel]] - ref[sel]) / max(float(amax[i]), 1e-30)
+        out[n] = float(e.max())
+        if not n.endswith(NOISE_BIAS):
+            el.append(e)
+    return (out, np.concatenate(el)) if elements else out
+
+
+def worst(errs, skip=NOISE_BIAS):
+    """(max error, its parameter) over the live parameters."""
+    live = {k: v for k, v in errs.items() if not k.endswith(skip)}
+    k = max(live, key=live.get)
+    return live[k], k

@@ -37,10 +37,13 @@ def extract(path: str, workdir: str) -> List[str]:
     or an ELF code object itself), written under `workdir`; their paths."""
     with open(path, "rb") as f:
         head = f.read(64)
+    fat = os.path.join(workdir, os.path.basename(path) + ".fatbin")
     if head[:4] == b"\x7fELF" and b"amdgpu" not in _e_machine_str(path):
-        fat = os.path.join(workdir, os.path.basename(path) + ".fatbin")
         subprocess.run([tool("llvm-objcopy"), "--dump-section", f".hip_fatbin={fat}", path,
                         os.devnull], check=True, capture_output=True, timeout=300)
+    elif head[:4] == b"CCOB" or head.startswith(_BUNDLE):
+        import shutil
+        shutil.copyfile(path, fat)  # a bare (compressed) bundle, e.g. hipBLASLt's .co files
     else:
         return [path]  # already a device code object (.co / .hsaco)
     with open(fat, "rb") as f:
@@ -147,6 +150,36 @@ def kernel_resources(co: str) -> Dict[str, Dict[str, int]]:
             cur[keys[m.group(1)]] = m.group(2)
     flush()
     return out
+
+
+def descriptor_registers(co: str, kernel: str) -> Dict[str, int]:
+    """Registers the hardware allocates per lane, from the kernel descriptor
+    (`<kernel>.kd`): compute_pgm_rsrc1 bits 0-5 = total VGPR+AGPR granules of 8
+    (gfx90a+ unified file), compute_pgm_rsrc3 bits 0-5 = ACCUM_OFFSET / 4 - 1.
+    Hand-assembled kernels (Tensile) report only arch VGPRs in the metadata."""
+    import struct
+    r = subprocess.run([tool("llvm-readelf"), "-S", "-s", "--wide", co], capture_output=True,
+                       text=True, timeout=300, check=True).stdout
+    secs = {}
+    for line in r.splitlines():
+        m = re.match(r"^\s*\[\s*(\d+)\]\s+(\S+)\s+\S+\s+([0-9a-f]+)\s+([0-9a-f]+)", line)
+        if m:
+            secs[int(m.group(1))] = (int(m.group(3), 16), int(m.group(4), 16))
+    addr = ndx = None
+    for line in r.splitlines():
+        f = line.split()
+        if len(f) >= 8 and f[7] == kernel + ".kd":
+            addr, ndx = int(f[1], 16), int(f[6])
+    if addr is None:
+        raise KeyError(kernel)
+    sec_addr, sec_off = secs[ndx]
+    with open(co, "rb") as fh:
+        fh.seek(addr - sec_addr + sec_off)
+        kd = fh.read(64)
+    rsrc3, rsrc1 = struct.unpack_from("<II", kd, 44)
+    total = ((rsrc1 & 0x3F) + 1) * 8
+    accum = ((rsrc3 & 0x3F) + 1) * 4
+    return {"alloc": total, "arch_vgpr": accum, "agpr": total - accum}
 
 
 def waves_per_simd(vgpr: int, agpr: int) -> int:

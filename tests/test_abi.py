@@ -54,3 +54,18 @@ def test_invalid_arguments_rejected_on_host():
     with pytest.raises(_lib.PcfmError, match="workspace"):
         _lib.call("pcfm_chamfer_fwd", None, None, 8, 20000, 20000, None, None, None, None, None,
                   0, None)
+
+
+def test_pointwise_bnstats_request_on_a_path_without_statistics_fails():
+    """The forward GEMM's shape -> kernel choice is one function (pointwise.hip
+    pw_path); only the 256-row tile writes BatchNorm statistics.  A statistics
+    request for a shape that takes another kernel is refused on the host
+    (nothing launched), instead of returning with the stats buffer unwritten."""
+    lib = _lib.load()
+    assert lib.pcfm_pointwise_bnstats_groups(8, 256, 256, 20000) == 8 * 313
+    for shape in ((8, 128, 128, 20000),   # the streaming 128-row form
+                  (1, 256, 256, 512)):    # too few tiles for the 256-row tile
+        assert lib.pcfm_pointwise_bnstats_groups(*shape) == 0
+        rc = lib.pcfm_pointwise_gemm_bnstats(None, None, None, *shape, None, None, None)
+        assert rc == -1, shape
+        assert b"unsupported shape" in lib.pcfm_last_error()

@@ -61,9 +61,15 @@ def test_pvconv_gpu_matches_reference(golden, report, mode):
         loss.backward()
     e_out = _rel_max(out.detach().cpu().numpy(), g["out"])
     e_grad = _rel_max(feats.grad.cpu().numpy(), g["grad_feats"])
-    report(f"pvconv_r8_{mode}", {"out": e_out, "grad_feats": e_grad})
+    # every parameter gradient element by element (pvconv_r8_grads.npz), normalised
+    # by the parameter's max |gradient|; the two conv biases that feed a BatchNorm
+    # have an analytically zero gradient (noise) and are left out
+    from golden_util import grad_errors_full, worst
+    e_pg, w_pg = worst(grad_errors_full(blk, golden("pvconv_r8_grads.npz")))
+    report(f"pvconv_r8_{mode}", {"out": e_out, "grad_feats": e_grad, "param_grads": e_pg,
+                                 "param_grads_worst": w_pg})
     tol = 1e-5 if mode == "exact_fp32" else 1e-4
-    assert e_out < tol and e_grad < tol, (e_out, e_grad)
+    assert e_out < tol and e_grad < tol and e_pg < tol, (e_out, e_grad, e_pg, w_pg)
 
 
 @pytest.mark.parametrize("perturbed", [False, True])
@@ -109,8 +115,36 @@ def test_hybrid_gpu_matches_reference(golden, report, mode, perturbed):
     e_g = float(gdev[live & ~se].max())
     e_se = float(gdev[live & se].max())
     worst = [names[i] for i in np.argsort(-np.where(live, gdev, 0))[:3]]
-    report(f"hybrid_c1{'_perturbed' if perturbed else ''}_{mode}",
-           {"v": e_v, "loss": e_loss, "grad_norms": e_g, "grad_norms_se": e_se, "worst": worst})
+    rep = {"v": e_v, "loss": e_loss, "grad_norms": e_g, "grad_norms_se": e_se, "worst": worst}
+    if perturbed:
+        # elementwise at 64 seeded positions per parameter, normalised by the
+        # parameter's max |gradient| (model_hybrid_c1_perturbed_grads.npz).  The
+        # ContextNet's backward is itself this sensitive: on the CPU path alone, rgb
+        # inputs moved by 1e-6 relative (coordinates untouched) move the gradients
+        # at the stage outputs by 7.5e-4 (stage 2) to 1.5e-2 (stage 0) -- ReLU
+        # masks that flip (profiles/r05_grad_sensitivity.json, tools/
+        # grad_localize.py MODE=sensitivity) -- while the GPU forward differs
+        # from the reference by ~1e-6 (v).  So the bounds are on the
+        # distribution: median, 99th percentile and max over the 10.9 k sampled
+        # elements.  Measured on MI355X (profiles/r05_hybrid_grads_elementwise.json):
+        # exact fp32 2.5e-5 / 1.2e-3 / 1.2e-2, bf16x3 3.3e-4 / 2.0e-2 / 7.3e-2.
+        # The PVConv block test above holds every gradient element to 1e-5 / 1e-4.
+        from golden_util import grad_errors_sampled
+        from golden_util import worst as worst_of
+        per, el = grad_errors_sampled(pf, golden("model_hybrid_c1_perturbed_grads.npz"),
+                                      elements=True)
+        e_el, w_el = worst_of(per)
+        rep.update(grads_elementwise=e_el, grads_elementwise_worst=w_el,
+                   grads_elementwise_quantiles={q: float(np.quantile(el, q))
+                                                for q in (0.5, 0.9, 0.99, 0.999)},
+                   grads_elementwise_over_1e4=int((el > 1e-4).sum()), grads_sampled=int(el.size),
+                   grads_elementwise_top={k: v for k, v in sorted(
+                       per.items(), key=lambda kv: -kv[1]) if not k.endswith(_NOISE_BIAS)})
+    report(f"hybrid_c1{'_perturbed' if perturbed else ''}_{mode}", rep)
+    if perturbed:
+        q = rep["grads_elementwise_quantiles"]
+        med, p99, mx = (1e-4, 5e-3, 5e-2) if mode == "exact_fp32" else (1e-3, 5e-2, 2e-1)
+        assert q[0.5] < med and q[0.99] < p99 and e_el < mx, (q, e_el, w_el)
     if mode == "exact_fp32":
         assert e_v < 1e-5 and e_loss < 1e-5 and e_g < 1e-3 and e_se < 2e-3, (e_v, e_loss, e_g,
                                                                              e_se, worst)

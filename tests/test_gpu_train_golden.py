@@ -12,7 +12,9 @@ random draws (tests/train_replay.py).
     within 1e-5, gradient norms within 2e-2 (measured 6.6e-3 on MI355X, 8.7e-4
     on the CPU path), updates within 5e-2 lr steps.
   * bf16x3 mode (the default fp32 convolutions on the matrix cores, amp off):
-    the measured deviation is reported and bounded at 1e-4.
+    the measured deviation is reported and bounded at 1e-4 (step 1; step 2's
+    AdamW-amplified gradient norms at 5e-2, as in exact fp32 plus the bf16x3
+    rounding -- bounds in the test).
   * the reference's post-epoch Heun sampling with the EMA weights
     (train.py:282-429) replayed through pcfm.sample.heun: 1e-5 exact-fp32,
     1e-4 bf16x3.
@@ -77,6 +79,15 @@ def test_bf16x3_step_deviation(golden, report):
     s = steps[0]
     for k in ("loss_point", "loss_latent", "v", "total_norm"):
         assert s[k] < 1e-4, (k, s)
+    # step 2 starts from AdamW-updated weights: elements whose step-1 gradient was
+    # ~0 moved by ~lr * sign(rounding noise), which the SE MLP's weight gradients
+    # (ds = sum over R^3 voxels of grid * g, cancelling) amplify -- measured on
+    # MI355X: losses <= 3.5e-7, v 4.6e-6, grad norms 3.3e-2 (SE fc.0 weight;
+    # 8.2e-4 in exact fp32), update 8.4e-3 lr steps, EMA 3.8e-5
+    s = steps[1]
+    for k in ("loss_point", "loss_latent", "v", "total_norm"):
+        assert s[k] < 1e-4, (k, s)
+    assert s["grad_norm"] < 5e-2 and s["update"] < 5e-2 and s["ema"] < 1e-3, s
     smp = train_replay.replay_sampling(golden("train_step_c1.npz"), tr)
     report("sampling_golden_bf16x3", smp)
     for k, v in smp.items():

@@ -4,7 +4,8 @@
 # (set -e), so nothing else touches the GPU after a fault, abort or timeout.
 #
 #   tests     full -m gpu suite, parity report  -> gpurun_out/pytest_gpu.log, parity.json
-#   quick     $TESTS (default tests/test_gpu_ops.py) -x -q  -> gpurun_out/pytest_quick.log
+#   quick     $TESTS (default tests/test_gpu_ops.py) -x -q  -> gpurun_out/pytest_quick.log,
+#             parity_quick.json
 #   smoke     __graft_entry__.smoke()           -> gpurun_out/smoke.log
 #   bench     default bench.py (+ $BENCH_ARGS)  -> gpurun_out/bench.json / .err
 #   benchq    bench.py without the CPU / Chamfer legs  -> gpurun_out/benchq.json
@@ -32,7 +33,7 @@ for task in "$@"; do
       PCFM_REPORT=gpurun_out/parity.json timeout -k 10 900 python -u -m pytest tests -m gpu -v \
         --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 ;;
     quick)
-      timeout -k 10 400 python -u -m pytest ${TESTS:-tests/test_gpu_ops.py} -m gpu -x -v \
+      PCFM_REPORT=gpurun_out/parity_quick.json timeout -k 10 400 python -u -m pytest ${TESTS:-tests/test_gpu_ops.py} -m gpu -x -v \
         --timeout 120 --timeout-method thread > gpurun_out/pytest_quick.log 2>&1 ;;
     smoke)
       timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 ;;
