@@ -46,7 +46,8 @@ extern "C" {
  * voxel convolution entry points; 14: voxel-list form of the voxel convolution;
  * 15: the head FiLM backward takes shift and recomputes u; 16: devoxelization
  * self-check entry point; 17: BatchNorm statistics from the pointwise GEMM's
- * epilogue; 18: fused EMD approxmatch + matchcost, SE3d MLP kernels). */
+ * epilogue; 18: fused EMD approxmatch + matchcost, SE3d MLP kernels; 19: PVConv's
+ * second BatchNorm fused with SE3d and the devoxelization). */
 int pcfm_abi_version(void);
 /* Thread-local text of the last non-zero return code. */
 const char* pcfm_last_error(void);
@@ -101,6 +102,18 @@ int pcfm_trilinear_devoxelize_scale_add_fwd(const float* coords, const float* fe
                                             const float* scale, const float* add, int b, int c,
                                             int n, int r, int training, float* out, int* inds,
                                             float* wgts, void* stream);
+
+/* pcfm_trilinear_devoxelize_scale_add_fwd of act(bn(x)): x [b][c][r^3] is a
+ * PVConv's second voxel-conv output, bn_mean / bn_invstd its batch statistics
+ * (pcfm_bn_act_fwd_rowmean), act(t) = t > 0 ? t : slope * t -- BatchNorm3d +
+ * LeakyReLU (pvconv.py:20-30) applied while the rows are staged, so the
+ * activation is never written.  r^3 <= 32768. */
+int pcfm_trilinear_devoxelize_bn_scale_add_fwd(const float* coords, const float* x,
+                                               const float* bn_mean, const float* bn_invstd,
+                                               const float* gamma, const float* beta, float slope,
+                                               const float* scale, const float* add, int b, int c,
+                                               int n, int r, int training, float* out, int* inds,
+                                               float* wgts, void* stream);
 
 /* Diagnosis only (not a reference interface): recompute scale * devox(feat) + add
  * per output in the plainest form and compare bit for bit with `out` (and, when
@@ -531,6 +544,33 @@ int pcfm_bn_act_fwd_split(const float* x, const float* gamma, const float* beta,
                           int s, float eps, float slope, float momentum, float* running_mean,
                           float* running_var, long long* num_batches_tracked, void* ys,
                           float* mean, float* invstd, void* ws, size_t ws_bytes, void* stream);
+
+/* PVConv's second voxel BatchNorm + LeakyReLU fused with SE3d and the
+ * devoxelization (pvconv.py:20-39, se.py:6-17), z = act(bn(x)) never written.
+ * Forward: pcfm_bn_act_fwd_rowmean = the batch statistics (as pcfm_bn_act_fwd,
+ * running stats updated) and rowmean [b][c] = mean over s of z (SE's pooling);
+ * then pcfm_trilinear_devoxelize_bn_scale_add_fwd.
+ * Backward, from g = devox_bwd(dout) [b][c][s]: with dz = se_scale * g + dmv
+ * (dmv [b][c] = SE's pooling gradient dm / s), pcfm_bn_se_bwd_stats writes
+ * rowstats [5][b][c] = (sum z g, sum a g, sum a, sum a g xhat, sum a xhat) per
+ * row, a = act'; rowstats[0] is SE's ds.  pcfm_bn_se_bwd_apply_split then writes
+ * dx as pcfm_bn_act_bwd_split does (conv split operand, dgamma, dbeta,
+ * dbias_in).  c, s multiples of 64.  Deterministic. */
+size_t pcfm_bn_act_fwd_rowmean_workspace_bytes(int b, int c, int s);
+int pcfm_bn_act_fwd_rowmean(const float* x, const float* gamma, const float* beta, int b, int c,
+                            int s, float eps, float slope, float momentum, float* running_mean,
+                            float* running_var, long long* num_batches_tracked, float* rowmean,
+                            float* mean, float* invstd, void* ws, size_t ws_bytes, void* stream);
+size_t pcfm_bn_se_bwd_workspace_bytes(int b, int c, int s);
+int pcfm_bn_se_bwd_stats(const float* g, const float* x, const float* mean, const float* invstd,
+                         const float* gamma, const float* beta, int b, int c, int s, float slope,
+                         float* rowstats, void* ws, size_t ws_bytes, void* stream);
+int pcfm_bn_se_bwd_apply_split(const float* g, const float* x, const float* mean,
+                               const float* invstd, const float* gamma, const float* beta,
+                               const float* se_scale, const float* dmv, const float* rowstats,
+                               int b, int c, int s, float slope, void* dxs, float* dgamma,
+                               float* dbeta, float* dbias_in, void* ws, size_t ws_bytes,
+                               void* stream);
 
 /* pcfm_bn_act_bwd for a voxel convolution's output x [b][c][s] (c, s multiples
  * of 64) whose dx only feeds that convolution's backward: dx is written

@@ -1758,6 +1758,10 @@ __global__ void __launch_bounds__(64)
   if (lane == 0) counts[pair * S + sp] = n;
 }
 
+// (Measured, round 5: issuing the next step's pieces between the MFMA groups of
+// the step, kW3Q / 4 per 16-voxel K-slice behind sched_barriers, instead of in
+// one burst at the step's start: 2.09 vs 2.04 ms/step, same box -- the issue
+// burst is not what holds the MFMA pipe at 0.56 busy.)
 __global__ void __launch_bounds__(kW3Threads)
     conv3_wgrad3_kernel(const uint16_t* __restrict__ xh, const uint16_t* __restrict__ xl,
                         const uint16_t* __restrict__ gh, const uint16_t* __restrict__ gl,
@@ -1813,26 +1817,27 @@ __global__ void __launch_bounds__(kW3Threads)
     // dY pieces: the whole in-step offset (the row is never clamped)
     pofs[q] = ((c >> 5) << 6) + (c & 31) + (img ? kSplitLo : 0) + (isA ? row * 2 * cout : 0);
   }
-  auto issue = [&](int b, int v0, uint8_t* buf) {
+  // piece q of the step at (b, v0) into buf
+  auto issue_q = [&](int q, int b, int v0, uint8_t* buf) {
     const size_t base = (size_t)b * V;
-    const uint16_t* ga = gh + (base + v0) * 2 * cout;  // dY rows of the step
-    const uint16_t* xb = xh + base * 2 * cin;
-    const int g0 = v0 + off - 1;  // X row of the halo's first row
-#pragma unroll
-    for (int q = 0; q < kW3Q; ++q) {
-      const int I = w + (kW3Threads / 64) * q;
-      if (I < 2 * kW3APieces) {
-        const int img = I / kW3APieces, P = I % kW3APieces;
-        glds16_asm(ga + pofs[q],
-                   lds_addr(buf + img * kW3AImg + P * 1024));
-      } else if (I < kW3Pieces) {
-        const int I2 = I - 2 * kW3APieces;
-        const int img = I2 / kW3BPieces, P = I2 % kW3BPieces;
-        const int gv = min(max(g0 + prow_[q], 0), V - 1);  // out-of-volume rows are masked at use
-        glds16_asm(xb + ((size_t)gv * 2 * cin + pofs[q]),
-                   lds_addr(buf + 2 * kW3AImg + img * kW3BImg + P * 1024));
-      }
+    const int I = w + (kW3Threads / 64) * q;
+    if (I < 2 * kW3APieces) {
+      const uint16_t* ga = gh + (base + v0) * 2 * cout;  // dY rows of the step
+      const int img = I / kW3APieces, P = I % kW3APieces;
+      glds16_asm(ga + pofs[q], lds_addr(buf + img * kW3AImg + P * 1024));
+    } else if (I < kW3Pieces) {
+      const uint16_t* xb = xh + base * 2 * cin;
+      const int g0 = v0 + off - 1;  // X row of the halo's first row
+      const int I2 = I - 2 * kW3APieces;
+      const int img = I2 / kW3BPieces, P = I2 % kW3BPieces;
+      const int gv = min(max(g0 + prow_[q], 0), V - 1);  // out-of-volume rows are masked at use
+      glds16_asm(xb + ((size_t)gv * 2 * cin + pofs[q]),
+                 lds_addr(buf + 2 * kW3AImg + img * kW3BImg + P * 1024));
     }
+  };
+  auto issue = [&](int b, int v0, uint8_t* buf) {
+#pragma unroll
+    for (int q = 0; q < kW3Q; ++q) issue_q(q, b, v0, buf);
   };
 
   f32x16 acc[2][2];
@@ -1852,11 +1857,12 @@ __global__ void __launch_bounds__(kW3Threads)
     __builtin_amdgcn_s_barrier();  // step st landed everywhere; step st-1 reads done
     const uint8_t* cur = lds + (st & 1) * kW3Buf;
     const int v0 = (cnext % cpb) * kWV;
+    const bool more = st + 1 < nst;
+    if (more) cnext = chunk_of(st + 1);
+    const int nb = cnext / cpb, nv0 = (cnext % cpb) * kWV;
+    uint8_t* nbuf = lds + ((st + 1) & 1) * kW3Buf;
 #ifndef PCFM_EXP_WG_NOLOAD
-    if (st + 1 < nst) {
-      cnext = chunk_of(st + 1);
-      issue(cnext / cpb, (cnext % cpb) * kWV, lds + ((st + 1) & 1) * kW3Buf);
-    }
+    if (more) issue(nb, nv0, nbuf);
 #endif
     const uint8_t* iAh = cur;
     const uint8_t* iAl = cur + kW3AImg;

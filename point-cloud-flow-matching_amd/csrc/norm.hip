@@ -13,6 +13,8 @@
 // 8 passes.  Partial sums are per (channel, part) block and combined in a
 // fixed order: deterministic.  The forward sums are shifted by the channel's
 // first element (sum (x - K), sum (x - K)^2) against cancellation.
+#include <algorithm>
+
 #include "pcfm_common.hpp"
 
 namespace pcfm {
@@ -612,6 +614,221 @@ __global__ void __launch_bounds__(256)
 }
 
 // ---------------------------------------------------------------------------
+// PVConv's second voxel BatchNorm + LeakyReLU fused with SE3d and the
+// devoxelization (pvconv.py:20-39, se.py:6-17): z = act(bn(x)) is never
+// written.  Forward: the batch statistics, then ONE pass computing the SE
+// pooling m[b][c] = mean_v z (bn_act_rowsum_kernel); the devoxelization
+// gather applies bn + act to the rows while staging them (rows.hpp RowBn).
+// Backward from g = devox_bwd(dout): dz = s[b][c] g + dmv[b][c] (SE's scale and
+// the pooling's gradient dm / V), so every sum BatchNorm's backward needs is
+// linear in (s, dmv) -- per (b, c) row, with a = act'(bn(x)), xh = xhat:
+//   ds = sum z g,  A = sum a g,  N = sum a,  AX = sum a g xh,  NX = sum a xh
+//   sum a dz = s A + dmv N,   sum a dz xh = s AX + dmv NX
+// ONE pass over (g, x) gives all five (bn_se_bwd_stats_kernel); the SE MLP's
+// backward turns ds into dmv; the apply pass writes dx as the conv's split
+// operand (bn_se_bwd_apply_split_kernel).  The SE rows_dot passes, the
+// rows_affine pass over g and the separate backward statistics pass are gone.
+// ---------------------------------------------------------------------------
+
+// grid (bn_apply_blocks(S), B * C): rowpart[row][bx] = sum over the block's
+// elements of act(bn(x)); thread 0 derives the channel statistics from the
+// partials (block bx == 0 of the first C rows publishes them, as the apply).
+__global__ void __launch_bounds__(256)
+    bn_act_rowsum_kernel(const float* __restrict__ x, BnFwdFin fin, float* __restrict__ mean,
+                         float* __restrict__ invstd, const float* __restrict__ gamma,
+                         const float* __restrict__ beta, int C, int S4, float slope,
+                         float* __restrict__ rowpart) {
+  __shared__ float sh[8];
+  __shared__ float st[2];
+  const unsigned row = blockIdx.y, bx = blockIdx.x;
+  const int c = (int)(row % C);
+  if (threadIdx.x == 0) {
+    float m, is, var;
+    double n;
+    fin.get(x, c, m, is, var, n);
+    if (bx == 0 && row < (unsigned)C) fin.publish(c, m, is, var, n, mean, invstd);
+    st[0] = m;
+    st[1] = is;
+  }
+  const float g = gamma[c], bt = beta[c];
+  const float4* __restrict__ x4 = reinterpret_cast<const float4*>(x) + (size_t)row * S4;
+  const int s0 = bx * 256 * kApplyU + threadIdx.x;
+  float4 v[kApplyU];
+#pragma unroll
+  for (int u = 0; u < kApplyU; ++u)
+    if (s0 + u * 256 < S4) v[u] = x4[s0 + u * 256];
+  __syncthreads();
+  const float m = st[0], is = st[1];
+  float sum = 0.0f;
+#pragma unroll
+  for (int u = 0; u < kApplyU; ++u) {
+    if (s0 + u * 256 >= S4) break;
+    sum += (act(__builtin_fmaf((v[u].x - m) * is, g, bt), slope) +
+            act(__builtin_fmaf((v[u].y - m) * is, g, bt), slope)) +
+           (act(__builtin_fmaf((v[u].z - m) * is, g, bt), slope) +
+            act(__builtin_fmaf((v[u].w - m) * is, g, bt), slope));
+  }
+  float z = 0.0f;
+  block_sum2(sum, z, sh);
+  if (threadIdx.x == 0) rowpart[(size_t)row * gridDim.x + bx] = sum;
+}
+
+// one thread per row: out[row] = scale * sum of its nblk partials, in order
+__global__ void __launch_bounds__(256)
+    rowpart_sum_kernel(const float* __restrict__ rowpart, int rows, int nblk, float scale,
+                       float* __restrict__ out) {
+  const int r = blockIdx.x * 256 + threadIdx.x;
+  if (r >= rows) return;
+  const float* __restrict__ p = rowpart + (size_t)r * nblk;
+  float s = 0.0f;
+  for (int k = 0; k < nblk; ++k) s += p[k];
+  out[r] = s * scale;
+}
+
+// grid (PS, B * C), PS = bn_parts(B) / B blocks per row:
+// part[(row * PS + ps) * 5 + k] = the five sums above over the block's range.
+constexpr int kSeSums = 5;
+__global__ void __launch_bounds__(256)
+    bn_se_bwd_stats_kernel(const float* __restrict__ g, const float* __restrict__ x,
+                           const float* __restrict__ mean, const float* __restrict__ invstd,
+                           const float* __restrict__ gamma, const float* __restrict__ beta, int C,
+                           int S, float slope, float* __restrict__ part) {
+  __shared__ float sh[8 * kSeSums];
+  const unsigned row = blockIdx.y;
+  const int c = (int)(row % C), ps = blockIdx.x, PS = gridDim.x;
+  const int S4 = S / 4;
+  int s0, s1;
+  part_range(S4, ps, PS, s0, s1);
+  const float m = mean[c], is = invstd[c], gm = gamma[c], bt = beta[c];
+  const float4* __restrict__ x4 = reinterpret_cast<const float4*>(x) + (size_t)row * S4;
+  const float4* __restrict__ g4 = reinterpret_cast<const float4*>(g) + (size_t)row * S4;
+  float acc[kSeSums] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f};  // ds, A, N, AX, NX
+  auto add = [&](const float4 v, const float4 d) {
+    const float xv[4] = {v.x, v.y, v.z, v.w}, dv[4] = {d.x, d.y, d.z, d.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float xh = (xv[e] - m) * is;
+      const float t = __builtin_fmaf(xh, gm, bt);
+      const float a = t > 0.0f ? 1.0f : slope;
+      const float z = t > 0.0f ? t : (slope == 0.0f ? 0.0f : t * slope);
+      const float ag = a * dv[e];
+      acc[0] = __builtin_fmaf(z, dv[e], acc[0]);
+      acc[1] += ag;
+      acc[2] += a;
+      acc[3] = __builtin_fmaf(ag, xh, acc[3]);
+      acc[4] = __builtin_fmaf(a, xh, acc[4]);
+    }
+  };
+  int s4 = s0 + threadIdx.x;
+  for (; s4 + (kBnUnroll - 1) * 256 < s1; s4 += kBnUnroll * 256) {
+    float4 v[kBnUnroll], d[kBnUnroll];
+#pragma unroll
+    for (int u = 0; u < kBnUnroll; ++u) {
+      v[u] = x4[s4 + u * 256];
+      d[u] = g4[s4 + u * 256];
+    }
+#pragma unroll
+    for (int u = 0; u < kBnUnroll; ++u) add(v[u], d[u]);
+  }
+  for (; s4 < s1; s4 += 256) add(x4[s4], g4[s4]);
+  // block sum of the five values: xor tree per wave, then the 4 waves in order
+#pragma unroll
+  for (int k = 0; k < kSeSums; ++k)
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) acc[k] += __shfl_xor(acc[k], off, 64);
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (lane == 0)
+#pragma unroll
+    for (int k = 0; k < kSeSums; ++k) sh[w * kSeSums + k] = acc[k];
+  __syncthreads();
+  if (threadIdx.x < kSeSums) {
+    const int k = threadIdx.x;
+    part[((size_t)row * PS + ps) * kSeSums + k] =
+        ((sh[k] + sh[kSeSums + k]) + sh[2 * kSeSums + k]) + sh[3 * kSeSums + k];
+  }
+}
+
+// one thread per (row, sum): rowstats[k][row] = sum over the row's PS parts, in order
+__global__ void __launch_bounds__(256)
+    bn_se_rowstats_kernel(const float* __restrict__ part, int rows, int PS,
+                          float* __restrict__ rowstats) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= rows * kSeSums) return;
+  const int row = i / kSeSums, k = i - row * kSeSums;
+  const float* __restrict__ p = part + (size_t)row * PS * kSeSums + k;
+  float s = 0.0f;
+  for (int q = 0; q < PS; ++q) s += p[(size_t)q * kSeSums];
+  rowstats[(size_t)k * rows + row] = s;
+}
+
+// bn_bwd_apply_split_kernel for dz = s[b][c] g + dmv[b][c]; the per-channel
+// sums from rowstats [5][B][C] (summed over b in order).
+__global__ void __launch_bounds__(256)
+    bn_se_bwd_apply_split_kernel(const float* __restrict__ g, const float* __restrict__ x,
+                                 const float* __restrict__ mean, const float* __restrict__ invstd,
+                                 const float* __restrict__ gamma, const float* __restrict__ beta,
+                                 const float* __restrict__ se_s, const float* __restrict__ dmv,
+                                 const float* __restrict__ rowstats, int B,
+                                 float* __restrict__ dgamma, float* __restrict__ dbeta, int C,
+                                 int S, float inv_n, float slope, uint16_t* __restrict__ dxh,
+                                 uint16_t* __restrict__ dxl, float* __restrict__ rowpart) {
+  __shared__ float tile[64][65];
+  __shared__ float st_g[64], st_gx[64], st_s[64], st_t[64];
+  const unsigned bx = bn_rev(blockIdx.x, gridDim.x);
+  const int v0 = bx * 64, c0 = blockIdx.y * 64, b = bn_rev(blockIdx.z, gridDim.z);
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+  if (t < 64) {
+    const int c = c0 + t;
+    const size_t BC = (size_t)B * C;
+    float sg = 0.0f, sgx = 0.0f;
+    for (int bb = 0; bb < B; ++bb) {
+      const size_t r = (size_t)bb * C + c;
+      const float sv = se_s[r], tv = dmv[r];
+      sg += __builtin_fmaf(sv, rowstats[BC + r], tv * rowstats[2 * BC + r]);
+      sgx += __builtin_fmaf(sv, rowstats[3 * BC + r], tv * rowstats[4 * BC + r]);
+    }
+    st_g[t] = sg;
+    st_gx[t] = sgx;
+    st_s[t] = se_s[(size_t)b * C + c];
+    st_t[t] = dmv[(size_t)b * C + c];
+    if (bx == 0 && b == 0) {
+      dbeta[c] = sg;
+      dgamma[c] = sgx;
+    }
+  }
+  __syncthreads();
+  const size_t rbase = ((size_t)b * C + c0) * S + v0;
+  float xv[16], dv[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const size_t o = rbase + (size_t)(4 * i + w) * S + lane;
+    xv[i] = x[o];
+    dv[i] = g[o];
+  }
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int cl = 4 * i + w, c = c0 + cl;
+    const float m = mean[c], is = invstd[c], gm = gamma[c], bt = beta[c];
+    const float mg = st_g[cl] * inv_n, mgx = st_gx[cl] * inv_n, k = gm * is;
+    const float xh = (xv[i] - m) * is;
+    const float dz = __builtin_fmaf(st_s[cl], dv[i], st_t[cl]);  // rows_affine's expression
+    const float gg = __builtin_fmaf(xh, gm, bt) > 0.0f ? dz : dz * slope;
+    tile[cl][lane] = k * ((gg - mg) - xh * mgx);
+  }
+  __syncthreads();
+  tile_store_split(tile, b, C, S, v0, c0, t, dxh, dxl);
+  if (rowpart != nullptr) {
+    const int c = t >> 2, vq = (t & 3) * 16;
+    float sum = 0.0f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) sum += tile[c][vq + q];
+    sum += __shfl_xor(sum, 1, 64);
+    sum += __shfl_xor(sum, 2, 64);
+    if ((t & 3) == 0) rowpart[((size_t)b * C + c0 + c) * (S / 64) + bx] = sum;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // GroupNorm + FiLM + residual of the hybrid backbone's PV blocks
 // (reference models.py:322-346 _FiLM1d with GroupNorm, :349-368 _PVBlock):
 //   out = x + (GN(x) * (1 + gamma[b]) + beta[b])
@@ -971,6 +1188,95 @@ extern "C" int pcfm_bn_act_fwd_split(const float* x, const float* gamma, const f
                      fin, mean, invstd, gamma, beta, c, s, slope, yh,
                      yh + kSplitLo);
   return check_launch("bn_act_fwd_split");
+}
+
+// --- PVConv's BN3d + LeakyReLU fused with SE3d and the devoxelization ------
+static int se_stat_parts(int b, int c, int s) {  // blocks per (b, c) row of the statistics pass
+  const long long rows = (long long)b * c;
+  const int by_len = std::max(1, ceil_div(s / 4, 1024));
+  const int by_grid = (int)std::max(1LL, (2048 + rows - 1) / rows);
+  return std::min(by_len, by_grid);
+}
+
+extern "C" size_t pcfm_bn_act_fwd_rowmean_workspace_bytes(int b, int c, int s) {
+  if (!bn_ok(b, c, s)) return 0;
+  return pcfm_bn_workspace_bytes(b, c, s) + (size_t)b * c * bn_apply_blocks(s) * sizeof(float);
+}
+
+extern "C" int pcfm_bn_act_fwd_rowmean(const float* x, const float* gamma, const float* beta,
+                                       int b, int c, int s, float eps, float slope,
+                                       float momentum, float* running_mean, float* running_var,
+                                       long long* num_batches_tracked, float* rowmean,
+                                       float* mean, float* invstd, void* ws, size_t ws_bytes,
+                                       void* stream) {
+  PCFM_CHECK_ARG(bn_ok(b, c, s), "bn_act_fwd_rowmean: bad shape b=%d c=%d s=%d", b, c, s);
+  PCFM_CHECK_ARG(ws_bytes >= pcfm_bn_act_fwd_rowmean_workspace_bytes(b, c, s),
+                 "bn_act_fwd_rowmean: workspace too small");
+  PCFM_CHECK_ARG((running_mean == nullptr) == (running_var == nullptr),
+                 "bn_act_fwd_rowmean: running_mean and running_var must both be given or both NULL");
+  hipStream_t st = (hipStream_t)stream;
+  float* part = (float*)ws;
+  float* rowpart = part + pcfm_bn_workspace_bytes(b, c, s) / sizeof(float);
+  hipLaunchKernelGGL(bn_stats_kernel, dim3(c, bn_parts(b)), dim3(256), 0, st, x, b, c, s, part);
+  const BnFwdFin fin{part,         b,           s,
+                     bn_parts(b),  eps,         momentum,
+                     running_mean, running_var, num_batches_tracked};
+  const int nblk = bn_apply_blocks(s);
+  hipLaunchKernelGGL(bn_act_rowsum_kernel, dim3(nblk, b * c), dim3(256), 0, st, x, fin, mean,
+                     invstd, gamma, beta, c, s / 4, slope, rowpart);
+  hipLaunchKernelGGL(rowpart_sum_kernel, dim3(ceil_div(b * c, 256)), dim3(256), 0, st,
+                     (const float*)rowpart, b * c, nblk, (float)(1.0 / (double)s), rowmean);
+  return check_launch("bn_act_fwd_rowmean");
+}
+
+extern "C" size_t pcfm_bn_se_bwd_workspace_bytes(int b, int c, int s) {
+  if (!bn_ok(b, c, s) || c % 64 != 0 || s % 64 != 0) return 0;
+  return ((size_t)b * c * se_stat_parts(b, c, s) * kSeSums + (size_t)b * c * (s / 64)) *
+         sizeof(float);
+}
+
+extern "C" int pcfm_bn_se_bwd_stats(const float* g, const float* x, const float* mean,
+                                    const float* invstd, const float* gamma, const float* beta,
+                                    int b, int c, int s, float slope, float* rowstats, void* ws,
+                                    size_t ws_bytes, void* stream) {
+  PCFM_CHECK_ARG(bn_ok(b, c, s) && c % 64 == 0 && s % 64 == 0,
+                 "bn_se_bwd_stats: bad shape b=%d c=%d s=%d (c, s multiples of 64)", b, c, s);
+  PCFM_CHECK_ARG(ws_bytes >= pcfm_bn_se_bwd_workspace_bytes(b, c, s),
+                 "bn_se_bwd_stats: workspace too small");
+  hipStream_t st = (hipStream_t)stream;
+  const int PS = se_stat_parts(b, c, s);
+  float* part = (float*)ws;
+  hipLaunchKernelGGL(bn_se_bwd_stats_kernel, dim3(PS, b * c), dim3(256), 0, st, g, x, mean,
+                     invstd, gamma, beta, c, s, slope, part);
+  hipLaunchKernelGGL(bn_se_rowstats_kernel, dim3(ceil_div(b * c * kSeSums, 256)), dim3(256), 0,
+                     st, (const float*)part, b * c, PS, rowstats);
+  return check_launch("bn_se_bwd_stats");
+}
+
+extern "C" int pcfm_bn_se_bwd_apply_split(const float* g, const float* x, const float* mean,
+                                          const float* invstd, const float* gamma,
+                                          const float* beta, const float* se_scale,
+                                          const float* dmv, const float* rowstats, int b, int c,
+                                          int s, float slope, void* dxs, float* dgamma,
+                                          float* dbeta, float* dbias_in, void* ws,
+                                          size_t ws_bytes, void* stream) {
+  PCFM_CHECK_ARG(bn_ok(b, c, s) && c % 64 == 0 && s % 64 == 0 && (long long)b < 65536,
+                 "bn_se_bwd_apply_split: bad shape b=%d c=%d s=%d (c, s multiples of 64)", b, c,
+                 s);
+  PCFM_CHECK_ARG(ws_bytes >= pcfm_bn_se_bwd_workspace_bytes(b, c, s),
+                 "bn_se_bwd_apply_split: workspace too small");
+  hipStream_t st = (hipStream_t)stream;
+  float* rowpart = dbias_in != nullptr
+                       ? (float*)ws + (size_t)b * c * se_stat_parts(b, c, s) * kSeSums
+                       : nullptr;
+  uint16_t* dxh = (uint16_t*)dxs;
+  hipLaunchKernelGGL(bn_se_bwd_apply_split_kernel, dim3(s / 64, c / 64, b), dim3(256), 0, st, g,
+                     x, mean, invstd, gamma, beta, se_scale, dmv, rowstats, b, dgamma, dbeta, c,
+                     s, (float)(1.0 / ((double)b * s)), slope, dxh, dxh + kSplitLo, rowpart);
+  if (dbias_in != nullptr)
+    hipLaunchKernelGGL(bn_bias_finalize_block_kernel, dim3(c), dim3(256), 0, st,
+                       (const float*)rowpart, b, c, s / 64, dbias_in);
+  return check_launch("bn_se_bwd_apply_split");
 }
 
 extern "C" size_t pcfm_bn_act_bwd_split_workspace_bytes(int b, int c, int s) {

@@ -175,12 +175,38 @@ struct GatherEpi {
   const float* add = nullptr;    // [B][C][NI]
 };
 
+// Optional transform of the rows as they are staged: row value v of channel c
+// becomes act(fma((v - mean[c]) * invstd[c], gamma[c], beta[c])) with act(t) =
+// t > 0 ? t : slope * t -- PVConv's BatchNorm3d + LeakyReLU applied to the conv
+// output while the devoxelization stages it, exactly as bn_act_apply_kernel
+// computes it (norm.hip), so the activation is never written.
+struct RowBn {
+  const float* mean = nullptr;  // nullptr: rows staged as they are
+  const float* invstd = nullptr;
+  const float* gamma = nullptr;
+  const float* beta = nullptr;
+  float slope = 0.0f;
+};
+struct RowBnC {  // one channel's constants
+  float m, is, g, bt, slope;
+  __device__ __forceinline__ float operator()(float v) const {
+    const float t = __builtin_fmaf((v - m) * is, g, bt);
+    return t > 0.0f ? t : (slope == 0.0f ? 0.0f : t * slope);
+  }
+  __device__ __forceinline__ float4 operator()(float4 v) const {
+    return make_float4((*this)(v.x), (*this)(v.y), (*this)(v.z), (*this)(v.w));
+  }
+};
+__device__ __forceinline__ RowBnC row_bn_at(const RowBn& bn, int c) {
+  return RowBnC{bn.mean[c], bn.invstd[c], bn.gamma[c], bn.beta[c], bn.slope};
+}
+
 // grid = (item splits, channel groups, b).  USE_LDS stages the block's
 // `cpb` rows (cpb * V floats) in LDS first.
 template <class Prov, bool USE_LDS>
 __global__ void __launch_bounds__(1024)
     gather_rows_kernel(const float* __restrict__ rows, float* __restrict__ out, int C, int V,
-                       int NI, int cpb, Prov prov, GatherEpi epi) {
+                       int NI, int cpb, Prov prov, GatherEpi epi, RowBn bn) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   constexpr int T = Prov::TAPS;
   const int b = blockIdx.z;
@@ -189,7 +215,10 @@ __global__ void __launch_bounds__(1024)
   const float* __restrict__ rb = rows + ((size_t)b * C + c0) * V;
   if constexpr (USE_LDS) {
     const int total = nc * V;
-    if ((((uintptr_t)rb) & 15) == 0 && (total & 3) == 0) {
+    if (bn.mean != nullptr) {  // block-uniform
+      for (int e = threadIdx.x; e < total; e += blockDim.x)
+        lds[e] = row_bn_at(bn, c0 + e / V)(rb[e]);
+    } else if ((((uintptr_t)rb) & 15) == 0 && (total & 3) == 0) {
       const float4* __restrict__ s4 = reinterpret_cast<const float4*>(rb);
       float4* d4 = reinterpret_cast<float4*>(lds);
       for (int e = threadIdx.x; e < (total >> 2); e += blockDim.x) d4[e] = s4[e];
@@ -264,7 +293,7 @@ __global__ void __launch_bounds__(1024)
 template <class Prov, int IPT>
 __global__ void __launch_bounds__(1024)
     gather_rows1_kernel(const float* __restrict__ rows, float* __restrict__ out, int C, int V,
-                        int NI, Prov prov, GatherEpi epi) {
+                        int NI, Prov prov, GatherEpi epi, RowBn bn) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   constexpr int T = Prov::TAPS;
   const int b = blockIdx.z;
@@ -273,7 +302,15 @@ __global__ void __launch_bounds__(1024)
   if ((((uintptr_t)rb) & 15) == 0 && (V & 3) == 0) {
     const float4* __restrict__ s4 = reinterpret_cast<const float4*>(rb);
     float4* d4 = reinterpret_cast<float4*>(lds);
-    for (int e = threadIdx.x; e < (V >> 2); e += blockDim.x) d4[e] = s4[e];
+    if (bn.mean != nullptr) {  // block-uniform
+      const RowBnC f = row_bn_at(bn, c0);
+      for (int e = threadIdx.x; e < (V >> 2); e += blockDim.x) d4[e] = f(s4[e]);
+    } else {
+      for (int e = threadIdx.x; e < (V >> 2); e += blockDim.x) d4[e] = s4[e];
+    }
+  } else if (bn.mean != nullptr) {
+    const RowBnC f = row_bn_at(bn, c0);
+    for (int e = threadIdx.x; e < V; e += blockDim.x) lds[e] = f(rb[e]);
   } else {
     for (int e = threadIdx.x; e < V; e += blockDim.x) lds[e] = rb[e];
   }
@@ -342,15 +379,24 @@ __device__ __forceinline__ float4 tap_sum4(const float4* __restrict__ s, const i
 template <class Prov>
 __global__ void __launch_bounds__(512)
     gather_rows4_kernel(const float* __restrict__ rows, float* __restrict__ out, int C, int V,
-                        int NI, Prov prov, GatherEpi epi) {
+                        int NI, Prov prov, GatherEpi epi, RowBn bn) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   float4* lds4 = reinterpret_cast<float4*>(lds);
   constexpr int T = Prov::TAPS;
   const int b = blockIdx.z;
   const int c0 = blockIdx.y * 4;
   const float* __restrict__ rb = rows + ((size_t)b * C + c0) * V;
-  for (int v = threadIdx.x; v < V; v += blockDim.x)
-    lds4[v] = make_float4(rb[v], rb[(size_t)V + v], rb[2 * (size_t)V + v], rb[3 * (size_t)V + v]);
+  if (bn.mean != nullptr) {  // block-uniform
+    const RowBnC f0 = row_bn_at(bn, c0), f1 = row_bn_at(bn, c0 + 1), f2 = row_bn_at(bn, c0 + 2),
+                 f3 = row_bn_at(bn, c0 + 3);
+    for (int v = threadIdx.x; v < V; v += blockDim.x)
+      lds4[v] = make_float4(f0(rb[v]), f1(rb[(size_t)V + v]), f2(rb[2 * (size_t)V + v]),
+                            f3(rb[3 * (size_t)V + v]));
+  } else {
+    for (int v = threadIdx.x; v < V; v += blockDim.x)
+      lds4[v] =
+          make_float4(rb[v], rb[(size_t)V + v], rb[2 * (size_t)V + v], rb[3 * (size_t)V + v]);
+  }
   __syncthreads();
   float* __restrict__ ob = out + ((size_t)b * C + c0) * NI;
   const float* __restrict__ ab = epi.add != nullptr ? epi.add + ((size_t)b * C + c0) * NI : nullptr;
@@ -459,7 +505,8 @@ inline bool prov_has_side_outputs(const ProvDevox& p) { return p.inds_out != nul
 
 template <class Prov>
 inline int launch_gather(const float* rows, float* out, int B, int C, int V, int NI, Prov prov,
-                         hipStream_t st, const char* what, GatherEpi epi = GatherEpi{}) {
+                         hipStream_t st, const char* what, GatherEpi epi = GatherEpi{},
+                         RowBn bn = RowBn{}) {
   if (B == 0 || NI == 0) return PCFM_OK;
   if (V == 0 && C > 0 && epi.add == nullptr) {  // empty rows: every tap is out of range -> zeros
     hipError_t e = hipMemsetAsync(out, 0, (size_t)B * C * NI * sizeof(float), st);
@@ -475,7 +522,7 @@ inline int launch_gather(const float* rows, float* out, int B, int C, int V, int
     int e = allow_big_lds((const void*)gather_rows4_kernel<Prov>);
     if (e) return e;
     hipLaunchKernelGGL((gather_rows4_kernel<Prov>), grid, dim3(512), p.lds_bytes, st, rows, out, C,
-                       V, NI, prov, epi);
+                       V, NI, prov, epi, bn);
   } else if (p.use_lds && p.cpb == 1 && p.threads == 1024 && gather1_ipt() > 1) {
     int e = allow_big_lds((const void*)gather_rows1_kernel<Prov, 2>);
     if (e) return e;
@@ -483,18 +530,22 @@ inline int launch_gather(const float* rows, float* out, int B, int C, int V, int
     if (e) return e;
     if (gather1_ipt() >= 4)
       hipLaunchKernelGGL((gather_rows1_kernel<Prov, 4>), grid, dim3(1024), p.lds_bytes, st, rows,
-                         out, C, V, NI, prov, epi);
+                         out, C, V, NI, prov, epi, bn);
     else
       hipLaunchKernelGGL((gather_rows1_kernel<Prov, 2>), grid, dim3(1024), p.lds_bytes, st, rows,
-                         out, C, V, NI, prov, epi);
+                         out, C, V, NI, prov, epi, bn);
   } else if (p.use_lds) {
     int e = allow_big_lds((const void*)gather_rows_kernel<Prov, true>);
     if (e) return e;
     hipLaunchKernelGGL((gather_rows_kernel<Prov, true>), grid, dim3(p.threads), p.lds_bytes, st,
-                       rows, out, C, V, NI, p.cpb, prov, epi);
+                       rows, out, C, V, NI, p.cpb, prov, epi, bn);
   } else {
+    if (bn.mean != nullptr) {  // the row transform needs the staged rows
+      set_error("%s: a row transform needs rows that fit LDS (V = %d)", what, V);
+      return PCFM_EINVAL;
+    }
     hipLaunchKernelGGL((gather_rows_kernel<Prov, false>), grid, dim3(p.threads), 0, st, rows,
-                       out, C, V, NI, p.cpb, prov, epi);
+                       out, C, V, NI, p.cpb, prov, epi, bn);
   }
   return check_launch(what);
 }

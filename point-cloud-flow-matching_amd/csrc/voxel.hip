@@ -269,6 +269,36 @@ extern "C" int pcfm_trilinear_devoxelize_scale_add_fwd(const float* coords, cons
                        "trilinear_devoxelize_scale_add_fwd", epi);
 }
 
+// scale[b, c] * devox(act(bn(x)))[b, c, i] + add[b, c, i]: PVConv's second
+// BatchNorm3d + LeakyReLU applied to the conv output x as the gather stages its
+// rows (rows.hpp RowBn), so the activation is never written (norm.hip,
+// pcfm_bn_act_fwd_rowmean).
+extern "C" int pcfm_trilinear_devoxelize_bn_scale_add_fwd(
+    const float* coords, const float* x, const float* bn_mean, const float* bn_invstd,
+    const float* gamma, const float* beta, float slope, const float* scale, const float* add,
+    int b, int c, int n, int r, int training, float* out, int* inds, float* wgts, void* stream) {
+  int s = 0;
+  PCFM_CHECK_ARG(b >= 0 && c >= 0 && n >= 0, "trilinear_devoxelize_bn_scale_add_fwd: negative size");
+  PCFM_CHECK_ARG(cube_fits(r, &s), "trilinear_devoxelize_bn_scale_add_fwd: bad resolution %d", r);
+  PCFM_CHECK_ARG(bn_mean != nullptr && bn_invstd != nullptr && gamma != nullptr && beta != nullptr,
+                 "trilinear_devoxelize_bn_scale_add_fwd: BatchNorm operands missing");
+  PCFM_CHECK_ARG(!training || (long long)b * n == 0 || (inds != nullptr && wgts != nullptr),
+                 "trilinear_devoxelize_bn_scale_add_fwd: training needs inds/wgts buffers");
+  PCFM_CHECK_ARG(s <= 32 * 1024, "trilinear_devoxelize_bn_scale_add_fwd: r^3 = %d > 32768", s);
+  ProvDevox prov{coords, n, r, r * r, s, training ? inds : nullptr, training ? wgts : nullptr};
+  GatherEpi epi;
+  epi.scale = scale;
+  epi.add = add;
+  RowBn bn;
+  bn.mean = bn_mean;
+  bn.invstd = bn_invstd;
+  bn.gamma = gamma;
+  bn.beta = beta;
+  bn.slope = slope;
+  return launch_gather(x, out, b, c, s, n, prov, (hipStream_t)stream,
+                       "trilinear_devoxelize_bn_scale_add_fwd", epi, bn);
+}
+
 // ---------------------------------------------------------------------------
 // Segment plans (include/pcfm.h): the scatter's sort + work units built once
 // and applied to every feature tensor over the same points.

@@ -127,6 +127,44 @@ class _Conv3dBnAct(torch.autograd.Function):
         return dx, dw, db, dgamma, dbeta, None, None, None, None, None, None
 
 
+def _pair_head(x, w1, b1, g1, bt1, rm1, rv1, nbt1, w2, b2, eps1, mom1, slope1, occ):
+    """Conv1 -> BN1 + act (written only as Conv2's split input) -> Conv2:
+    -> (xs, y1, m1, is1, z1s, y2), y2 the second conv's pre-BatchNorm output."""
+    from pcfm import ops
+    bsz, cin, r = x.shape[0], x.shape[1], x.shape[2]
+    cmid, cout = w1.shape[0], w2.shape[0]
+    xs = ops.conv3d_split(x)
+    masks, vl, cnt = (occ.masks, occ.lists, occ.cnt) if occ is not None else (None, None, None)
+    y1 = ops.conv3d_igemm_split(xs, ops.conv3d_prep_weight(w1, False), b1, bsz, cin, cmid,
+                                r, "conv3d_fwd", occ=masks, occ_mode=1, vlists=vl, cnt=cnt)
+    z1s, m1, is1 = ops.bn_act_forward_split(y1, g1, bt1, eps1, slope1, mom1, rm1, rv1, nbt1)
+    y2 = ops.conv3d_igemm_split(z1s, ops.conv3d_prep_weight(w2, False), b2, bsz, cmid, cout,
+                                r, "conv3d_fwd")
+    return xs, y1, m1, is1, z1s, y2
+
+
+def _pair_tail(gys2, xs, w1, y1, g1, bt1, m1, is1, z1s, w2, slope1, has_bias1, dims, occ,
+               needs_dx):
+    """Backward of _pair_head from split(d y2): -> (dx, dw1, db1, dg1, dbt1, dw2)."""
+    from pcfm import ops
+    bsz, cin, cmid, cout, r = dims
+    dz1 = ops.conv3d_igemm_split(gys2, ops.conv3d_prep_weight(w2, True), None, bsz, cout,
+                                 cmid, r, "conv3d_bwd_data")
+    dw2 = ops.conv3d_wgrad_split(z1s, gys2, bsz, cmid, cout, r)
+    del gys2
+    gys1, dg1, dbt1, db1 = ops.bn_act_backward_split(dz1, y1, g1, bt1, m1, is1, slope1,
+                                                     want_dbias_in=has_bias1)
+    del dz1
+    dx = None
+    masks, vl, cnt = (occ.masks, occ.lists, occ.cnt) if occ is not None else (None, None, None)
+    if needs_dx:
+        dx = ops.conv3d_igemm_split(gys1, ops.conv3d_prep_weight(w1, True), None, bsz, cmid,
+                                    cin, r, "conv3d_bwd_data", occ=masks, occ_mode=2,
+                                    vlists=vl, cnt=cnt)
+    dw1 = ops.conv3d_wgrad_split(xs, gys1, bsz, cin, cmid, r, occ=masks)
+    return dx, dw1, db1, dg1, dbt1, dw2
+
+
 class _Conv3dBnActPair(torch.autograd.Function):
     """PVConv's two voxel layers act2(BN2(Conv2(act1(BN1(Conv1(x)))))) in one
     autograd node, so the inner activation lives only as Conv2's channels-last
@@ -146,49 +184,45 @@ class _Conv3dBnActPair(torch.autograd.Function):
     def forward(ctx, x, w1, b1, g1, bt1, rm1, rv1, nbt1, w2, b2, g2, bt2, rm2, rv2, nbt2, eps1,
                 mom1, slope1, eps2, mom2, slope2, occ=None):
         from pcfm import ops
-        bsz, cin, r = x.shape[0], x.shape[1], x.shape[2]
-        cmid, cout = w1.shape[0], w2.shape[0]
-        xs = ops.conv3d_split(x)
-        masks, vl, cnt = (occ.masks, occ.lists, occ.cnt) if occ is not None else (None, None, None)
-        y1 = ops.conv3d_igemm_split(xs, ops.conv3d_prep_weight(w1, False), b1, bsz, cin, cmid,
-                                    r, "conv3d_fwd", occ=masks, occ_mode=1, vlists=vl, cnt=cnt)
-        z1s, m1, is1 = ops.bn_act_forward_split(y1, g1, bt1, eps1, slope1, mom1, rm1, rv1, nbt1)
-        y2 = ops.conv3d_igemm_split(z1s, ops.conv3d_prep_weight(w2, False), b2, bsz, cmid, cout,
-                                    r, "conv3d_fwd")
+        xs, y1, m1, is1, z1s, y2 = _pair_head(x, w1, b1, g1, bt1, rm1, rv1, nbt1, w2, b2, eps1,
+                                              mom1, slope1, occ)
         z2, m2, is2 = ops.bn_act_forward(y2, g2, bt2, eps2, slope2, mom2, rm2, rv2, nbt2)
         ctx.save_for_backward(xs, w1, y1, g1, bt1, m1, is1, z1s, w2, y2, g2, bt2, m2, is2)
         ctx.occ = occ
         ctx.slopes = (slope1, slope2)
         ctx.has_bias = (b1 is not None, b2 is not None)
-        ctx.dims = (bsz, cin, cmid, cout, r)
+        ctx.dims = (x.shape[0], x.shape[1], w1.shape[0], w2.shape[0], x.shape[2])
         return z2
 
     @staticmethod
     def backward(ctx, dz2):
         from pcfm import ops
         xs, w1, y1, g1, bt1, m1, is1, z1s, w2, y2, g2, bt2, m2, is2 = ctx.saved_tensors
-        bsz, cin, cmid, cout, r = ctx.dims
         gys2, dg2, dbt2, db2 = ops.bn_act_backward_split(dz2, y2, g2, bt2, m2, is2,
                                                          ctx.slopes[1],
                                                          want_dbias_in=ctx.has_bias[1])
-        dz1 = ops.conv3d_igemm_split(gys2, ops.conv3d_prep_weight(w2, True), None, bsz, cout,
-                                     cmid, r, "conv3d_bwd_data")
-        dw2 = ops.conv3d_wgrad_split(z1s, gys2, bsz, cmid, cout, r)
-        del gys2
-        gys1, dg1, dbt1, db1 = ops.bn_act_backward_split(dz1, y1, g1, bt1, m1, is1,
-                                                         ctx.slopes[0],
-                                                         want_dbias_in=ctx.has_bias[0])
-        del dz1
-        dx = None
-        occ = ctx.occ
-        masks, vl, cnt = (occ.masks, occ.lists, occ.cnt) if occ is not None else (None, None, None)
-        if ctx.needs_input_grad[0]:
-            dx = ops.conv3d_igemm_split(gys1, ops.conv3d_prep_weight(w1, True), None, bsz, cmid,
-                                        cin, r, "conv3d_bwd_data", occ=masks, occ_mode=2,
-                                        vlists=vl, cnt=cnt)
-        dw1 = ops.conv3d_wgrad_split(xs, gys1, bsz, cin, cmid, r, occ=masks)
+        dx, dw1, db1, dg1, dbt1, dw2 = _pair_tail(gys2, xs, w1, y1, g1, bt1, m1, is1, z1s, w2,
+                                                  ctx.slopes[0], ctx.has_bias[0], ctx.dims,
+                                                  ctx.occ, ctx.needs_input_grad[0])
         return (dx, dw1, db1, dg1, dbt1, None, None, None, dw2, db2, dg2, dbt2, None, None,
                 None, None, None, None, None, None, None, None)
+
+
+def pair_fusable(conv1, bn1, conv2, bn2, x: torch.Tensor) -> bool:
+    """Whether conv_bn_act_pair runs its two layers as one fused GPU node."""
+    from modules.shared_mlp import PointwiseConv1d
+    ok = (not isinstance(conv1, PointwiseConv1d) and not isinstance(conv2, PointwiseConv1d)
+          and _fusable_pre(bn1) and _fusable_pre(bn2) and hasattr(conv1, "x3_ok")
+          and hasattr(conv2, "x3_ok") and conv1.x3_ok(x) and conv1.bias is not None
+          and conv2.bias is not None and conv1.out_channels % 64 == 0
+          and x[0, 0].numel() % 64 == 0 and x.shape[0] * conv2.out_channels < 65536
+          and x.shape[0] * conv1.out_channels < 65536 and x.shape[0] * x[0, 0].numel() > 1)
+    if ok:
+        from pcfm import ops
+        # shape / dtype / device stand-in for conv1's output (no allocation)
+        probe = x.new_empty(()).expand((x.shape[0], conv1.out_channels) + tuple(x.shape[2:]))
+        ok = conv2.x3_ok(probe) and ops.conv3d_split_supported(probe)
+    return ok
 
 
 def conv_bn_act_pair(conv1, bn1, slope1: float, conv2, bn2, slope2: float,
@@ -209,19 +243,7 @@ def conv_bn_act_pair(conv1, bn1, slope1: float, conv2, bn2, slope2: float,
         if bool((x.reshape(x.shape[0], x.shape[1], -1)[empty] != 0).any()):
             raise AssertionError("conv_bn_act_pair: voxelized_input_occ given but x is non-zero "
                                  "at an empty voxel")
-    from modules.shared_mlp import PointwiseConv1d
-    ok = (not isinstance(conv1, PointwiseConv1d) and not isinstance(conv2, PointwiseConv1d)
-          and _fusable_pre(bn1) and _fusable_pre(bn2) and hasattr(conv1, "x3_ok")
-          and hasattr(conv2, "x3_ok") and conv1.x3_ok(x) and conv1.bias is not None
-          and conv2.bias is not None and conv1.out_channels % 64 == 0
-          and x[0, 0].numel() % 64 == 0 and x.shape[0] * conv2.out_channels < 65536
-          and x.shape[0] * conv1.out_channels < 65536 and x.shape[0] * x[0, 0].numel() > 1)
-    if ok:
-        from pcfm import ops
-        # shape / dtype / device stand-in for conv1's output (no allocation)
-        probe = x.new_empty(()).expand((x.shape[0], conv1.out_channels) + tuple(x.shape[2:]))
-        ok = conv2.x3_ok(probe) and ops.conv3d_split_supported(probe)
-    if not ok:
+    if not pair_fusable(conv1, bn1, conv2, bn2, x):
         x = conv_bn_act(conv1, bn1, x, slope1)
         return conv_bn_act(conv2, bn2, x, slope2)
     return _Conv3dBnActPair.apply(

@@ -13,7 +13,7 @@ import torch.nn as nn
 import torch.nn.functional as TF
 
 import modules.functional as F
-from modules.norm_act import conv_bn_act_pair
+from modules.norm_act import _nbt, _pair_head, _pair_tail, conv_bn_act_pair, pair_fusable
 from modules.se import SE3d
 from modules.shared_mlp import SharedMLP
 from modules.voxel_conv import VoxelConv3d
@@ -100,6 +100,81 @@ class _SEDevoxAdd(torch.autograd.Function):
         return g.view(ctx.shape), None, dout, dw1, dw2, None, None
 
 
+class _VoxelBranchSEDevox(torch.autograd.Function):
+    """The whole voxel branch of a PVConv with SE in one autograd node:
+    devox(SE(act2(BN2(Conv2(act1(BN1(Conv1(grid)))))))) + pf
+    (pvconv.py:20-39, se.py:6-17).  act2(BN2(.)) is never written: its batch
+    statistics and SE's pooling come from one pass over Conv2's output y2
+    (bn_act_forward_rowmean), and the devoxelization applies BN2 + act2 while
+    staging its rows.  Backward from g = devox_bwd(dout): one pass over (g, y2)
+    gives SE's ds and every BN2 sum (dz = s g + dm / V is linear in s and dm:
+    bn_se_backward_stats), the SE MLP's backward gives dm, and the apply pass
+    writes d y2 as Conv2's split operand (bn_se_backward_apply_split).  Against
+    _Conv3dBnActPair + _SEDevoxAdd: the activation's write, both SE rows_dot
+    passes, the rows_affine pass and BN2's backward statistics pass are gone."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, g1, bt1, rm1, rv1, nbt1, w2, b2, g2, bt2, rm2, rv2, nbt2,
+                sw1, sw2, coords, pf, eps1, mom1, slope1, eps2, mom2, slope2, r, occ=None):
+        from pcfm import ops, plans
+        xs, y1, m1, is1, z1s, y2 = _pair_head(x, w1, b1, g1, bt1, rm1, rv1, nbt1, w2, b2, eps1,
+                                              mom1, slope1, occ)
+        mse, m2, is2 = ops.bn_act_forward_rowmean(y2, g2, bt2, eps2, slope2, mom2, rm2, rv2,
+                                                  nbt2)
+        sw1, sw2 = sw1.contiguous(), sw2.contiguous()
+        s, hid = ops.se_mlp_forward(mse, sw1, sw2)
+        shared = plans.devox_corners(coords, r)
+        out, inds, wgts = ops.trilinear_devoxelize_bn_scale_add(
+            r, shared is None, coords, y2, m2, is2, g2, bt2, slope2, s, pf)
+        if shared is not None:
+            inds, wgts = shared
+        else:
+            plans.put_devox_corners(coords, r, inds, wgts)
+        ctx.save_for_backward(xs, w1, y1, g1, bt1, m1, is1, z1s, w2, y2, g2, bt2, m2, is2,
+                              inds, wgts, mse, s, hid, sw1, sw2)
+        ctx.points, ctx.r, ctx.occ = coords, r, occ
+        ctx.slopes = (slope1, slope2)
+        ctx.has_bias = (b1 is not None, b2 is not None)
+        ctx.dims = (x.shape[0], x.shape[1], w1.shape[0], w2.shape[0], x.shape[2])
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        from pcfm import ops, plans
+        (xs, w1, y1, g1, bt1, m1, is1, z1s, w2, y2, g2, bt2, m2, is2, inds, wgts, mse, s, hid,
+         sw1, sw2) = ctx.saved_tensors
+        dout = dout.contiguous()
+        if plans.ENABLED:
+            plan = plans.devox_bwd_plan(ctx.points, inds, wgts, ctx.r)
+            g = ops.trilinear_devoxelize_backward_planned(dout, plan)
+        else:
+            g = ops.trilinear_devoxelize_backward(dout, inds, wgts, ctx.r)
+        g = g.view(y2.shape)
+        rowstats = ops.bn_se_backward_stats(g, y2, m2, is2, g2, bt2, ctx.slopes[1])
+        v = y2[0, 0].numel()
+        dmv, dsw1, dsw2 = ops.se_mlp_backward(mse, hid, s, rowstats[0], sw1, sw2, 1.0 / v)
+        gys2, dg2, dbt2, db2 = ops.bn_se_backward_apply_split(
+            g, y2, m2, is2, g2, bt2, s, dmv, rowstats, ctx.slopes[1],
+            want_dbias_in=ctx.has_bias[1])
+        del g
+        dx, dw1, db1, dg1, dbt1, dw2 = _pair_tail(gys2, xs, w1, y1, g1, bt1, m1, is1, z1s, w2,
+                                                  ctx.slopes[0], ctx.has_bias[0], ctx.dims,
+                                                  ctx.occ, ctx.needs_input_grad[0])
+        return (dx, dw1, db1, dg1, dbt1, None, None, None, dw2, db2, dg2, dbt2, None, None, None,
+                dsw1, dsw2, None, dout, None, None, None, None, None, None, None, None)
+
+
+# the voxel branch as one node (PCFM_PV_FUSED=0: the conv pair + the SE devoxelization
+# as two nodes, the round-4 form; A/B knob)
+_PV_FUSED = __import__("os").environ.get("PCFM_PV_FUSED", "1") != "0"
+
+
+def _se_fused_ok(b, c, w1) -> bool:
+    """The SE MLP fits its one-block kernels (pcfm_se_mlp_fwd / _bwd)."""
+    h = w1.shape[0]
+    return _SE_FUSED and 2 * (b + h) * c + 2 * b * h <= 32768
+
+
 def _se_devox_ok(se, grid, pf) -> bool:
     if not (grid.is_cuda and grid.dtype == torch.float32 and pf.dtype == torch.float32
             and isinstance(se, SE3d)):
@@ -143,10 +218,28 @@ class PVConv(nn.Module):
             # occupied voxels, and its gradient is read back only on them
             from pcfm import plans
             occ = plans.conv_occupancy(self.voxelization._coords(coords)[1], self.resolution)
+        if (_PV_FUSED and self.training and torch.is_grad_enabled() and len(layers) > 6
+                and grid.is_cuda and pair_fusable(layers[0], layers[1], layers[3], layers[4], grid)):
+            pf = self.point_features(features)
+            fc = layers[6].fc
+            if (_se_devox_ok(layers[6], grid, pf) and grid[0, 0].numel() <= 32768
+                    and _se_fused_ok(grid.shape[0], layers[3].out_channels, fc[0].weight)):
+                c1, n1, c2, n2 = layers[0], layers[1], layers[3], layers[4]
+                out = _VoxelBranchSEDevox.apply(
+                    grid.contiguous(), c1.weight, c1.bias, n1.weight, n1.bias, n1.running_mean,
+                    n1.running_var, _nbt(n1), c2.weight, c2.bias, n2.weight, n2.bias,
+                    n2.running_mean, n2.running_var, _nbt(n2), fc[0].weight, fc[2].weight,
+                    grid_coords, pf, float(n1.eps), float(n1.momentum),
+                    float(layers[2].negative_slope), float(n2.eps), float(n2.momentum),
+                    float(layers[5].negative_slope), self.resolution, occ)
+                return out, coords
+        else:
+            pf = None
         grid = conv_bn_act_pair(layers[0], layers[1], layers[2].negative_slope,
                                 layers[3], layers[4], layers[5].negative_slope, grid,
                                 voxelized_input_occ=occ)
-        pf = self.point_features(features)
+        if pf is None:
+            pf = self.point_features(features)
         if (len(layers) > 6 and _se_devox_ok(layers[6], grid, pf)
                 and (self.training or not torch.is_grad_enabled())):
             fc = layers[6].fc

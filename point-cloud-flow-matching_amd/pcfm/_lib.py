@@ -80,6 +80,15 @@ SIGNATURES = {
     "pcfm_debug_devox_verify": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _P]),
     "pcfm_se_mlp_fwd": (_I, [_P, _P, _P, _I, _I, _I, _P, _P, _P]),
     "pcfm_se_mlp_bwd": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _F, _P, _P, _P, _P]),
+    "pcfm_trilinear_devoxelize_bn_scale_add_fwd": (_I, [_P, _P, _P, _P, _P, _P, _F, _P, _P, _I,
+                                                       _I, _I, _I, _I, _P, _P, _P, _P]),
+    "pcfm_bn_act_fwd_rowmean_workspace_bytes": (_Z, [_I, _I, _I]),
+    "pcfm_bn_act_fwd_rowmean": (_I, [_P, _P, _P, _I, _I, _I, _F, _F, _F, _P, _P, _P, _P, _P, _P,
+                                     _P, _Z, _P]),
+    "pcfm_bn_se_bwd_workspace_bytes": (_Z, [_I, _I, _I]),
+    "pcfm_bn_se_bwd_stats": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _F, _P, _P, _Z, _P]),
+    "pcfm_bn_se_bwd_apply_split": (_I, [_P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _F, _P,
+                                        _P, _P, _P, _P, _Z, _P]),
     "pcfm_rows_dot": (_I, [_P, _P, _L, _I, _F, _P, _P]),
     "pcfm_rows_affine": (_I, [_P, _P, _P, _L, _I, _P]),
     "pcfm_rows_colsum_workspace_bytes": (_Z, [_I, _L, _I]),
@@ -133,7 +142,7 @@ SIGNATURES = {
     "pcfm_adamw_ema_step": (_I, [_P, _P, _I, _P, _P, _I, _DP, _DP, _D, _D, _D, _D, _P]),
 }
 
-ABI_VERSION = 18
+ABI_VERSION = 19
 
 _lock = threading.Lock()
 _lib = None

@@ -1273,6 +1273,122 @@ def bn_act_backward_split(dz: torch.Tensor, x: torch.Tensor, weight, bias, mean,
     return dxs, dgb[0], dgb[1], (dgb[2] if want_dbias_in else None)
 
 
+# PVConv's second voxel BatchNorm + LeakyReLU fused with SE3d and the
+# devoxelization (include/pcfm.h, ABI 19): act(bn(x)) is never written
+def bn_act_forward_rowmean(x: torch.Tensor, weight: torch.Tensor, bias: torch.Tensor, eps: float,
+                           slope: float, momentum: float, running_mean, running_var,
+                           num_batches_tracked=None):
+    """BatchNorm statistics of x (B, C, ...) (running stats updated) and the per-(b, c)
+    mean of act(bn(x)) -- SE3d's pooling -- without writing act(bn(x)):
+    -> (rowmean (B, C), mean, invstd)."""
+    _check(x, "input", "f")
+    b, c = x.shape[0], x.shape[1]
+    s = x.numel() // max(1, b * c)
+    rowmean = torch.empty((b, c), dtype=torch.float32, device=x.device)
+    stats = torch.empty((2, c), dtype=torch.float32, device=x.device)
+    ws = _workspace(_lib.query("pcfm_bn_act_fwd_rowmean_workspace_bytes", b, c, s), x)
+    with _timed("bn_act_fwd", 4 * 2 * x.numel(), x):
+        _lib.call("pcfm_bn_act_fwd_rowmean", _ptr(x), _ptr(weight), _ptr(bias), b, c, s,
+                  float(eps), float(slope), float(momentum), _p(running_mean), _p(running_var),
+                  _p(_counter(num_batches_tracked, x)), _ptr(rowmean), _ptr(stats[0]),
+                  _ptr(stats[1]), _ptr(ws), ws.numel(), _stream(x))
+    return rowmean, stats[0], stats[1]
+
+
+def trilinear_devoxelize_bn_scale_add(r: int, is_training: bool, coords: torch.Tensor,
+                                      x: torch.Tensor, mean, invstd, weight, bias, slope: float,
+                                      scale, add):
+    """trilinear_devoxelize_scale_add of act(bn(x)) with the given batch statistics;
+    the activation is applied as the rows are staged -> [outs, inds, wgts]."""
+    _check(x, "x", "f")
+    _check(coords, "coords", "f")
+    b, c = x.shape[0], x.shape[1]
+    n = coords.shape[2]
+    r = int(r)
+    dev = x.device
+    for t, nm in ((mean, "mean"), (invstd, "invstd"), (weight, "weight"), (bias, "bias")):
+        _check(t, nm, "f")
+        if t.numel() != c:
+            raise ValueError(f"trilinear_devoxelize_bn_scale_add: {nm} must have C values")
+    if scale is not None:
+        scale = scale.contiguous()
+        _check(scale, "scale", "f")
+        if scale.numel() != b * c:
+            raise ValueError("trilinear_devoxelize_bn_scale_add: scale must be (B, C)")
+    if add is not None:
+        add = add.contiguous()
+        _check(add, "add", "f")
+        if tuple(add.shape) != (b, c, n):
+            raise ValueError("trilinear_devoxelize_bn_scale_add: add must be (B, C, N)")
+    outs = torch.empty((b, c, n), dtype=torch.float32, device=dev)
+    if is_training:
+        inds = torch.empty((b, 8, n), dtype=torch.int32, device=dev)
+        wgts = torch.empty((b, 8, n), dtype=torch.float32, device=dev)
+        pi, pw = _ptr(inds), _ptr(wgts)
+    else:
+        inds = torch.zeros((1,), dtype=torch.int32, device=dev)
+        wgts = torch.zeros((1,), dtype=torch.float32, device=dev)
+        pi, pw = None, None
+    nbytes = 4 * b * (3 * n + c * r ** 3 + c * n * (2 if add is not None else 1)
+                      + (16 * n if is_training else 0))
+    with _timed("trilinear_devoxelize_fwd", nbytes, x):
+        _lib.call("pcfm_trilinear_devoxelize_bn_scale_add_fwd", _ptr(coords), _ptr(x), _ptr(mean),
+                  _ptr(invstd), _ptr(weight), _ptr(bias), float(slope),
+                  _ptr(scale) if scale is not None else None,
+                  _ptr(add) if add is not None else None, b, c, n, r, 1 if is_training else 0,
+                  _ptr(outs), pi, pw, _stream(x))
+    return [outs, inds, wgts]
+
+
+def bn_se_backward_stats(g: torch.Tensor, x: torch.Tensor, mean, invstd, weight, bias,
+                         slope: float) -> torch.Tensor:
+    """rowstats (5, B, C): per (b, c) row of g (B, C, S) and x, with z = act(bn(x)),
+    a = act'(bn(x)), xh = xhat: (sum z g, sum a g, sum a, sum a g xh, sum a xh)."""
+    _check(g, "g", "f")
+    _check(x, "x", "f")
+    b, c = x.shape[0], x.shape[1]
+    s = x.numel() // max(1, b * c)
+    if g.shape != x.shape:
+        raise ValueError("bn_se_backward_stats: g and x shapes differ")
+    wsb = _lib.query("pcfm_bn_se_bwd_workspace_bytes", b, c, s)
+    if wsb == 0:
+        raise RuntimeError(f"bn_se_backward_stats: unsupported shape {tuple(x.shape)}")
+    rowstats = torch.empty((5, b, c), dtype=torch.float32, device=x.device)
+    ws = _workspace(wsb, x)
+    with _timed("bn_act_bwd", 4 * 2 * x.numel(), x):
+        _lib.call("pcfm_bn_se_bwd_stats", _ptr(g), _ptr(x), _ptr(mean), _ptr(invstd),
+                  _ptr(weight), _ptr(bias), b, c, s, float(slope), _ptr(rowstats), _ptr(ws),
+                  ws.numel(), _stream(x))
+    return rowstats
+
+
+def bn_se_backward_apply_split(g: torch.Tensor, x: torch.Tensor, mean, invstd, weight, bias,
+                               se_scale: torch.Tensor, dmv: torch.Tensor, rowstats: torch.Tensor,
+                               slope: float, want_dbias_in: bool = False):
+    """bn_act_backward_split for dz = se_scale[b, c] * g + dmv[b, c] (never written),
+    the sums from bn_se_backward_stats -> (dxs, dgamma, dbeta, dbias_in or None)."""
+    b, c, r = x.shape[0], x.shape[1], x.shape[2]
+    s = x.numel() // max(1, b * c)
+    for t, nm in ((se_scale, "se_scale"), (dmv, "dmv")):
+        _check(t, nm, "f")
+        if t.numel() != b * c:
+            raise ValueError(f"bn_se_backward_apply_split: {nm} must be (B, C)")
+    _check(rowstats, "rowstats", "f")
+    n = _lib.query("pcfm_conv3d_split_bytes", b, c, r)
+    wsb = _lib.query("pcfm_bn_se_bwd_workspace_bytes", b, c, s)
+    if n == 0 or wsb == 0:
+        raise RuntimeError(f"bn_se_backward_apply_split: unsupported shape {tuple(x.shape)}")
+    dxs = torch.empty(n, dtype=torch.uint8, device=x.device)
+    dgb = torch.empty((3, c), dtype=torch.float32, device=x.device)
+    ws = _workspace(wsb, x)
+    with _timed("bn_act_bwd", 4 * 3 * x.numel(), x):
+        _lib.call("pcfm_bn_se_bwd_apply_split", _ptr(g), _ptr(x), _ptr(mean), _ptr(invstd),
+                  _ptr(weight), _ptr(bias), _ptr(se_scale), _ptr(dmv), _ptr(rowstats), b, c, s,
+                  float(slope), _ptr(dxs), _ptr(dgb[0]), _ptr(dgb[1]),
+                  _ptr(dgb[2]) if want_dbias_in else None, _ptr(ws), ws.numel(), _stream(x))
+    return dxs, dgb[0], dgb[1], (dgb[2] if want_dbias_in else None)
+
+
 def rows_max_bf16(h: torch.Tensor):
     """(values bf16 (B, C), indices int32 (B, C)) = max over dim 1 of h (B, N, C) bf16."""
     _check_cuda(h, "h")

@@ -262,3 +262,88 @@ def test_conv_bn_act_pair_matches_two_nodes(ops, b, c, r):
         for (name, b_ref), bb in zip(m_ref.named_buffers(), m.buffers()):
             assert torch.equal(b_ref, bb), name
     assert int(mods[1].num_batches_tracked) == int(mods[3].num_batches_tracked) == 1
+
+
+def _unsplit(buf, b, c, s):
+    """Decode a conv split operand (pcfm_common.hpp split_off: channels-last rows,
+    [hi 32 | lo 32] per 32-channel group) back to fp32 (B, C, S) = hi + lo."""
+    t = buf.view(torch.bfloat16).view(b * s, c // 32, 2, 32).float()
+    return (t[:, :, 0] + t[:, :, 1]).reshape(b, s, c).permute(0, 2, 1).contiguous()
+
+
+@pytest.mark.parametrize("b,c,r,slope", [(2, 128, 16, 0.1), (8, 256, 8, 0.1), (2, 128, 32, 0.1),
+                                         (1, 64, 4, 0.0)])
+def test_bn_act_rowmean_and_bn_devox_match_unfused(ops, b, c, r, slope):
+    """PVConv's BN2 fused with SE and the devoxelization, forward: the statistics,
+    running stats and counter bit-equal to pcfm_bn_act_fwd (same passes); rowmean
+    = the per-(b, c) mean of act(bn(x)) to fp32 summation order; the gather that
+    applies bn + act while staging bit-equal to the plain gather of act(bn(x))."""
+    g = torch.Generator(device="cuda").manual_seed(r)
+    s = r ** 3
+    x = torch.randn(b, c, r, r, r, device="cuda", generator=g) * 2.0 + 1.0
+    gamma = torch.rand(c, device="cuda", generator=g) + 0.5
+    beta = torch.rand(c, device="cuda", generator=g) - 0.5
+    rm, rv = torch.zeros(c, device="cuda"), torch.ones(c, device="cuda")
+    rm2, rv2 = rm.clone(), rv.clone()
+    nbt = torch.zeros((), dtype=torch.int64, device="cuda")
+    nbt2 = nbt.clone()
+    z, m, iv = ops.bn_act_forward(x, gamma, beta, 1e-4, slope, 0.1, rm, rv, nbt)
+    rowmean, m2, iv2 = ops.bn_act_forward_rowmean(x, gamma, beta, 1e-4, slope, 0.1, rm2, rv2, nbt2)
+    assert torch.equal(m, m2) and torch.equal(iv, iv2)
+    assert torch.equal(rm, rm2) and torch.equal(rv, rv2) and int(nbt2) == 1
+    ref = z.double().reshape(b, c, s).mean(-1)
+    torch.testing.assert_close(rowmean.double(), ref, rtol=0, atol=2e-6 * float(z.abs().max()))
+    n = 3000
+    coords = torch.rand(b, 3, n, device="cuda", generator=g) * (r - 1)
+    sc = torch.rand(b, c, device="cuda", generator=g)
+    pf = torch.randn(b, c, n, device="cuda", generator=g)
+    o_ref, i_ref, w_ref = ops.trilinear_devoxelize_scale_add(r, True, coords, z, sc, pf)
+    o, i, w = ops.trilinear_devoxelize_bn_scale_add(r, True, coords, x, m2, iv2, gamma, beta,
+                                                    slope, sc, pf)
+    assert torch.equal(o, o_ref) and torch.equal(i, i_ref) and torch.equal(w, w_ref)
+
+
+@pytest.mark.parametrize("b,c,r,slope", [(2, 128, 16, 0.1), (8, 256, 8, 0.1), (2, 128, 32, 0.1),
+                                         (1, 64, 4, 0.0)])
+def test_bn_se_backward_matches_composition(ops, b, c, r, slope):
+    """PVConv's BN2 + SE backward from g = devox_bwd(dout): pcfm_bn_se_bwd_stats'
+    ds = sum z g against fp64, and pcfm_bn_se_bwd_apply_split against the round-4
+    composition (dz = rows_affine(g, s, dmv) -> pcfm_bn_act_bwd): dx (split operand,
+    decoded), dgamma, dbeta within fp32 summation-order bounds."""
+    gen = torch.Generator(device="cuda").manual_seed(7 + r)
+    s = r ** 3
+    x = torch.randn(b, c, r, r, r, device="cuda", generator=gen) * 2.0 + 1.0
+    gr = torch.randn(b, c, r, r, r, device="cuda", generator=gen)
+    gamma = torch.rand(c, device="cuda", generator=gen) + 0.5
+    beta = torch.rand(c, device="cuda", generator=gen) - 0.5
+    se_s = torch.rand(b, c, device="cuda", generator=gen)
+    dmv = torch.randn(b, c, device="cuda", generator=gen) * 1e-3
+    mean = x.mean(dim=(0, 2, 3, 4))
+    invstd = torch.rsqrt(x.var(dim=(0, 2, 3, 4), unbiased=False) + 1e-4)
+    # reference composition
+    xh = (x.double() - mean.double()[None, :, None, None, None]) * invstd.double()[None, :, None,
+                                                                                      None, None]
+    t = xh * gamma.double()[None, :, None, None, None] + beta.double()[None, :, None, None, None]
+    z = torch.where(t > 0, t, t * slope)
+    ds_ref = (z * gr.double()).reshape(b, c, s).sum(-1)
+    dz = gr.clone().reshape(b * c, s)
+    ops.rows_affine_(dz, se_s.reshape(-1), dmv.reshape(-1))
+    dx, dg, dbt, db = ops.bn_act_backward(dz.view_as(x), x, gamma, beta, mean, invstd, slope,
+                                          want_dbias_in=True)
+    # fused
+    rowstats = ops.bn_se_backward_stats(gr, x, mean, invstd, gamma, beta, slope)
+    assert rowstats.shape == (5, b, c)
+    scale = float((z.abs() * gr.double().abs()).reshape(b, c, s).sum(-1).max())
+    torch.testing.assert_close(rowstats[0].double(), ds_ref, rtol=0, atol=1e-5 * scale)
+    dxs, dg2, dbt2, db2 = ops.bn_se_backward_apply_split(gr, x, mean, invstd, gamma, beta, se_s,
+                                                         dmv, rowstats, slope, want_dbias_in=True)
+    got = _unsplit(dxs, b, c, s)
+    ref = dx.reshape(b, c, s)
+    torch.testing.assert_close(got, ref, rtol=0, atol=2e-5 * float(ref.abs().max()))
+    for a, e in ((dg2, dg), (dbt2, dbt)):
+        torch.testing.assert_close(a, e, rtol=0, atol=2e-5 * float(e.abs().max()) + 1e-6)
+    sc = float(dx.abs().sum(dim=(0, 2, 3, 4)).max())
+    torch.testing.assert_close(db2, db, rtol=0, atol=1e-5 * sc)
+    # deterministic
+    rs2 = ops.bn_se_backward_stats(gr, x, mean, invstd, gamma, beta, slope)
+    assert torch.equal(rowstats, rs2)

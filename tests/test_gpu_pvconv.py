@@ -344,3 +344,50 @@ def test_conv_voxel_list_gemm_is_exact(ops, b, cin, cout, r, surface, report):
            {"occupied_fraction": float((cnt > 0).float().mean()),
             "listed_fwd_chunk_fraction": int(lists[1]) * 32 / float(b * r ** 3),
             "listed_bwd_chunk_fraction": int(lists[0]) * 32 / float(b * r ** 3)})
+
+
+@pytest.mark.parametrize("cin,cout,r,n", [(128, 128, 32, 20000), (256, 256, 16, 8000),
+                                          (256, 256, 8, 5000)])
+def test_voxel_branch_node_matches_two_node_form(ops, monkeypatch, cin, cout, r, n):
+    """The PVConv voxel branch as one node (_VoxelBranchSEDevox: BN2's activation
+    never written, SE pooling and BN2 backward sums from single passes) against
+    the round-4 two-node form (_Conv3dBnActPair + _SEDevoxAdd) at the C2 stage
+    shapes: outputs, every gradient and the running statistics to fp32
+    summation order (SE's pooling and BN2's backward sums are taken in another
+    order)."""
+    import modules.pvconv as pv
+    torch.manual_seed(r)
+    mod = pv.PVConv(cin, cout, 3, r, with_se=True, normalize=True).cuda().train()
+    g = torch.Generator(device="cuda").manual_seed(r)
+    feats = torch.randn(2, cin, n, device="cuda", generator=g)
+    coords = torch.randn(2, 3, n, device="cuda", generator=g)
+    gy = torch.randn(2, cout, n, device="cuda", generator=g)
+    state = {k: v.clone() for k, v in mod.state_dict().items()}
+
+    def run():
+        mod.load_state_dict(state)
+        f = feats.clone().requires_grad_(True)
+        out, _ = mod((f, coords))
+        node = type(out.grad_fn).__name__
+        out.backward(gy)
+        grads = [("input", f.grad)] + [(k, p.grad.clone()) for k, p in mod.named_parameters()]
+        bufs = {k: v.clone() for k, v in mod.state_dict().items()}
+        mod.zero_grad(set_to_none=True)
+        return out.detach(), grads, bufs, node
+
+    o1, g1, b1, n1 = run()
+    monkeypatch.setattr(pv, "_PV_FUSED", False)
+    o0, g0, b0, n0 = run()
+    assert n1 == "_VoxelBranchSEDevoxBackward" and n0 != n1, (n1, n0)
+    assert _rel(o1, o0) < 1e-5
+    zero_grad = {"voxel_layers.0.bias", "voxel_layers.3.bias", "point_features.layers.0.bias"}
+    for (name, a), (_, b) in zip(g1, g0):
+        if name in zero_grad:
+            assert (a - b).abs().max().item() < 1e-3, name
+        else:
+            assert _rel(a, b) < 1e-4, (name, _rel(a, b))
+    for k in b0:  # running statistics (and the unchanged parameters)
+        if b0[k].dtype.is_floating_point:
+            torch.testing.assert_close(b1[k], b0[k], rtol=1e-6, atol=1e-7, msg=k)
+        else:
+            assert torch.equal(b1[k], b0[k]), k
