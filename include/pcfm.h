@@ -107,13 +107,16 @@ int pcfm_trilinear_devoxelize_scale_add_fwd(const float* coords, const float* fe
  * PVConv's second voxel-conv output, bn_mean / bn_invstd its batch statistics
  * (pcfm_bn_act_fwd_rowmean), act(t) = t > 0 ? t : slope * t -- BatchNorm3d +
  * LeakyReLU (pvconv.py:20-30) applied while the rows are staged, so the
- * activation is never written.  r^3 <= 32768. */
-int pcfm_trilinear_devoxelize_bn_scale_add_fwd(const float* coords, const float* x,
-                                               const float* bn_mean, const float* bn_invstd,
-                                               const float* gamma, const float* beta, float slope,
-                                               const float* scale, const float* add, int b, int c,
-                                               int n, int r, int training, float* out, int* inds,
-                                               float* wgts, void* stream);
+ * activation is never written.  With add_mean != NULL the add operand is
+ * likewise act(bn(add)) with its own statistics and affine (the point branch's
+ * pre-BatchNorm1d output, shared_mlp.py:15-27; add_slope 0 = ReLU).
+ * r^3 <= 32768. */
+int pcfm_trilinear_devoxelize_bn_scale_add_fwd(
+    const float* coords, const float* x, const float* bn_mean, const float* bn_invstd,
+    const float* gamma, const float* beta, float slope, const float* scale, const float* add,
+    const float* add_mean, const float* add_invstd, const float* add_gamma,
+    const float* add_beta, float add_slope, int b, int c, int n, int r, int training, float* out,
+    int* inds, float* wgts, void* stream);
 
 /* Diagnosis only (not a reference interface): recompute scale * devox(feat) + add
  * per output in the plainest form and compare bit for bit with `out` (and, when
@@ -556,6 +559,14 @@ int pcfm_bn_act_fwd_split(const float* x, const float* gamma, const float* beta,
  * row, a = act'; rowstats[0] is SE's ds.  pcfm_bn_se_bwd_apply_split then writes
  * dx as pcfm_bn_act_bwd_split does (conv split operand, dgamma, dbeta,
  * dbias_in).  c, s multiples of 64.  Deterministic. */
+/* BatchNorm batch statistics only (mean, invstd; running stats and the counter
+ * updated as pcfm_bn_act_fwd): from x by a statistics pass (part NULL; workspace
+ * pcfm_bn_workspace_bytes), or finalized from a producer's epilogue statistics
+ * part [c][P] (pcfm_pointwise_gemm_bnstats, P = b * ceil(s / 64)). */
+int pcfm_bn_fwd_stats(const float* x, const float* part, int P, int b, int c, int s, float eps,
+                      float momentum, float* running_mean, float* running_var,
+                      long long* num_batches_tracked, float* mean, float* invstd, void* ws,
+                      size_t ws_bytes, void* stream);
 size_t pcfm_bn_act_fwd_rowmean_workspace_bytes(int b, int c, int s);
 int pcfm_bn_act_fwd_rowmean(const float* x, const float* gamma, const float* beta, int b, int c,
                             int s, float eps, float slope, float momentum, float* running_mean,

@@ -128,7 +128,7 @@ __global__ void __launch_bounds__(256)
     bn_finalize_kernel(const float* __restrict__ part, const float* __restrict__ x, int B, int C,
                        int S, int P, float eps, float momentum, float* __restrict__ rmean,
                        float* __restrict__ rvar, float* __restrict__ mean,
-                       float* __restrict__ invstd) {
+                       float* __restrict__ invstd, long long* __restrict__ nbt = nullptr) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
   float s, q;
@@ -144,6 +144,7 @@ __global__ void __launch_bounds__(256)
     rmean[c] = (1.0f - momentum) * rmean[c] + momentum * m;
     rvar[c] = (1.0f - momentum) * rvar[c] + momentum * (float)(var * n / (n - 1.0));
   }
+  if (nbt != nullptr && c == 0) nbt[0] += 1;
 }
 
 // bn_finalize / bn_bwd_finalize folded into the apply passes (one launch
@@ -1227,6 +1228,32 @@ extern "C" int pcfm_bn_act_fwd_rowmean(const float* x, const float* gamma, const
   hipLaunchKernelGGL(rowpart_sum_kernel, dim3(ceil_div(b * c, 256)), dim3(256), 0, st,
                      (const float*)rowpart, b * c, nblk, (float)(1.0 / (double)s), rowmean);
   return check_launch("bn_act_fwd_rowmean");
+}
+
+extern "C" int pcfm_bn_fwd_stats(const float* x, const float* part, int P, int b, int c, int s,
+                                 float eps, float momentum, float* running_mean,
+                                 float* running_var, long long* num_batches_tracked, float* mean,
+                                 float* invstd, void* ws, size_t ws_bytes, void* stream) {
+  PCFM_CHECK_ARG(bn_ok(b, c, s), "bn_fwd_stats: bad shape b=%d c=%d s=%d", b, c, s);
+  PCFM_CHECK_ARG((running_mean == nullptr) == (running_var == nullptr),
+                 "bn_fwd_stats: running_mean and running_var must both be given or both NULL");
+  hipStream_t st = (hipStream_t)stream;
+  if (part != nullptr) {  // the producer's epilogue statistics (pcfm_pointwise_gemm_bnstats)
+    PCFM_CHECK_ARG(P == b * ceil_div(s, 64),
+                   "bn_fwd_stats: need b * ceil(s / 64) = %d groups per channel, got %d",
+                   b * ceil_div(s, 64), P);
+    hipLaunchKernelGGL(bn_fin_parts_kernel, dim3(c), dim3(256), 0, st,
+                       reinterpret_cast<const float2*>(part), P, s, eps, momentum, running_mean,
+                       running_var, num_batches_tracked, mean, invstd);
+  } else {
+    PCFM_CHECK_ARG(ws_bytes >= pcfm_bn_workspace_bytes(b, c, s), "bn_fwd_stats: workspace too small");
+    float* wp = (float*)ws;
+    hipLaunchKernelGGL(bn_stats_kernel, dim3(c, bn_parts(b)), dim3(256), 0, st, x, b, c, s, wp);
+    hipLaunchKernelGGL(bn_finalize_kernel, dim3(ceil_div(c, 256)), dim3(256), 0, st,
+                       (const float*)wp, x, b, c, s, bn_parts(b), eps, momentum, running_mean,
+                       running_var, mean, invstd, num_batches_tracked);
+  }
+  return check_launch("bn_fwd_stats");
 }
 
 extern "C" size_t pcfm_bn_se_bwd_workspace_bytes(int b, int c, int s) {

@@ -170,9 +170,17 @@ __device__ __forceinline__ float tap_sum(const float* __restrict__ s, const int 
 // Optional epilogue of a gather: out = scale[b, c] * sum + add[b, c, i]
 // (either pointer may be null).  Used to fold a squeeze-excitation channel
 // scale of the rows and the residual point branch into the devoxelization.
+struct RowBn;
 struct GatherEpi {
   const float* scale = nullptr;  // [B][C]
   const float* add = nullptr;    // [B][C][NI]
+  // optional act(bn(.)) of the add operand (PVConv's point-branch BatchNorm1d +
+  // ReLU: SharedMLP's activation is never written); mean == nullptr: plain add
+  const float* add_mean = nullptr;
+  const float* add_invstd = nullptr;
+  const float* add_gamma = nullptr;
+  const float* add_beta = nullptr;
+  float add_slope = 0.0f;
 };
 
 // Optional transform of the rows as they are staged: row value v of channel c
@@ -199,6 +207,12 @@ struct RowBnC {  // one channel's constants
 };
 __device__ __forceinline__ RowBnC row_bn_at(const RowBn& bn, int c) {
   return RowBnC{bn.mean[c], bn.invstd[c], bn.gamma[c], bn.beta[c], bn.slope};
+}
+// the add operand's transform for channel c (identity when epi.add_mean == nullptr)
+__device__ __forceinline__ RowBnC add_bn_at(const GatherEpi& epi, int c) {
+  if (epi.add_mean == nullptr) return RowBnC{0.0f, 1.0f, 1.0f, 0.0f, 1.0f};
+  return RowBnC{epi.add_mean[c], epi.add_invstd[c], epi.add_gamma[c], epi.add_beta[c],
+                epi.add_slope};
 }
 
 // grid = (item splits, channel groups, b).  USE_LDS stages the block's
@@ -252,11 +266,13 @@ __global__ void __launch_bounds__(1024)
           epi.add != nullptr ? epi.add + ((size_t)b * C + c0) * NI + i : nullptr;
       const float* __restrict__ sb = epi.scale != nullptr ? epi.scale + (size_t)b * C + c0 : nullptr;
       float ad[4], sc[4];
+      const bool abn = epi.add_mean != nullptr;  // block-uniform
       auto fetch = [&](int cq) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           const int cc = min(cq + k, nc - 1);
           ad[k] = ab != nullptr ? nt_ld(ab + (size_t)cc * NI) : 0.0f;
+          if (abn) ad[k] = add_bn_at(epi, c0 + cc)(ad[k]);
           sc[k] = sb != nullptr ? sb[cc] : 1.0f;
         }
       };
@@ -318,6 +334,8 @@ __global__ void __launch_bounds__(1024)
   float* __restrict__ ob = out + ((size_t)b * C + c0) * NI;
   const float* __restrict__ ab = epi.add != nullptr ? epi.add + ((size_t)b * C + c0) * NI : nullptr;
   const float sc = epi.scale != nullptr ? epi.scale[(size_t)b * C + c0] : 1.0f;
+  const bool abn = epi.add_mean != nullptr;  // block-uniform
+  const RowBnC fa = add_bn_at(epi, c0);
   const bool primary = blockIdx.y == 0;
   const int stride = gridDim.x * blockDim.x;
   for (int i0 = blockIdx.x * blockDim.x + threadIdx.x; i0 < NI; i0 += IPT * stride) {
@@ -337,7 +355,7 @@ __global__ void __launch_bounds__(1024)
       if (i < NI) {
         float acc = tap_sum<T>(lds, id[u], w[u]);
         if (epi.scale != nullptr) acc *= sc;
-        if (ab != nullptr) acc += ad[u];
+        if (ab != nullptr) acc += abn ? fa(ad[u]) : ad[u];
         ob[i] = acc;
       }
     }
@@ -405,6 +423,9 @@ __global__ void __launch_bounds__(512)
 #pragma unroll
     for (int k = 0; k < 4; ++k) sc[k] = epi.scale[(size_t)b * C + c0 + k];
   }
+  const bool abn = epi.add_mean != nullptr;  // block-uniform
+  const RowBnC fa[4] = {add_bn_at(epi, c0), add_bn_at(epi, c0 + 1), add_bn_at(epi, c0 + 2),
+                        add_bn_at(epi, c0 + 3)};
   const bool primary = blockIdx.y == 0;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < NI; i += gridDim.x * blockDim.x) {
     float ad[4] = {0.0f, 0.0f, 0.0f, 0.0f};
@@ -421,7 +442,7 @@ __global__ void __launch_bounds__(512)
     for (int k = 0; k < 4; ++k) {
       float acc = r[k];
       if (epi.scale != nullptr) acc *= sc[k];
-      if (ab != nullptr) acc += ad[k];
+      if (ab != nullptr) acc += abn ? fa[k](ad[k]) : ad[k];
       ob[(size_t)k * NI + i] = acc;
     }
   }

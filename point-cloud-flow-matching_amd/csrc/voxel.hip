@@ -269,14 +269,18 @@ extern "C" int pcfm_trilinear_devoxelize_scale_add_fwd(const float* coords, cons
                        "trilinear_devoxelize_scale_add_fwd", epi);
 }
 
-// scale[b, c] * devox(act(bn(x)))[b, c, i] + add[b, c, i]: PVConv's second
+// scale[b, c] * devox(act(bn(x)))[b, c, i] + add'[b, c, i]: PVConv's second
 // BatchNorm3d + LeakyReLU applied to the conv output x as the gather stages its
 // rows (rows.hpp RowBn), so the activation is never written (norm.hip,
-// pcfm_bn_act_fwd_rowmean).
+// pcfm_bn_act_fwd_rowmean); add' = add, or act(bn(add)) with its own BatchNorm
+// operands (the point branch's BatchNorm1d + ReLU, SharedMLP's activation
+// never written either).
 extern "C" int pcfm_trilinear_devoxelize_bn_scale_add_fwd(
     const float* coords, const float* x, const float* bn_mean, const float* bn_invstd,
     const float* gamma, const float* beta, float slope, const float* scale, const float* add,
-    int b, int c, int n, int r, int training, float* out, int* inds, float* wgts, void* stream) {
+    const float* add_mean, const float* add_invstd, const float* add_gamma,
+    const float* add_beta, float add_slope, int b, int c, int n, int r, int training, float* out,
+    int* inds, float* wgts, void* stream) {
   int s = 0;
   PCFM_CHECK_ARG(b >= 0 && c >= 0 && n >= 0, "trilinear_devoxelize_bn_scale_add_fwd: negative size");
   PCFM_CHECK_ARG(cube_fits(r, &s), "trilinear_devoxelize_bn_scale_add_fwd: bad resolution %d", r);
@@ -286,9 +290,18 @@ extern "C" int pcfm_trilinear_devoxelize_bn_scale_add_fwd(
                  "trilinear_devoxelize_bn_scale_add_fwd: training needs inds/wgts buffers");
   PCFM_CHECK_ARG(s <= 32 * 1024, "trilinear_devoxelize_bn_scale_add_fwd: r^3 = %d > 32768", s);
   ProvDevox prov{coords, n, r, r * r, s, training ? inds : nullptr, training ? wgts : nullptr};
+  PCFM_CHECK_ARG(add_mean == nullptr ||
+                     (add != nullptr && add_invstd != nullptr && add_gamma != nullptr &&
+                      add_beta != nullptr),
+                 "trilinear_devoxelize_bn_scale_add_fwd: incomplete BatchNorm operands of add");
   GatherEpi epi;
   epi.scale = scale;
   epi.add = add;
+  epi.add_mean = add_mean;
+  epi.add_invstd = add_invstd;
+  epi.add_gamma = add_gamma;
+  epi.add_beta = add_beta;
+  epi.add_slope = add_slope;
   RowBn bn;
   bn.mean = bn_mean;
   bn.invstd = bn_invstd;

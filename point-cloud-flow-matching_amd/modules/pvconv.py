@@ -13,7 +13,8 @@ import torch.nn as nn
 import torch.nn.functional as TF
 
 import modules.functional as F
-from modules.norm_act import _nbt, _pair_head, _pair_tail, conv_bn_act_pair, pair_fusable
+from modules.norm_act import (_BN_FROM_GEMM, _fusable_pre, _nbt, _pair_head, _pair_tail,
+                              conv_bn_act_pair, pair_fusable)
 from modules.se import SE3d
 from modules.shared_mlp import SharedMLP
 from modules.voxel_conv import VoxelConv3d
@@ -101,22 +102,35 @@ class _SEDevoxAdd(torch.autograd.Function):
 
 
 class _VoxelBranchSEDevox(torch.autograd.Function):
-    """The whole voxel branch of a PVConv with SE in one autograd node:
-    devox(SE(act2(BN2(Conv2(act1(BN1(Conv1(grid)))))))) + pf
-    (pvconv.py:20-39, se.py:6-17).  act2(BN2(.)) is never written: its batch
-    statistics and SE's pooling come from one pass over Conv2's output y2
-    (bn_act_forward_rowmean), and the devoxelization applies BN2 + act2 while
-    staging its rows.  Backward from g = devox_bwd(dout): one pass over (g, y2)
-    gives SE's ds and every BN2 sum (dz = s g + dm / V is linear in s and dm:
-    bn_se_backward_stats), the SE MLP's backward gives dm, and the apply pass
-    writes d y2 as Conv2's split operand (bn_se_backward_apply_split).  Against
-    _Conv3dBnActPair + _SEDevoxAdd: the activation's write, both SE rows_dot
-    passes, the rows_affine pass and BN2's backward statistics pass are gone."""
+    """A PVConv with SE in one autograd node, voxel and point branches:
+    devox(SE(act2(BN2(Conv2(act1(BN1(Conv1(grid)))))))) + ReLU(BN(W f + b))
+    (pvconv.py:20-39, se.py:6-17, shared_mlp.py:15-27).  Neither act2(BN2(.))
+    nor the point branch's ReLU(BN(.)) is ever written: BN2's batch statistics
+    and SE's pooling come from one pass over Conv2's output y2
+    (bn_act_forward_rowmean), the point branch's statistics from its GEMM's
+    epilogue, and the devoxelization applies both BatchNorms + activations as it
+    stages its rows and reads its add operand.  Backward from g = devox_bwd(dout):
+    one pass over (g, y2) gives SE's ds and every BN2 sum (dz = s g + dm / V is
+    linear in s and dm: bn_se_backward_stats), the SE MLP's backward gives dm,
+    and the apply pass writes d y2 as Conv2's split operand
+    (bn_se_backward_apply_split); the point branch's gradient is dout through
+    its BatchNorm + ReLU and GEMM, as _PwBnAct.  Against _Conv3dBnActPair +
+    _SEDevoxAdd + _PwBnAct: both activations' writes, both SE rows_dot passes,
+    the rows_affine pass and BN2's backward statistics pass are gone."""
 
     @staticmethod
     def forward(ctx, x, w1, b1, g1, bt1, rm1, rv1, nbt1, w2, b2, g2, bt2, rm2, rv2, nbt2,
-                sw1, sw2, coords, pf, eps1, mom1, slope1, eps2, mom2, slope2, r, occ=None):
+                sw1, sw2, coords, f, pw, pb, pg, pbt, prm, prv, pnbt, eps1, mom1, slope1, eps2,
+                mom2, slope2, peps, pmom, r, occ=None):
         from pcfm import ops, plans
+        # point branch: y_pf = W f + b, its BatchNorm statistics (the GEMM epilogue's
+        # when the 256-row tile runs); ReLU(BN(y_pf)) is applied inside the gather
+        ys = ops.pointwise_forward_bnstats(f, pw, pb) if _BN_FROM_GEMM else None
+        if ys is not None:
+            y_pf, parts = ys
+        else:
+            y_pf, parts = ops.pointwise_forward(f, pw, pb), None
+        pm, pis = ops.bn_forward_stats(y_pf, peps, pmom, prm, prv, pnbt, parts=parts)
         xs, y1, m1, is1, z1s, y2 = _pair_head(x, w1, b1, g1, bt1, rm1, rv1, nbt1, w2, b2, eps1,
                                               mom1, slope1, occ)
         mse, m2, is2 = ops.bn_act_forward_rowmean(y2, g2, bt2, eps2, slope2, mom2, rm2, rv2,
@@ -125,16 +139,17 @@ class _VoxelBranchSEDevox(torch.autograd.Function):
         s, hid = ops.se_mlp_forward(mse, sw1, sw2)
         shared = plans.devox_corners(coords, r)
         out, inds, wgts = ops.trilinear_devoxelize_bn_scale_add(
-            r, shared is None, coords, y2, m2, is2, g2, bt2, slope2, s, pf)
+            r, shared is None, coords, y2, m2, is2, g2, bt2, slope2, s, y_pf,
+            add_bn=(pm, pis, pg, pbt, 0.0))
         if shared is not None:
             inds, wgts = shared
         else:
             plans.put_devox_corners(coords, r, inds, wgts)
         ctx.save_for_backward(xs, w1, y1, g1, bt1, m1, is1, z1s, w2, y2, g2, bt2, m2, is2,
-                              inds, wgts, mse, s, hid, sw1, sw2)
+                              inds, wgts, mse, s, hid, sw1, sw2, f, pw, y_pf, pg, pbt, pm, pis)
         ctx.points, ctx.r, ctx.occ = coords, r, occ
         ctx.slopes = (slope1, slope2)
-        ctx.has_bias = (b1 is not None, b2 is not None)
+        ctx.has_bias = (b1 is not None, b2 is not None, pb is not None)
         ctx.dims = (x.shape[0], x.shape[1], w1.shape[0], w2.shape[0], x.shape[2])
         return out
 
@@ -142,8 +157,14 @@ class _VoxelBranchSEDevox(torch.autograd.Function):
     def backward(ctx, dout):
         from pcfm import ops, plans
         (xs, w1, y1, g1, bt1, m1, is1, z1s, w2, y2, g2, bt2, m2, is2, inds, wgts, mse, s, hid,
-         sw1, sw2) = ctx.saved_tensors
+         sw1, sw2, f, pw, y_pf, pg, pbt, pm, pis) = ctx.saved_tensors
         dout = dout.contiguous()
+        # point branch (_PwBnAct's backward): ReLU + BatchNorm, then the GEMM's
+        dy_pf, dpg, dpbt, dpb = ops.bn_act_backward(dout, y_pf, pg, pbt, pm, pis, 0.0,
+                                                    want_dbias_in=ctx.has_bias[2])
+        df = ops.pointwise_backward_data(dy_pf, pw) if ctx.needs_input_grad[18] else None
+        dpw = ops.pointwise_backward_weight(f, dy_pf).view_as(pw)
+        del dy_pf
         if plans.ENABLED:
             plan = plans.devox_bwd_plan(ctx.points, inds, wgts, ctx.r)
             g = ops.trilinear_devoxelize_backward_planned(dout, plan)
@@ -161,12 +182,26 @@ class _VoxelBranchSEDevox(torch.autograd.Function):
                                                   ctx.slopes[0], ctx.has_bias[0], ctx.dims,
                                                   ctx.occ, ctx.needs_input_grad[0])
         return (dx, dw1, db1, dg1, dbt1, None, None, None, dw2, db2, dg2, dbt2, None, None, None,
-                dsw1, dsw2, None, dout, None, None, None, None, None, None, None, None)
+                dsw1, dsw2, None, df, dpw, dpb, dpg, dpbt, None, None, None, None, None, None,
+                None, None, None, None, None, None, None)
 
 
 # the voxel branch as one node (PCFM_PV_FUSED=0: the conv pair + the SE devoxelization
 # as two nodes, the round-4 form; A/B knob)
 _PV_FUSED = __import__("os").environ.get("PCFM_PV_FUSED", "1") != "0"
+
+
+def _point_branch_fusable(layers, x) -> bool:
+    """The point branch is one Conv1d(1x1) + BatchNorm1d + ReLU that the fused
+    PVConv node can run (the _PwBnAct conditions of modules/norm_act.py)."""
+    from modules.shared_mlp import PointwiseConv1d
+    if len(layers) != 3 or not isinstance(layers[2], nn.ReLU):
+        return False
+    conv, bn = layers[0], layers[1]
+    return (isinstance(conv, PointwiseConv1d) and isinstance(bn, nn.BatchNorm1d)
+            and _fusable_pre(bn) and conv.x3_ok(x) and conv.bias is not None
+            and x.shape[2] % 4 == 0 and x.shape[0] * conv.out_channels < 65536
+            and x.shape[0] * x.shape[2] > 1)
 
 
 def _se_fused_ok(b, c, w1) -> bool:
@@ -218,23 +253,25 @@ class PVConv(nn.Module):
             # occupied voxels, and its gradient is read back only on them
             from pcfm import plans
             occ = plans.conv_occupancy(self.voxelization._coords(coords)[1], self.resolution)
+        pm = self.point_features.layers
         if (_PV_FUSED and self.training and torch.is_grad_enabled() and len(layers) > 6
-                and grid.is_cuda and pair_fusable(layers[0], layers[1], layers[3], layers[4], grid)):
-            pf = self.point_features(features)
+                and grid.is_cuda and pair_fusable(layers[0], layers[1], layers[3], layers[4], grid)
+                and _point_branch_fusable(pm, features)):
             fc = layers[6].fc
-            if (_se_devox_ok(layers[6], grid, pf) and grid[0, 0].numel() <= 32768
+            if (_se_devox_ok(layers[6], grid, features) and grid[0, 0].numel() <= 32768
                     and _se_fused_ok(grid.shape[0], layers[3].out_channels, fc[0].weight)):
                 c1, n1, c2, n2 = layers[0], layers[1], layers[3], layers[4]
                 out = _VoxelBranchSEDevox.apply(
                     grid.contiguous(), c1.weight, c1.bias, n1.weight, n1.bias, n1.running_mean,
                     n1.running_var, _nbt(n1), c2.weight, c2.bias, n2.weight, n2.bias,
                     n2.running_mean, n2.running_var, _nbt(n2), fc[0].weight, fc[2].weight,
-                    grid_coords, pf, float(n1.eps), float(n1.momentum),
-                    float(layers[2].negative_slope), float(n2.eps), float(n2.momentum),
-                    float(layers[5].negative_slope), self.resolution, occ)
+                    grid_coords, features.contiguous(), pm[0].weight, pm[0].bias, pm[1].weight,
+                    pm[1].bias, pm[1].running_mean, pm[1].running_var, _nbt(pm[1]),
+                    float(n1.eps), float(n1.momentum), float(layers[2].negative_slope),
+                    float(n2.eps), float(n2.momentum), float(layers[5].negative_slope),
+                    float(pm[1].eps), float(pm[1].momentum), self.resolution, occ)
                 return out, coords
-        else:
-            pf = None
+        pf = None
         grid = conv_bn_act_pair(layers[0], layers[1], layers[2].negative_slope,
                                 layers[3], layers[4], layers[5].negative_slope, grid,
                                 voxelized_input_occ=occ)

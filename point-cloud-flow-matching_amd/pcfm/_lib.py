@@ -80,8 +80,10 @@ SIGNATURES = {
     "pcfm_debug_devox_verify": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _P]),
     "pcfm_se_mlp_fwd": (_I, [_P, _P, _P, _I, _I, _I, _P, _P, _P]),
     "pcfm_se_mlp_bwd": (_I, [_P, _P, _P, _P, _P, _P, _I, _I, _I, _F, _P, _P, _P, _P]),
-    "pcfm_trilinear_devoxelize_bn_scale_add_fwd": (_I, [_P, _P, _P, _P, _P, _P, _F, _P, _P, _I,
-                                                       _I, _I, _I, _I, _P, _P, _P, _P]),
+    "pcfm_trilinear_devoxelize_bn_scale_add_fwd": (_I, [_P, _P, _P, _P, _P, _P, _F, _P, _P, _P,
+                                                       _P, _P, _P, _F, _I, _I, _I, _I, _I, _P,
+                                                       _P, _P, _P]),
+    "pcfm_bn_fwd_stats": (_I, [_P, _P, _I, _I, _I, _I, _F, _F, _P, _P, _P, _P, _P, _P, _Z, _P]),
     "pcfm_bn_act_fwd_rowmean_workspace_bytes": (_Z, [_I, _I, _I]),
     "pcfm_bn_act_fwd_rowmean": (_I, [_P, _P, _P, _I, _I, _I, _F, _F, _F, _P, _P, _P, _P, _P, _P,
                                      _P, _Z, _P]),

@@ -1297,9 +1297,11 @@ def bn_act_forward_rowmean(x: torch.Tensor, weight: torch.Tensor, bias: torch.Te
 
 def trilinear_devoxelize_bn_scale_add(r: int, is_training: bool, coords: torch.Tensor,
                                       x: torch.Tensor, mean, invstd, weight, bias, slope: float,
-                                      scale, add):
+                                      scale, add, add_bn=None):
     """trilinear_devoxelize_scale_add of act(bn(x)) with the given batch statistics;
-    the activation is applied as the rows are staged -> [outs, inds, wgts]."""
+    the activation is applied as the rows are staged -> [outs, inds, wgts].
+    add_bn = (mean, invstd, weight, bias, slope) of the add operand: add enters as
+    act(bn(add)) (PVConv's point-branch BatchNorm1d + ReLU, never written)."""
     _check(x, "x", "f")
     _check(coords, "coords", "f")
     b, c = x.shape[0], x.shape[1]
@@ -1331,13 +1333,48 @@ def trilinear_devoxelize_bn_scale_add(r: int, is_training: bool, coords: torch.T
         pi, pw = None, None
     nbytes = 4 * b * (3 * n + c * r ** 3 + c * n * (2 if add is not None else 1)
                       + (16 * n if is_training else 0))
+    abn = [None, None, None, None]
+    aslope = 0.0
+    if add_bn is not None:
+        if add is None:
+            raise ValueError("trilinear_devoxelize_bn_scale_add: add_bn without add")
+        for t in add_bn[:4]:
+            _check(t, "add_bn", "f")
+            if t.numel() != c:
+                raise ValueError("trilinear_devoxelize_bn_scale_add: add_bn entries must have C values")
+        abn = [_ptr(t) for t in add_bn[:4]]
+        aslope = float(add_bn[4])
     with _timed("trilinear_devoxelize_fwd", nbytes, x):
         _lib.call("pcfm_trilinear_devoxelize_bn_scale_add_fwd", _ptr(coords), _ptr(x), _ptr(mean),
                   _ptr(invstd), _ptr(weight), _ptr(bias), float(slope),
                   _ptr(scale) if scale is not None else None,
-                  _ptr(add) if add is not None else None, b, c, n, r, 1 if is_training else 0,
-                  _ptr(outs), pi, pw, _stream(x))
+                  _ptr(add) if add is not None else None, *abn, aslope, b, c, n, r,
+                  1 if is_training else 0, _ptr(outs), pi, pw, _stream(x))
     return [outs, inds, wgts]
+
+
+def bn_forward_stats(x: torch.Tensor, eps: float, momentum: float, running_mean, running_var,
+                     num_batches_tracked=None, parts=None):
+    """BatchNorm batch statistics of x (B, C, ...) only -> (mean, invstd); running stats
+    and the counter updated.  parts: the producer's epilogue statistics
+    (pointwise_forward_bnstats) instead of a statistics pass over x."""
+    _check(x, "input", "f")
+    b, c = x.shape[0], x.shape[1]
+    s = x.numel() // max(1, b * c)
+    stats = torch.empty((2, c), dtype=torch.float32, device=x.device)
+    if parts is not None:
+        _check(parts, "parts", "f")
+        ws = _workspace(1, x)
+        npart, nbytes = int(parts.shape[1]), 0
+    else:
+        ws = _workspace(_lib.query("pcfm_bn_workspace_bytes", b, c, s), x)
+        npart, nbytes = 0, 4 * x.numel()
+    with _timed("bn_act_fwd", nbytes, x):
+        _lib.call("pcfm_bn_fwd_stats", _ptr(x), _ptr(parts) if parts is not None else None,
+                  npart, b, c, s, float(eps), float(momentum), _p(running_mean),
+                  _p(running_var), _p(_counter(num_batches_tracked, x)), _ptr(stats[0]),
+                  _ptr(stats[1]), _ptr(ws), ws.numel(), _stream(x))
+    return stats[0], stats[1]
 
 
 def bn_se_backward_stats(g: torch.Tensor, x: torch.Tensor, mean, invstd, weight, bias,
