@@ -47,7 +47,8 @@ extern "C" {
  * 15: the head FiLM backward takes shift and recomputes u; 16: devoxelization
  * self-check entry point; 17: BatchNorm statistics from the pointwise GEMM's
  * epilogue; 18: fused EMD approxmatch + matchcost, SE3d MLP kernels; 19: PVConv's
- * second BatchNorm fused with SE3d and the devoxelization). */
+ * second BatchNorm fused with SE3d and the devoxelization; 20: the PV block's
+ * post BatchNorm + ReLU fused into its GroupNorm-FiLM residual). */
 int pcfm_abi_version(void);
 /* Thread-local text of the last non-zero return code. */
 const char* pcfm_last_error(void);
@@ -610,6 +611,43 @@ int pcfm_gn_film_res_bwd(const float* dout, const float* x, const float* w, cons
                          const float* gamma, const float* mean, const float* rstd, int b, int c,
                          int n, int groups, float* dx, float* dw, float* dbias, float* dgamma,
                          float* dbeta, void* ws, size_t ws_bytes, void* stream);
+
+/* The PV block's post SharedMLP activation fused into its GroupNorm + FiLM +
+ * residual (models.py:349-368; shared_mlp.py:15-27 for the BatchNorm + ReLU):
+ * the GroupNorm's input is z = act(bn(y)) for y f32 [b][c][n], the post 1x1
+ * conv's output, with the BatchNorm's batch statistics bn_mean / bn_invstd,
+ * affine bn_gamma / bn_beta and act(v) = v > 0 ? v : slope v (slope 0: ReLU)
+ * -- z is computed as pcfm_bn_act_fwd does, bit for bit, and never written:
+ *   out = z + (GroupNorm(z) * (1 + gamma[b]) + beta[b]).
+ * Same workspace as pcfm_gn_film_res_*.  Replaces pcfm_bn_act_fwd(y) followed
+ * by pcfm_gn_film_res_fwd(z). */
+int pcfm_gn_film_res_fwd_bnin(const float* y, const float* bn_mean, const float* bn_invstd,
+                              const float* bn_gamma, const float* bn_beta, float slope,
+                              const float* w, const float* bias, const float* gamma,
+                              const float* beta, int b, int c, int n, int groups, float eps,
+                              float* out, float* mean, float* rstd, void* ws, size_t ws_bytes,
+                              void* stream);
+/* Backward: dz = dL/dz f32 [b][c][n] and the GroupNorm / FiLM gradients as
+ * pcfm_gn_film_res_bwd, plus the BatchNorm backward statistics of
+ * g = dz * act'(bn(y)) -- bnpart f32 [c][P][2] = (sum g, sum g * xhat) over
+ * P = pcfm_gn_bnin_parts(b, n) blocks per channel -- for
+ * pcfm_bn_act_bwd_apply_parts (no separate statistics pass over (dz, y)). */
+int pcfm_gn_bnin_parts(int b, int n);
+int pcfm_gn_film_res_bwd_bnin(const float* dout, const float* y, const float* bn_mean,
+                              const float* bn_invstd, const float* bn_gamma, const float* bn_beta,
+                              float slope, const float* w, const float* bias, const float* gamma,
+                              const float* mean, const float* rstd, int b, int c, int n,
+                              int groups, float* dz, float* dw, float* dbias, float* dgamma,
+                              float* dbeta, float* bnpart, void* ws, size_t ws_bytes,
+                              void* stream);
+/* pcfm_bn_act_bwd's apply pass on given statistics part f32 [c][P][2]
+ * (sum g, sum g * xhat per block): dx, dgamma, dbeta and, when dbias_in is
+ * non-NULL, the producer's bias gradient (ws: pcfm_bn_workspace_bytes). */
+int pcfm_bn_act_bwd_apply_parts(const float* dz, const float* x, const float* gamma,
+                                const float* beta, const float* mean, const float* invstd,
+                                const float* part, int P, int b, int c, int s, float slope,
+                                float* dx, float* dgamma, float* dbeta, float* dbias_in, void* ws,
+                                size_t ws_bytes, void* stream);
 
 /* SiLU(GroupNorm(x; w, bias, groups, eps)) over x f32 [b][c][n] (ContextNet's
  * head_norm + head_act, models.py:460-466); mean/rstd f32 [b][groups]; same

@@ -843,20 +843,65 @@ __global__ void __launch_bounds__(256)
 // ---------------------------------------------------------------------------
 constexpr int kGnParts = 4;  // blocks per (b, group) row set / per (b, c) row
 
+// GroupNorm over the activation of a SharedMLP layer given as its pre-BatchNorm
+// tensor y (the PV block's post layer, models.py:349-368): the GroupNorm reads
+// z = act(bn(y)) = act(fma((y - m) * is, g, bt)) -- bn_act_apply_kernel's
+// arithmetic, so z is bit-identical to the activation it no longer writes.
+struct BnIn {
+  const float* mean;
+  const float* invstd;
+  const float* gamma;
+  const float* beta;
+  float slope;
+};
+struct BnInC {
+  float m, is, g, bt, slope;
+  __device__ __forceinline__ float xh(float v) const { return (v - m) * is; }
+  __device__ __forceinline__ float z(float v) const {
+    return act(__builtin_fmaf((v - m) * is, g, bt), slope);
+  }
+  // the BatchNorm backward's g = dz * act'(bn(y)) (bn_bwd_stats_kernel's form)
+  __device__ __forceinline__ float grad(float v, float dz) const {
+    return __builtin_fmaf(xh(v), g, bt) > 0.0f ? dz : dz * slope;
+  }
+};
+__device__ __forceinline__ BnInC bnin_at(const BnIn& p, int c) {
+  return BnInC{p.mean[c], p.invstd[c], p.gamma[c], p.beta[c], p.slope};
+}
+
 // fwd stats: grid (G * kGnParts, B); part[(b*G + g)*P + p] = (sum (x-K), sum (x-K)^2)
+// IN: over z = act(bn(x)) (BnIn), K = z of the group's first element
+template <bool IN>
 __global__ void __launch_bounds__(256)
-    gn_stats_kernel(const float* __restrict__ x, int C, int N, int G, float* __restrict__ part) {
+    gn_stats_kernel(const float* __restrict__ x, int C, int N, int G, float* __restrict__ part,
+                    BnIn bn = {}) {
   __shared__ float sh[8];
   const int b = blockIdx.y, g = blockIdx.x / kGnParts, p = blockIdx.x % kGnParts;
   const int cpg = C / G, N4 = N / 4;
   const float* base = x + ((size_t)b * C + (size_t)g * cpg) * N;  // cpg rows of N, contiguous
-  const float K = base[0];
+  const float K = IN ? bnin_at(bn, g * cpg).z(base[0]) : base[0];
   const int tot = cpg * N4, chunk = (tot + kGnParts - 1) / kGnParts;
   const int f0 = min(tot, p * chunk), f1 = min(tot, f0 + chunk);
   const float4* x4 = reinterpret_cast<const float4*>(base);
   float s = 0.0f, q = 0.0f;
-  for (int f = f0 + threadIdx.x; f < f1; f += 256) {
-    const float4 v = x4[f];
+  // IN: the thread's current channel (its stride, 256 float4s, is below a row's N4)
+  int f = f0 + threadIdx.x, bnd = 0;
+  BnInC tc{};
+  if (IN && f < f1) {
+    const int cl = f / N4;
+    bnd = (cl + 1) * N4;
+    tc = bnin_at(bn, g * cpg + cl);
+  }
+  for (; f < f1; f += 256) {
+    float4 v = x4[f];
+    if (IN) {
+      if (f >= bnd) {
+        const int cl = f / N4;
+        bnd = (cl + 1) * N4;
+        tc = bnin_at(bn, g * cpg + cl);
+      }
+      v = make_float4(tc.z(v.x), tc.z(v.y), tc.z(v.z), tc.z(v.w));
+    }
     const float d0 = v.x - K, d1 = v.y - K, d2 = v.z - K, d3 = v.w - K;
     s += (d0 + d1) + (d2 + d3);
     q += (d0 * d0 + d1 * d1) + (d2 * d2 + d3 * d3);
@@ -874,7 +919,7 @@ __global__ void __launch_bounds__(256)
                        const float* __restrict__ w, const float* __restrict__ bias,
                        const float* __restrict__ gamma, int B, int C, int N, int G, float eps,
                        float* __restrict__ mean_o, float* __restrict__ rstd_o,
-                       float* __restrict__ coef) {
+                       float* __restrict__ coef, BnIn bn = {}) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= B * C) return;
   const int b = i / C, c = i - b * C, cpg = C / G, g = c / cpg;
@@ -884,7 +929,8 @@ __global__ void __launch_bounds__(256)
     q += part[(((size_t)b * G + g) * kGnParts + p) * 2 + 1];
   }
   const double n = (double)cpg * N;
-  const float K = x[((size_t)b * C + (size_t)g * cpg) * N];
+  float K = x[((size_t)b * C + (size_t)g * cpg) * N];
+  if (bn.mean != nullptr) K = bnin_at(bn, g * cpg).z(K);
   const float md = (float)(s / n);
   const float var = fmaxf((float)(q / n) - md * md, 0.0f);
   const float mean = K + md, rstd = rsqrtf(var + eps);
@@ -924,16 +970,23 @@ __global__ void __launch_bounds__(256)
 }
 
 // out = x + ((x * a + s) * g1 + beta); grid (ceil(N4 / 256), B * C)
+// IN: x -> z = act(bn(x)) first (the residual is z too)
+template <bool IN>
 __global__ void __launch_bounds__(256)
     gn_film_apply_kernel(const float* __restrict__ x, const float* __restrict__ coef,
-                         const float* __restrict__ beta, int N4, float* __restrict__ out) {
+                         const float* __restrict__ beta, int N4, float* __restrict__ out,
+                         int C = 1, BnIn bn = {}) {
   const int n4 = blockIdx.x * 256 + threadIdx.x;
   if (n4 >= N4) return;
   const int row = blockIdx.y;
   const float a = coef[3 * (size_t)row], s = coef[3 * (size_t)row + 1];
   const float g1 = coef[3 * (size_t)row + 2], bt = beta[row];
   const size_t i = (size_t)row * N4 + n4;
-  const float4 v = reinterpret_cast<const float4*>(x)[i];
+  float4 v = reinterpret_cast<const float4*>(x)[i];
+  if (IN) {
+    const BnInC tc = bnin_at(bn, row % C);
+    v = make_float4(tc.z(v.x), tc.z(v.y), tc.z(v.z), tc.z(v.w));
+  }
   float4 o;
   o.x = v.x + (__builtin_fmaf(v.x, a, s) * g1 + bt);
   o.y = v.y + (__builtin_fmaf(v.y, a, s) * g1 + bt);
@@ -948,12 +1001,13 @@ __global__ void __launch_bounds__(256)
 
 // bwd row sums: grid (kGnParts, B * C); part[row * P + p] = (sum dout, sum dout * xhat)
 // ACT (GN + SiLU): the gradient entering GN is dout * SiLU'(x * a + s), recomputed
-template <bool ACT>
+// IN: over z = act(bn(x)) (BnIn)
+template <bool ACT, bool IN = false>
 __global__ void __launch_bounds__(256)
     gn_bwd_stats_kernel(const float* __restrict__ dout, const float* __restrict__ x,
                         const float* __restrict__ mean, const float* __restrict__ rstd,
                         const float* __restrict__ w, const float* __restrict__ bias, int C,
-                        int N, int G, float* __restrict__ part) {
+                        int N, int G, float* __restrict__ part, BnIn bn = {}) {
   __shared__ float sh[8];
   const int row = blockIdx.y, p = blockIdx.x;
   const int b = row / C, c = row - b * C, g = c / (C / G);
@@ -964,8 +1018,11 @@ __global__ void __launch_bounds__(256)
   const float4* x4 = reinterpret_cast<const float4*>(x) + (size_t)row * N4;
   const float4* d4 = reinterpret_cast<const float4*>(dout) + (size_t)row * N4;
   float a2 = 0.0f, a3 = 0.0f;
+  BnInC tc{};
+  if (IN) tc = bnin_at(bn, c);
   for (int f = f0 + threadIdx.x; f < f1; f += 256) {
-    const float4 v = x4[f];
+    float4 v = x4[f];
+    if (IN) v = make_float4(tc.z(v.x), tc.z(v.y), tc.z(v.z), tc.z(v.w));
     float4 d = d4[f];
     if (ACT) {
       d.x *= gn_dsilu(__builtin_fmaf(v.x, ca, cs));
@@ -1040,45 +1097,80 @@ __global__ void __launch_bounds__(1024)
 
 // dx = dout + dout * kc0 - kc1 - xhat * kc2; grid (ceil(N4 / 256), B * C)
 // ACT: dx = dy * kc0 - kc1 - xhat * kc2 with dy = dout * SiLU'(x * a + s) (no residual)
-template <bool ACT>
+// IN (GroupNorm over z = act(bn(x)), the residual z too): dx is dL/dz, and the
+// block's BatchNorm backward sums of g = dx * act'(bn(x)) -- sum g and
+// sum g * xhat_bn, bn_bwd_stats_kernel's terms -- go to bnpart[c][b * nbx + bx]
+// (float2; nbx = gridDim.x): the separate BatchNorm statistics pass over
+// (dL/dz, x) is not needed.
+template <bool ACT, bool IN = false>
 __global__ void __launch_bounds__(256)
     gn_film_bwd_apply_kernel(const float* __restrict__ dout, const float* __restrict__ x,
                              const float* __restrict__ mean, const float* __restrict__ rstd,
                              const float* __restrict__ kc, const float* __restrict__ w,
                              const float* __restrict__ bias, int C, int G, int N4,
-                             float* __restrict__ dx) {
+                             float* __restrict__ dx, BnIn bn = {},
+                             float* __restrict__ bnpart = nullptr) {
   // reverse of the statistics pass's row order (Infinity-cache reuse, as BN)
-  const int n4 = bn_rev(blockIdx.x, gridDim.x) * 256 + threadIdx.x;
-  if (n4 >= N4) return;
+  const unsigned bx = bn_rev(blockIdx.x, gridDim.x);
+  const int n4 = bx * 256 + threadIdx.x;
+  if (!IN && n4 >= N4) return;  // IN: every thread reaches the block sum
   const int row = bn_rev(blockIdx.y, gridDim.y);
   const int b = row / C, c = row - b * C, g = c / (C / G);
   const float m = mean[b * G + g], rs = rstd[b * G + g];
   const float k0 = kc[3 * (size_t)row], k1 = kc[3 * (size_t)row + 1], k2 = kc[3 * (size_t)row + 2];
   const size_t i = (size_t)row * N4 + n4;
-  const float4 v = reinterpret_cast<const float4*>(x)[i];
-  const float4 d = reinterpret_cast<const float4*>(dout)[i];
-  float4 o;
-  if (ACT) {
-    const float ca = rs * w[c], cs = bias[c] - m * ca;
-    const float dy0 = d.x * gn_dsilu(__builtin_fmaf(v.x, ca, cs));
-    const float dy1 = d.y * gn_dsilu(__builtin_fmaf(v.y, ca, cs));
-    const float dy2 = d.z * gn_dsilu(__builtin_fmaf(v.z, ca, cs));
-    const float dy3 = d.w * gn_dsilu(__builtin_fmaf(v.w, ca, cs));
-    o.x = (dy0 * k0 - k1) - ((v.x - m) * rs) * k2;
-    o.y = (dy1 * k0 - k1) - ((v.y - m) * rs) * k2;
-    o.z = (dy2 * k0 - k1) - ((v.z - m) * rs) * k2;
-    o.w = (dy3 * k0 - k1) - ((v.w - m) * rs) * k2;
-  } else {
-    o.x = d.x + ((d.x * k0 - k1) - ((v.x - m) * rs) * k2);
-    o.y = d.y + ((d.y * k0 - k1) - ((v.y - m) * rs) * k2);
-    o.z = d.z + ((d.z * k0 - k1) - ((v.z - m) * rs) * k2);
-    o.w = d.w + ((d.w * k0 - k1) - ((v.w - m) * rs) * k2);
-  }
+  float sg = 0.0f, sgx = 0.0f;
+  if (n4 < N4) {
+    const float4 y = reinterpret_cast<const float4*>(x)[i];
+    float4 v = y;
+    BnInC tc{};
+    if (IN) {
+      tc = bnin_at(bn, c);
+      v = make_float4(tc.z(y.x), tc.z(y.y), tc.z(y.z), tc.z(y.w));
+    }
+    const float4 d = reinterpret_cast<const float4*>(dout)[i];
+    float4 o;
+    if (ACT) {
+      const float ca = rs * w[c], cs = bias[c] - m * ca;
+      const float dy0 = d.x * gn_dsilu(__builtin_fmaf(v.x, ca, cs));
+      const float dy1 = d.y * gn_dsilu(__builtin_fmaf(v.y, ca, cs));
+      const float dy2 = d.z * gn_dsilu(__builtin_fmaf(v.z, ca, cs));
+      const float dy3 = d.w * gn_dsilu(__builtin_fmaf(v.w, ca, cs));
+      o.x = (dy0 * k0 - k1) - ((v.x - m) * rs) * k2;
+      o.y = (dy1 * k0 - k1) - ((v.y - m) * rs) * k2;
+      o.z = (dy2 * k0 - k1) - ((v.z - m) * rs) * k2;
+      o.w = (dy3 * k0 - k1) - ((v.w - m) * rs) * k2;
+    } else {
+      o.x = d.x + ((d.x * k0 - k1) - ((v.x - m) * rs) * k2);
+      o.y = d.y + ((d.y * k0 - k1) - ((v.y - m) * rs) * k2);
+      o.z = d.z + ((d.z * k0 - k1) - ((v.z - m) * rs) * k2);
+      o.w = d.w + ((d.w * k0 - k1) - ((v.w - m) * rs) * k2);
+    }
 #ifdef PCFM_GN_NT_STORE
-  nt_store4(reinterpret_cast<float4*>(dx) + i, o);
+    nt_store4(reinterpret_cast<float4*>(dx) + i, o);
 #else
-  reinterpret_cast<float4*>(dx)[i] = o;
+    reinterpret_cast<float4*>(dx)[i] = o;
 #endif
+    if (IN) {
+      const float yv[4] = {y.x, y.y, y.z, y.w}, ov[4] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float gg = tc.grad(yv[e], ov[e]);
+        sg += gg;
+        sgx += gg * tc.xh(yv[e]);
+      }
+    }
+  }
+  if (IN) {
+    __shared__ float sh[8];
+    block_sum2(sg, sgx, sh);
+    if (threadIdx.x == 0) {
+      const int nbx = (int)gridDim.x, P = (int)(gridDim.y / C) * nbx;
+      float* pp = bnpart + ((size_t)c * P + (size_t)b * nbx + bx) * 2;
+      pp[0] = sg;
+      pp[1] = sgx;
+    }
+  }
 }
 
 bool gn_ok(int b, int c, int n, int g) {
@@ -1353,12 +1445,12 @@ extern "C" int pcfm_gn_film_res_fwd(const float* x, const float* w, const float*
   hipStream_t st = (hipStream_t)stream;
   float* part = (float*)ws;
   float* coef = part + (size_t)b * groups * kGnParts * 2;
-  hipLaunchKernelGGL(gn_stats_kernel, dim3(groups * kGnParts, b), dim3(256), 0, st, x, c, n,
+  hipLaunchKernelGGL(gn_stats_kernel<false>, dim3(groups * kGnParts, b), dim3(256), 0, st, x, c, n,
                      groups, part);
   hipLaunchKernelGGL(gn_finalize_kernel, dim3(ceil_div((long long)b * c, 256)), dim3(256), 0, st,
                      (const float*)part, x, w, bias, gamma, b, c, n, groups, eps, mean, rstd,
                      coef);
-  hipLaunchKernelGGL(gn_film_apply_kernel, dim3(ceil_div(n / 4, 256), b * c), dim3(256), 0, st,
+  hipLaunchKernelGGL(gn_film_apply_kernel<false>, dim3(ceil_div(n / 4, 256), b * c), dim3(256), 0, st,
                      x, (const float*)coef, beta, n / 4, out);
   return check_launch("gn_film_res_fwd");
 }
@@ -1384,6 +1476,98 @@ extern "C" int pcfm_gn_film_res_bwd(const float* dout, const float* x, const flo
   return check_launch("gn_film_res_bwd");
 }
 
+// --- the PV block's post SharedMLP activation fused into its GroupNorm-FiLM
+// residual (models.py:349-368: out = z + GN(z) (1 + gamma) + beta with
+// z = ReLU(BN(y)), y = post's 1x1 conv output): z is never written, and the
+// BatchNorm's backward statistics come out of the GroupNorm backward's apply.
+static bool bnin_ok(const float* m, const float* is, const float* g, const float* bt) {
+  return m != nullptr && is != nullptr && g != nullptr && bt != nullptr;
+}
+
+extern "C" int pcfm_gn_film_res_fwd_bnin(const float* y, const float* bn_mean,
+                                         const float* bn_invstd, const float* bn_gamma,
+                                         const float* bn_beta, float slope, const float* w,
+                                         const float* bias, const float* gamma,
+                                         const float* beta, int b, int c, int n, int groups,
+                                         float eps, float* out, float* mean, float* rstd,
+                                         void* ws, size_t ws_bytes, void* stream) {
+  PCFM_CHECK_ARG(gn_ok(b, c, n, groups), "gn_film_res_fwd_bnin: bad shape b=%d c=%d n=%d groups=%d",
+                 b, c, n, groups);
+  PCFM_CHECK_ARG(bnin_ok(bn_mean, bn_invstd, bn_gamma, bn_beta),
+                 "gn_film_res_fwd_bnin: BatchNorm operands missing");
+  PCFM_CHECK_ARG(ws_bytes >= pcfm_gn_film_workspace_bytes(b, c, n, groups),
+                 "gn_film_res_fwd_bnin: workspace too small");
+  hipStream_t st = (hipStream_t)stream;
+  const BnIn bn{bn_mean, bn_invstd, bn_gamma, bn_beta, slope};
+  float* part = (float*)ws;
+  float* coef = part + (size_t)b * groups * kGnParts * 2;
+  hipLaunchKernelGGL(gn_stats_kernel<true>, dim3(groups * kGnParts, b), dim3(256), 0, st, y, c, n,
+                     groups, part, bn);
+  hipLaunchKernelGGL(gn_finalize_kernel, dim3(ceil_div((long long)b * c, 256)), dim3(256), 0, st,
+                     (const float*)part, y, w, bias, gamma, b, c, n, groups, eps, mean, rstd,
+                     coef, bn);
+  hipLaunchKernelGGL(gn_film_apply_kernel<true>, dim3(ceil_div(n / 4, 256), b * c), dim3(256), 0,
+                     st, y, (const float*)coef, beta, n / 4, out, c, bn);
+  return check_launch("gn_film_res_fwd_bnin");
+}
+
+extern "C" int pcfm_gn_bnin_parts(int b, int n) {
+  if (b <= 0 || n <= 0 || n % 4 != 0) return 0;
+  return b * ceil_div(n / 4, 256);
+}
+
+extern "C" int pcfm_gn_film_res_bwd_bnin(const float* dout, const float* y, const float* bn_mean,
+                                         const float* bn_invstd, const float* bn_gamma,
+                                         const float* bn_beta, float slope, const float* w,
+                                         const float* bias, const float* gamma, const float* mean,
+                                         const float* rstd, int b, int c, int n, int groups,
+                                         float* dz, float* dw, float* dbias, float* dgamma,
+                                         float* dbeta, float* bnpart, void* ws, size_t ws_bytes,
+                                         void* stream) {
+  PCFM_CHECK_ARG(gn_ok(b, c, n, groups), "gn_film_res_bwd_bnin: bad shape b=%d c=%d n=%d groups=%d",
+                 b, c, n, groups);
+  PCFM_CHECK_ARG(bnin_ok(bn_mean, bn_invstd, bn_gamma, bn_beta) && bnpart != nullptr,
+                 "gn_film_res_bwd_bnin: BatchNorm operands missing");
+  PCFM_CHECK_ARG(ws_bytes >= pcfm_gn_film_workspace_bytes(b, c, n, groups),
+                 "gn_film_res_bwd_bnin: workspace too small");
+  hipStream_t st = (hipStream_t)stream;
+  const BnIn bn{bn_mean, bn_invstd, bn_gamma, bn_beta, slope};
+  float* part = (float*)ws;
+  float* kc = part + (size_t)b * c * kGnParts * 2;
+  hipLaunchKernelGGL((gn_bwd_stats_kernel<false, true>), dim3(kGnParts, b * c), dim3(256), 0, st,
+                     dout, y, mean, rstd, w, bias, c, n, groups, part, bn);
+  hipLaunchKernelGGL(gn_bwd_finalize_kernel, dim3(1), dim3(1024), 0, st, (const float*)part, w,
+                     bias, gamma, rstd, b, c, n, groups, kc, dgamma, dbeta, dw, dbias);
+  hipLaunchKernelGGL((gn_film_bwd_apply_kernel<false, true>), dim3(ceil_div(n / 4, 256), b * c),
+                     dim3(256), 0, st, dout, y, mean, rstd, (const float*)kc, w, bias, c, groups,
+                     n / 4, dz, bn, bnpart);
+  return check_launch("gn_film_res_bwd_bnin");
+}
+
+// pcfm_bn_act_bwd's apply pass (+ the producer's bias gradient) on statistics
+// a neighbouring kernel produced: part float2 [c][P] of (sum g, sum g xhat).
+extern "C" int pcfm_bn_act_bwd_apply_parts(const float* dz, const float* x, const float* gamma,
+                                           const float* beta, const float* mean,
+                                           const float* invstd, const float* part, int P, int b,
+                                           int c, int s, float slope, float* dx, float* dgamma,
+                                           float* dbeta, float* dbias_in, void* ws,
+                                           size_t ws_bytes, void* stream) {
+  PCFM_CHECK_ARG(bn_ok(b, c, s), "bn_act_bwd_apply_parts: bad shape b=%d c=%d s=%d", b, c, s);
+  PCFM_CHECK_ARG(part != nullptr && P > 0, "bn_act_bwd_apply_parts: no statistics");
+  const int nch = bn_bwd_blocks(s);
+  PCFM_CHECK_ARG(dbias_in == nullptr || ws_bytes >= (size_t)b * c * nch * sizeof(float),
+                 "bn_act_bwd_apply_parts: workspace too small");
+  hipStream_t st = (hipStream_t)stream;
+  float* rowpart = dbias_in != nullptr ? (float*)ws : nullptr;
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(nch, b * c), dim3(256), 0, st, dz, x, mean, invstd,
+                     gamma, beta, part, P, dgamma, dbeta, c, s / 4,
+                     (float)(1.0 / ((double)b * s)), slope, dx, rowpart);
+  if (dbias_in != nullptr)
+    hipLaunchKernelGGL(bn_bias_finalize_kernel, dim3(ceil_div(c, 4)), dim3(256), 0, st,
+                       (const float*)rowpart, b, c, nch, dbias_in);
+  return check_launch("bn_act_bwd_apply_parts");
+}
+
 // ContextNet head: SiLU(GroupNorm(x)) (models.py:460-466 head_norm + head_act)
 extern "C" int pcfm_gn_silu_fwd(const float* x, const float* w, const float* bias, int b, int c,
                                 int n, int groups, float eps, float* out, float* mean, float* rstd,
@@ -1395,7 +1579,7 @@ extern "C" int pcfm_gn_silu_fwd(const float* x, const float* w, const float* bia
   hipStream_t st = (hipStream_t)stream;
   float* part = (float*)ws;
   float* coef = part + (size_t)b * groups * kGnParts * 2;
-  hipLaunchKernelGGL(gn_stats_kernel, dim3(groups * kGnParts, b), dim3(256), 0, st, x, c, n,
+  hipLaunchKernelGGL(gn_stats_kernel<false>, dim3(groups * kGnParts, b), dim3(256), 0, st, x, c, n,
                      groups, part);
   hipLaunchKernelGGL(gn_finalize_kernel, dim3(ceil_div((long long)b * c, 256)), dim3(256), 0, st,
                      (const float*)part, x, w, bias, nullptr, b, c, n, groups, eps, mean, rstd,

@@ -43,5 +43,5 @@ int allow_big_lds(const void* kernel) {
 
 }  // namespace pcfm
 
-extern "C" int pcfm_abi_version(void) { return 19; }
+extern "C" int pcfm_abi_version(void) { return 20; }
 extern "C" const char* pcfm_last_error(void) { return pcfm::g_err; }

@@ -12,7 +12,7 @@ and the activation run as in the reference.
 import torch
 import torch.nn.functional as F
 
-__all__ = ["bn_act", "conv_bn_act", "gn_film_residual"]
+__all__ = ["bn_act", "conv_bn_act", "gn_film_residual", "post_gn_film_residual"]
 
 # PCFM_DEBUG_CHECKS=1: assert the preconditions of the exact-skip fast paths
 _DEBUG_CHECKS = __import__("os").environ.get("PCFM_DEBUG_CHECKS") == "1"
@@ -344,3 +344,73 @@ def gn_film_residual(x: torch.Tensor, norm, gamma: torch.Tensor, beta: torch.Ten
                                 int(norm.num_groups), float(norm.eps))
     y = norm(x)
     return x + (y * (1.0 + gamma[:, :, None]) + beta[:, :, None])
+
+
+# PCFM_POST_GN_FUSED=0: the PV block's post SharedMLP and GroupNorm-FiLM residual
+# as two nodes (the post activation written, its BatchNorm backward statistics a
+# separate pass)
+_POST_GN_FUSED = __import__("os").environ.get("PCFM_POST_GN_FUSED", "1") != "0"
+
+
+class _PostGNFiLMRes(torch.autograd.Function):
+    """The PV block's tail (models.py:349-368) as one autograd node:
+    z = ReLU(BN(Conv1d_1x1(x))) (SharedMLP, shared_mlp.py:15-27), then
+    out = z + GroupNorm(z) (1 + gamma) + beta.  z is never written -- the
+    GroupNorm kernels compute it from the conv output y as bn_act_forward does,
+    bit for bit -- and the GroupNorm backward's apply pass also sums the
+    BatchNorm's backward statistics, so of the unfused form's passes the
+    BatchNorm apply (read y, write z) and the BatchNorm backward statistics
+    (read dL/dz, y) are gone."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, g_bn, bt_bn, rm, rv, nbt, eps, momentum, slope, gn_w, gn_b, gamma,
+                beta, groups, gn_eps):
+        from pcfm import ops
+        ys = ops.pointwise_forward_bnstats(x, w, b) if _BN_FROM_GEMM else None
+        if ys is not None:
+            y, stats = ys
+            mean, invstd = ops.bn_forward_stats(y, eps, momentum, rm, rv, nbt, parts=stats)
+        else:
+            y = ops.pointwise_forward(x, w, b)
+            mean, invstd = ops.bn_forward_stats(y, eps, momentum, rm, rv, nbt)
+        out, gm, grs = ops.gn_film_res_forward_bnin(y, mean, invstd, g_bn, bt_bn, slope, gn_w,
+                                                    gn_b, gamma, beta, groups, gn_eps)
+        ctx.save_for_backward(x, w, y, g_bn, bt_bn, mean, invstd, gn_w, gn_b, gamma, gm, grs)
+        ctx.slope, ctx.groups, ctx.has_bias = slope, groups, b is not None
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        from pcfm import ops
+        x, w, y, g_bn, bt_bn, mean, invstd, gn_w, gn_b, gamma, gm, grs = ctx.saved_tensors
+        dz, dgnw, dgnb, dgamma, dbeta, bnpart = ops.gn_film_res_backward_bnin(
+            dout, y, mean, invstd, g_bn, bt_bn, ctx.slope, gn_w, gn_b, gamma, gm, grs, ctx.groups)
+        dy, dg_bn, db_bn, db = ops.bn_act_backward_parts(dz, y, g_bn, bt_bn, mean, invstd, bnpart,
+                                                         ctx.slope, want_dbias_in=ctx.has_bias)
+        del dz
+        dx = ops.pointwise_backward_data(dy, w) if ctx.needs_input_grad[0] else None
+        dw = ops.pointwise_backward_weight(x, dy).view_as(w) if ctx.needs_input_grad[1] else None
+        return (dx, dw, db, dg_bn, db_bn, None, None, None, None, None, None, dgnw, dgnb, dgamma,
+                dbeta, None, None)
+
+
+def post_gn_film_residual(post, norm, x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor):
+    """z + GroupNorm(z) (1 + gamma) + beta with z = post(x) for a one-layer
+    SharedMLP `post` (conv, BN, ReLU) and a GroupNorm `norm`: one fused node on
+    the GPU training path (_PostGNFiLMRes), else the two modules' paths."""
+    layers = post.layers
+    conv, bn = layers[0], layers[1]
+    fused = (_POST_GN_FUSED and len(layers) == 3 and isinstance(layers[2], torch.nn.ReLU)
+             and x.is_cuda and x.dtype == torch.float32 and x.dim() == 3
+             and _fusable_pre(bn) and hasattr(conv, "x3_ok") and conv.x3_ok(x)
+             and conv.bias is not None and isinstance(norm, torch.nn.GroupNorm) and norm.affine
+             and x.shape[2] % 4 == 0 and conv.out_channels <= 1024
+             and x.shape[0] * conv.out_channels < 65536 and x.shape[0] * x.shape[2] > 1
+             and conv.out_channels % norm.num_groups == 0
+             and gamma.dtype == torch.float32 and beta.dtype == torch.float32)
+    if not fused:
+        return gn_film_residual(post(x), norm, gamma, beta)
+    return _PostGNFiLMRes.apply(
+        x.contiguous(), conv.weight, conv.bias, bn.weight, bn.bias, bn.running_mean,
+        bn.running_var, _nbt(bn), float(bn.eps), float(bn.momentum), 0.0, norm.weight, norm.bias,
+        gamma, beta, int(norm.num_groups), float(norm.eps))

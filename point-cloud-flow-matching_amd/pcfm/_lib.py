@@ -132,6 +132,13 @@ SIGNATURES = {
                                   _P]),
     "pcfm_gn_film_res_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P,
                                   _P, _P, _Z, _P]),
+    "pcfm_gn_film_res_fwd_bnin": (_I, [_P, _P, _P, _P, _P, _F, _P, _P, _P, _P, _I, _I, _I, _I,
+                                       _F, _P, _P, _P, _P, _Z, _P]),
+    "pcfm_gn_bnin_parts": (_I, [_I, _I]),
+    "pcfm_gn_film_res_bwd_bnin": (_I, [_P, _P, _P, _P, _P, _P, _F, _P, _P, _P, _P, _P, _I, _I,
+                                       _I, _I, _P, _P, _P, _P, _P, _P, _P, _Z, _P]),
+    "pcfm_bn_act_bwd_apply_parts": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _F, _P, _P,
+                                         _P, _P, _P, _Z, _P]),
     "pcfm_seg_plan_bytes": (_Z, [_I, _I, _I, _I]),
     "pcfm_seg_apply_workspace_bytes": (_Z, [_I, _I, _I, _I, _I]),
     "pcfm_avg_voxelize_plan": (_I, [_P, _I, _I, _I, _P, _P, _P, _Z, _P]),
@@ -144,7 +151,7 @@ SIGNATURES = {
     "pcfm_adamw_ema_step": (_I, [_P, _P, _I, _P, _P, _I, _DP, _DP, _D, _D, _D, _D, _P]),
 }
 
-ABI_VERSION = 19
+ABI_VERSION = 20
 
 _lock = threading.Lock()
 _lib = None

@@ -23,7 +23,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from modules.norm_act import bn_act, gn_film_residual, gn_silu
+from modules.norm_act import bn_act, gn_silu, post_gn_film_residual
 from modules.pvconv import PVConv
 from modules.shared_mlp import PointwiseConv1d, SharedMLP
 from pcfm.layers import RowsLinear, fused_trunk, fused_trunk_supported, max_over_points
@@ -334,12 +334,14 @@ class _PVBlock(nn.Module):
                 gb: Optional[Tuple[torch.Tensor, torch.Tensor]] = None):
         """gb: this block's (gamma, beta) = film.affine(emb) precomputed by
         ContextNet with the other blocks' in one batched product."""
-        f, c = self.post(self.pvconv(feat_coords))
+        f, c = self.pvconv(feat_coords)
         film = self.film
         if film.one_plus and isinstance(film.norm, nn.GroupNorm):
-            # f + GroupNorm(f) * (1 + gamma) + beta as one fused op (modules/norm_act.py)
+            # f + GroupNorm(f) * (1 + gamma) + beta with f = post(.) as one fused op
+            # (modules/norm_act.py: the post activation is never written)
             gamma, beta = gb if gb is not None else film.affine(emb.to(f.dtype)).chunk(2, dim=-1)
-            return gn_film_residual(f, film.norm, gamma, beta), c
+            return post_gn_film_residual(self.post, film.norm, f, gamma, beta), c
+        f = self.post(f)
         return f + film(f, emb), c
 
 

@@ -1458,6 +1458,74 @@ def gn_film_res_forward(x, weight, bias, gamma, beta, groups: int, eps: float):
     return out, stats[0], stats[1]
 
 
+def gn_film_res_forward_bnin(y, bn_mean, bn_invstd, bn_weight, bn_bias, slope: float, weight,
+                             bias, gamma, beta, groups: int, eps: float):
+    """gn_film_res_forward over z = act(bn(y)) (the PV block's post SharedMLP
+    activation, computed as bn_act_forward does and never written) -> (out, mean, rstd)"""
+    _check(y, "input", "f")
+    b, c, n = y.shape
+    for t, nm in ((bn_mean, "bn_mean"), (bn_invstd, "bn_invstd"), (bn_weight, "bn_weight"),
+                  (bn_bias, "bn_bias")):
+        _check(t, nm, "f")
+        if t.numel() != c:
+            raise ValueError(f"gn_film_res_forward_bnin: {nm} must have C values")
+    gamma, beta = gamma.contiguous(), beta.contiguous()
+    out = torch.empty_like(y)
+    stats = torch.empty((2, b, groups), dtype=torch.float32, device=y.device)
+    ws = _workspace(_lib.query("pcfm_gn_film_workspace_bytes", b, c, n, groups), y)
+    with _timed("gn_film_res_fwd", 4 * 3 * y.numel(), y):
+        _lib.call("pcfm_gn_film_res_fwd_bnin", _ptr(y), _ptr(bn_mean), _ptr(bn_invstd),
+                  _ptr(bn_weight), _ptr(bn_bias), float(slope), _ptr(weight), _ptr(bias),
+                  _ptr(gamma), _ptr(beta), b, c, n, groups, float(eps), _ptr(out),
+                  _ptr(stats[0]), _ptr(stats[1]), _ptr(ws), ws.numel(), _stream(y))
+    return out, stats[0], stats[1]
+
+
+def gn_film_res_backward_bnin(dout, y, bn_mean, bn_invstd, bn_weight, bn_bias, slope: float,
+                              weight, bias, gamma, mean, rstd, groups: int):
+    """Backward of gn_film_res_forward_bnin -> (dz, dweight, dbias, dgamma (B, C),
+    dbeta (B, C), bnpart (C, P, 2)): dz = dL/dz and the BatchNorm backward
+    statistics for bn_act_backward_parts."""
+    dout = dout.contiguous()
+    b, c, n = y.shape
+    P = _lib.query("pcfm_gn_bnin_parts", b, n)
+    if P <= 0:
+        raise RuntimeError(f"gn_film_res_backward_bnin: unsupported shape {tuple(y.shape)}")
+    dz = torch.empty_like(y)
+    small = torch.empty((2 * c + 2 * b * c,), dtype=torch.float32, device=y.device)
+    dw, dbias = small[:c], small[c:2 * c]
+    dgamma = small[2 * c:2 * c + b * c].view(b, c)
+    dbeta = small[2 * c + b * c:].view(b, c)
+    bnpart = torch.empty((c, P, 2), dtype=torch.float32, device=y.device)
+    ws = _workspace(_lib.query("pcfm_gn_film_workspace_bytes", b, c, n, groups), y)
+    with _timed("gn_film_res_bwd", 4 * 5 * y.numel(), y):
+        _lib.call("pcfm_gn_film_res_bwd_bnin", _ptr(dout), _ptr(y), _ptr(bn_mean),
+                  _ptr(bn_invstd), _ptr(bn_weight), _ptr(bn_bias), float(slope), _ptr(weight),
+                  _ptr(bias), _ptr(gamma.contiguous()), _ptr(mean), _ptr(rstd), b, c, n, groups,
+                  _ptr(dz), _ptr(dw), _ptr(dbias), _ptr(dgamma), _ptr(dbeta), _ptr(bnpart),
+                  _ptr(ws), ws.numel(), _stream(y))
+    return dz, dw, dbias, dgamma, dbeta, bnpart
+
+
+def bn_act_backward_parts(dz: torch.Tensor, x: torch.Tensor, weight, bias, mean, invstd,
+                          part: torch.Tensor, slope: float, want_dbias_in: bool = False):
+    """bn_act_backward's apply pass on statistics a neighbouring kernel produced
+    (part (C, P, 2) of (sum g, sum g * xhat)) -> (dx, dgamma, dbeta, dbias_in or None)."""
+    dz = dz.contiguous()
+    _check(part, "part", "f")
+    b, c = x.shape[0], x.shape[1]
+    s = x.numel() // max(1, b * c)
+    dx = torch.empty_like(x)
+    dgb = torch.empty((3, c), dtype=torch.float32, device=x.device)
+    ws = _workspace(_lib.query("pcfm_bn_workspace_bytes", b, c, s), x)
+    with _timed("bn_act_bwd", 4 * 3 * x.numel(), x):
+        _lib.call("pcfm_bn_act_bwd_apply_parts", _ptr(dz), _ptr(x), _ptr(weight), _ptr(bias),
+                  _ptr(mean), _ptr(invstd), _ptr(part), int(part.shape[1]), b, c, s,
+                  float(slope), _ptr(dx), _ptr(dgb[0]), _ptr(dgb[1]),
+                  _ptr(dgb[2]) if want_dbias_in else None, _ptr(ws), ws.numel(), _stream(x))
+    return dx, dgb[0], dgb[1], (dgb[2] if want_dbias_in else None)
+
+
 def gn_silu_forward(x, weight, bias, groups: int, eps: float):
     """out = SiLU(GroupNorm(x)) -> (out, mean, rstd)"""
     _check(x, "input", "f")

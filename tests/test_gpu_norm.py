@@ -347,3 +347,61 @@ def test_bn_se_backward_matches_composition(ops, b, c, r, slope):
     # deterministic
     rs2 = ops.bn_se_backward_stats(gr, x, mean, invstd, gamma, beta, slope)
     assert torch.equal(rowstats, rs2)
+
+
+def _relerr(a, ref):
+    a, ref = a.detach().double(), ref.detach().double()
+    return ((a - ref).abs().max() / ref.pow(2).mean().sqrt().clamp_min(1e-30)).item()
+
+
+@pytest.mark.parametrize("b,c,n,groups", [(8, 256, 20000, 32), (2, 128, 3000, 32), (3, 64, 36, 8)])
+def test_post_gn_film_fused_matches_two_nodes(ops, monkeypatch, b, c, n, groups):
+    """The PV block's tail as one node (_PostGNFiLMRes: the post SharedMLP's
+    ReLU(BN(.)) read by the GroupNorm kernels from the conv output, never
+    written) against the two-node form (SharedMLP node, then the GroupNorm-FiLM
+    residual node).  The forward computes the same z bit for bit, so the output
+    and running statistics are equal; the BatchNorm backward sums come from the
+    GroupNorm backward's blocks instead of the statistics pass (another
+    summation order): gradients within 1e-5 of the two-node form's (relative to
+    their rms)."""
+    import modules.norm_act as na
+    from modules.shared_mlp import SharedMLP
+    torch.manual_seed(7)
+    post = SharedMLP(c, [c]).cuda()
+    norm = torch.nn.GroupNorm(groups, c, eps=1e-6).cuda()
+    with torch.no_grad():
+        norm.weight.uniform_(0.5, 1.5)
+        norm.bias.uniform_(-0.5, 0.5)
+        post.layers[1].weight.uniform_(0.5, 1.5)
+        post.layers[1].bias.uniform_(-0.5, 0.5)
+    mods = [post, norm]
+    ref = copy.deepcopy(mods)
+    x = torch.randn(b, c, n, device="cuda")
+    gam = (0.2 * torch.randn(b, c, device="cuda")).requires_grad_(True)
+    bet = (0.2 * torch.randn(b, c, device="cuda")).requires_grad_(True)
+    gam2, bet2 = gam.detach().clone().requires_grad_(True), bet.detach().clone().requires_grad_(True)
+    xa, xb = x.clone().requires_grad_(True), x.clone().requires_grad_(True)
+    monkeypatch.setattr(na, "_POST_GN_FUSED", False)
+    oa = na.post_gn_film_residual(ref[0], ref[1], xa, gam2, bet2)
+    monkeypatch.setattr(na, "_POST_GN_FUSED", True)
+    ob = na.post_gn_film_residual(mods[0], mods[1], xb, gam, bet)
+    assert isinstance(ob.grad_fn, na._PostGNFiLMRes._backward_cls)
+    assert not isinstance(oa.grad_fn, na._PostGNFiLMRes._backward_cls)
+    assert torch.equal(oa, ob)
+    go = torch.randn_like(oa)
+    oa.backward(go)
+    ob.backward(go)
+    errs = {"x": _relerr(xb.grad, xa.grad), "gamma": _relerr(gam.grad, gam2.grad),
+            "beta": _relerr(bet.grad, bet2.grad)}
+    for m_ref, m in zip(ref, mods):
+        for (name, p_ref), p in zip(m_ref.named_parameters(), m.parameters()):
+            errs[name] = _relerr(p.grad, p_ref.grad)
+        for (name, b_ref), bb in zip(m_ref.named_buffers(), m.buffers()):
+            assert torch.equal(b_ref, bb), name
+    # the conv bias gradient is sum(dL/dy) behind a training-mode BatchNorm: 0 up to
+    # rounding in both forms, so it is compared on the scale of the weight gradient
+    # (sum dy x^T with x ~ N(0, 1)) instead of its own rms
+    db, db_ref = post.layers[0].bias.grad, ref[0].layers[0].bias.grad
+    errs["layers.0.bias"] = ((db - db_ref).abs().max()
+                             / ref[0].layers[0].weight.grad.pow(2).mean().sqrt()).item()
+    assert max(errs.values()) < 1e-5, errs
