@@ -48,7 +48,8 @@ extern "C" {
  * self-check entry point; 17: BatchNorm statistics from the pointwise GEMM's
  * epilogue; 18: fused EMD approxmatch + matchcost, SE3d MLP kernels; 19: PVConv's
  * second BatchNorm fused with SE3d and the devoxelization; 20: the PV block's
- * post BatchNorm + ReLU fused into its GroupNorm-FiLM residual). */
+ * post BatchNorm + ReLU fused into its GroupNorm-FiLM residual, the devoxelization
+ * self-check of the BatchNorm-transformed gather). */
 int pcfm_abi_version(void);
 /* Thread-local text of the last non-zero return code. */
 const char* pcfm_last_error(void);
@@ -128,6 +129,16 @@ int pcfm_debug_devox_verify(const float* coords, const float* feat, const float*
                             const float* add, const float* out, const int* inds,
                             const float* wgts, int b, int c, int n, int r, int* rec,
                             void* stream);
+/* pcfm_debug_devox_verify for pcfm_trilinear_devoxelize_bn_scale_add_fwd: the
+ * grid rows enter as act(bn(feat)) and, with add_mean non-NULL, the add operand
+ * as act(bn(add)) -- the same transforms, bit for bit. */
+int pcfm_debug_devox_verify_bn(const float* coords, const float* feat, const float* bn_mean,
+                               const float* bn_invstd, const float* bn_gamma,
+                               const float* bn_beta, float slope, const float* scale,
+                               const float* add, const float* add_mean, const float* add_invstd,
+                               const float* add_gamma, const float* add_beta, float add_slope,
+                               const float* out, const int* inds, const float* wgts, int b, int c,
+                               int n, int r, int* rec, void* stream);
 
 /* SE3d's channel MLP (modules/se.py over pvconv.py:35-39; se.py:9-19):
  *   hid [b][h] = relu(m [b][c] . W1^T), W1 [h][c];  s [b][c] = sigmoid(hid . W2^T), W2 [c][h]

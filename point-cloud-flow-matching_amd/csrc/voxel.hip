@@ -96,11 +96,14 @@ __global__ void __launch_bounds__(256)
 // stored weights do not sum to 1 within 1e-5; rec[2 + 8k ..] holds up to 16
 // records {kind, b, c, i, got bits, want bits, lane, i / 64}.
 constexpr int kVerifyRecs = 16;
+// bn / abn (mean != nullptr): the grid rows / the add operand enter as
+// act(bn(.)) (pcfm_trilinear_devoxelize_bn_scale_add_fwd's RowBn transforms)
 __global__ void __launch_bounds__(256)
     devox_verify_kernel(const float* __restrict__ coords, const float* __restrict__ feat,
                         const float* __restrict__ scale, const float* __restrict__ add,
                         const float* __restrict__ out, const int* __restrict__ inds,
-                        const float* __restrict__ wgts, int C, int n, int r, int* __restrict__ rec) {
+                        const float* __restrict__ wgts, int C, int n, int r, int* __restrict__ rec,
+                        RowBn bn = {}, RowBn abn = {}) {
   const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const int b = blockIdx.y;
   if (t >= (long long)C * n) return;
@@ -111,9 +114,20 @@ __global__ void __launch_bounds__(256)
   float w[8];
   prov.get(b, i, false, id, w);
   const float* row = feat + ((size_t)b * C + c) * s;
-  float a = tap_sum<8>(row, id, w);
+  float a;
+  if (bn.mean != nullptr) {  // tap_sum's order on the transformed values
+    const RowBnC tc = row_bn_at(bn, c);
+    a = w[1] * tc(row[id[1]]);
+    a = __builtin_fmaf(w[0], tc(row[id[0]]), a);
+    for (int k = 2; k < 8; ++k) a = __builtin_fmaf(w[k], tc(row[id[k]]), a);
+  } else {
+    a = tap_sum<8>(row, id, w);
+  }
   if (scale != nullptr) a *= scale[(size_t)b * C + c];
-  if (add != nullptr) a += add[((size_t)b * C + c) * n + i];
+  if (add != nullptr) {
+    const float av = add[((size_t)b * C + c) * n + i];
+    a += abn.mean != nullptr ? row_bn_at(abn, c)(av) : av;
+  }
   const float got = out[((size_t)b * C + c) * n + i];
   auto note = [&](int kind, float gv, float wv) {
     const int k = atomicAdd(rec, 1);
@@ -157,6 +171,32 @@ extern "C" int pcfm_debug_devox_verify(const float* coords, const float* feat, c
   hipLaunchKernelGGL(devox_verify_kernel, dim3(ceil_div((long long)c * n, 256), b), dim3(256), 0,
                      (hipStream_t)stream, coords, feat, scale, add, out, inds, wgts, c, n, r, rec);
   return check_launch("debug_devox_verify");
+}
+
+extern "C" int pcfm_debug_devox_verify_bn(const float* coords, const float* feat,
+                                          const float* bn_mean, const float* bn_invstd,
+                                          const float* bn_gamma, const float* bn_beta,
+                                          float slope, const float* scale, const float* add,
+                                          const float* add_mean, const float* add_invstd,
+                                          const float* add_gamma, const float* add_beta,
+                                          float add_slope, const float* out, const int* inds,
+                                          const float* wgts, int b, int c, int n, int r, int* rec,
+                                          void* stream) {
+  int s = 0;
+  PCFM_CHECK_ARG(b >= 0 && c >= 0 && n >= 0 && cube_fits(r, &s) && rec != nullptr &&
+                     bn_mean != nullptr && bn_invstd != nullptr && bn_gamma != nullptr &&
+                     bn_beta != nullptr,
+                 "debug_devox_verify_bn: bad arguments");
+  PCFM_CHECK_ARG(add_mean == nullptr || (add != nullptr && add_invstd != nullptr &&
+                                         add_gamma != nullptr && add_beta != nullptr),
+                 "debug_devox_verify_bn: incomplete BatchNorm operands of add");
+  if ((long long)b * c * n == 0) return PCFM_OK;
+  const RowBn bn{bn_mean, bn_invstd, bn_gamma, bn_beta, slope};
+  const RowBn abn{add_mean, add_invstd, add_gamma, add_beta, add_slope};
+  hipLaunchKernelGGL(devox_verify_kernel, dim3(ceil_div((long long)c * n, 256), b), dim3(256), 0,
+                     (hipStream_t)stream, coords, feat, scale, add, out, inds, wgts, c, n, r, rec,
+                     bn, abn);
+  return check_launch("debug_devox_verify_bn");
 }
 
 extern "C" size_t pcfm_avg_voxelize_fwd_workspace_bytes(int b, int c, int n, int r) {

@@ -132,6 +132,8 @@ SIGNATURES = {
                                   _P]),
     "pcfm_gn_film_res_bwd": (_I, [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P,
                                   _P, _P, _Z, _P]),
+    "pcfm_debug_devox_verify_bn": (_I, [_P, _P, _P, _P, _P, _P, _F, _P, _P, _P, _P, _P, _P, _F,
+                                        _P, _P, _P, _I, _I, _I, _I, _P, _P]),
     "pcfm_gn_film_res_fwd_bnin": (_I, [_P, _P, _P, _P, _P, _F, _P, _P, _P, _P, _I, _I, _I, _I,
                                        _F, _P, _P, _P, _P, _Z, _P]),
     "pcfm_gn_bnin_parts": (_I, [_I, _I]),

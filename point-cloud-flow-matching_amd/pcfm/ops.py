@@ -296,6 +296,23 @@ class _DevoxVerify:
                   _ptr(wgts) if wgts is not None else None, b, c, n, int(r), _ptr(self.rec),
                   _stream(outs))
 
+    def bn(self, coords, features, bn, scale, add, add_bn, outs, inds, wgts, r):
+        """The check for trilinear_devoxelize_bn_scale_add (bn / add_bn: the
+        (mean, invstd, weight, bias, slope) transforms of the rows / the add)."""
+        if self.rec is None or self.rec.device != outs.device:
+            self.rec = torch.zeros(2 + 16 * 8, dtype=torch.int32, device=outs.device)
+        b, c, n = outs.shape
+        self.calls += 1
+        abn = [_ptr(t) for t in add_bn[:4]] if add_bn is not None else [None] * 4
+        aslope = float(add_bn[4]) if add_bn is not None else 0.0
+        _lib.call("pcfm_debug_devox_verify_bn", _ptr(coords), _ptr(features),
+                  *[_ptr(t) for t in bn[:4]], float(bn[4]),
+                  _ptr(scale) if scale is not None else None,
+                  _ptr(add) if add is not None else None, *abn, aslope, _ptr(outs),
+                  _ptr(inds) if inds is not None else None,
+                  _ptr(wgts) if wgts is not None else None, b, c, n, int(r), _ptr(self.rec),
+                  _stream(outs))
+
     def report(self):
         if self.rec is None:
             return {"calls": self.calls, "mismatches": 0, "bad_weight_sums": 0, "records": []}
@@ -1350,6 +1367,9 @@ def trilinear_devoxelize_bn_scale_add(r: int, is_training: bool, coords: torch.T
                   _ptr(scale) if scale is not None else None,
                   _ptr(add) if add is not None else None, *abn, aslope, b, c, n, r,
                   1 if is_training else 0, _ptr(outs), pi, pw, _stream(x))
+    if devox_verify.enabled:
+        devox_verify.bn(coords, x, (mean, invstd, weight, bias, slope), scale, add, add_bn, outs,
+                        inds if is_training else None, wgts if is_training else None, r)
     return [outs, inds, wgts]
 
 
