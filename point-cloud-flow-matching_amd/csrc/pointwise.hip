@@ -1222,13 +1222,20 @@ extern "C" int pcfm_pointwise_prep_weight(const float* w, int cout, int cin, int
 // The forward GEMM's kernel for a shape: ONE decision, used by the launcher
 // and by pcfm_pointwise_bnstats_groups(), so a caller is never told that a
 // shape writes BatchNorm statistics when the kernel that runs does not.
-enum class PwPath { Stream128, Glds256, Tile256, Tile128, Tile64 };
+enum class PwPath { Stream128, StreamM, Glds256, Tile256, Tile128, Tile64 };
 
 static PwPath pw_path(int b, int cin, int cout, int n) {
   const int Mpad = pw_mpad(cout), Kpad = pad_to(cin, kKT);
   const long long big = (long long)ceil_div(n, 128) * (Mpad / 128) * b;
 #ifndef PCFM_PW_NOSTREAM
   if (Mpad == 128 && Kpad <= 256 && cin % 32 == 0 && cout % 32 == 0) return PwPath::Stream128;
+  // M > 128 as 128-row slices of the streaming kernel: opt-in measurement form
+  // (PCFM_PW_STREAM_M=1; re-measured in round 5 with its missing statistics
+  // epilogue reported -- see DESIGN.md section 5)
+  const char* sm = std::getenv("PCFM_PW_STREAM_M");
+  if (sm != nullptr && sm[0] == '1' && Mpad % 128 == 0 && Kpad <= 256 && cin % 32 == 0 &&
+      cout % 32 == 0)
+    return PwPath::StreamM;
 #endif
 #ifndef PCFM_PW_NO256
 #ifndef PCFM_PW_NOGLDS
@@ -1259,7 +1266,7 @@ static int pw_gemm_launch(const Parts& x, const void* wsplit, const float* bias,
   PCFM_CHECK_ARG(stats == nullptr || pw_path_has_stats(path),
                  "pointwise_gemm: BatchNorm statistics requested for a shape whose kernel has "
                  "no statistics epilogue (b=%d cin=%d cout=%d n=%d)", b, cin, cout, n);
-  if (path == PwPath::Stream128) {
+  if (path == PwPath::Stream128 || path == PwPath::StreamM) {
     const uint16_t* wl_img = wh + total;
     const long long tiles = (long long)b * ceil_div(n, 32);
     const size_t lds = (size_t)2 * 128 * (Kpad + 8) * sizeof(uint16_t);
