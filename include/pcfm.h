@@ -530,8 +530,10 @@ int pcfm_bn_act_fwd(const float* x, const float* gamma, const float* beta, int b
  * (shared_mlp.py:21-25: Conv1d -> BatchNorm1d -> ReLU).  For the shapes where
  * pcfm_pointwise_bnstats_groups(b, cin, cout, n) = P > 0,
  * pcfm_pointwise_gemm_bnstats writes y = W x + bias as pcfm_pointwise_gemm and
- * stats f32 [cout][P][2]: per 64-point group (mean, centred sum of squares);
- * pcfm_bn_act_fwd_parts then finalizes them (fixed order, deterministic) and
+ * stats f32 [cout][P][2]: per point group (mean, centred sum of squares) --
+ * 64-point groups (P = b * ceil(n / 64)) from the 256-row tiles, 32-point
+ * groups (P = b * ceil(n / 32)) from the 128-row streaming form (the group size
+ * follows from P); pcfm_bn_act_fwd_parts then finalizes them (fixed order, deterministic) and
  * applies the BatchNorm + activation like pcfm_bn_act_fwd, without a
  * statistics pass over y. */
 int pcfm_pointwise_bnstats_groups(int b, int cin, int cout, int n);
@@ -574,7 +576,7 @@ int pcfm_bn_act_fwd_split(const float* x, const float* gamma, const float* beta,
 /* BatchNorm batch statistics only (mean, invstd; running stats and the counter
  * updated as pcfm_bn_act_fwd): from x by a statistics pass (part NULL; workspace
  * pcfm_bn_workspace_bytes), or finalized from a producer's epilogue statistics
- * part [c][P] (pcfm_pointwise_gemm_bnstats, P = b * ceil(s / 64)). */
+ * part [c][P] (pcfm_pointwise_gemm_bnstats, P = b * ceil(s / 64) or b * ceil(s / 32)). */
 int pcfm_bn_fwd_stats(const float* x, const float* part, int P, int b, int c, int s, float eps,
                       float momentum, float* running_mean, float* running_var,
                       long long* num_batches_tracked, float* mean, float* invstd, void* ws,

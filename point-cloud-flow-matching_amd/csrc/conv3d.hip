@@ -917,6 +917,230 @@ __device__ __forceinline__ void glds16_asm(const void* g, uint32_t lds) {
 }
 
 // ---------------------------------------------------------------------------
+// Small-grid form (r <= 8, the split-K launches): a 256-voxel tile's 27 taps
+// read rows of ONE window of the channels-last input, voxels [v0 - H, v0 + 256
+// + H) with H = r^2 + r + 1 (416 rows at r = 8), so the window is staged once
+// per 32-channel chunk and every tap reads its B fragments at row offset
+// H + dx r^2 + dy r + dz of it.  conv3_igemm_glds_kernel instead DMAs the
+// tile's 256 shifted rows at every tap: at r = 8 its 6 LDS-DMA pieces per wave
+// per step (issue cost, MI355X_MICROARCH.md) against 24 MFMAs set the pace.
+// Here a step moves only the weight slice (2 pieces per wave).  A neighbour
+// outside the volume (the window holds the linear-index neighbour there) is
+// zeroed in registers per lane and tap (the 27-bit validity masks of the
+// LDS-DMA kernel).  Same tile, waves, split-K partition (whole chunks per
+// split), step order (chunk-major, taps 0..26) and MFMA order as
+// conv3_igemm_glds_kernel, whose zero rows give the same zero products: the
+// results are bit-identical to it (tests/test_gpu_conv3d.py).
+// ---------------------------------------------------------------------------
+constexpr int kWinRowsMax = 416;  // 256 + 2 (r^2 + r + 1) rounded up to 16 rows (r = 8)
+#ifndef PCFM_CONV_WIN_STAGES
+#define PCFM_CONV_WIN_STAGES 3  // 6: 56.0 vs 53.0 us at C256 r = 8 (tools/conv_ab.py)
+#endif
+constexpr int kWinStages = PCFM_CONV_WIN_STAGES;  // weight slices in flight + 1
+
+__host__ __device__ constexpr int win_rows(int r) {
+  return ((kGN + 2 * (r * r + r + 1)) + 15) / 16 * 16;
+}
+
+__global__ void __launch_bounds__(512)
+    conv3_igemm_win_kernel(const uint16_t* __restrict__ xh, const uint16_t* __restrict__ wh,
+                           const float* __restrict__ bias, float* __restrict__ y, int K, int M,
+                           int R, int S, float* __restrict__ part) {
+  using G = GK<32, kGN>;
+  constexpr int kAStage = 2 * G::A;                 // weight slice hi | lo: 16 KiB
+  constexpr int kWinImg = kWinRowsMax * G::RB;      // 26 KiB per image
+  constexpr int NS = kWinStages;                    // weight ring depth
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  uint8_t* win = lds;                               // [hi | lo] window images
+  uint8_t* aring = lds + 2 * kWinImg;               // kGStages weight stages
+  const int V = R * R * R, R2 = R * R, H = R2 + R + 1, WR = win_rows(R);
+  const int nmt = M / kGM, nvt = V / kGN;
+  int id = (int)blockIdx.x;
+  {
+    const int nwg = (int)gridDim.x, q = nwg / 8, rr = nwg % 8, xcd = id % 8;
+    id = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + id / 8;
+  }
+  const int nb = (int)gridDim.x / (S * nmt * nvt);
+  const int m0 = (id % nmt) * kGM;
+  id /= nmt;
+  const int v0 = (id % nvt) * kGN;
+  id /= nvt;
+  const int b = id % nb, sp = id / nb;
+  const int nch = K / 32;                             // 32-channel chunks
+  const int ch0 = nch * sp / S, ch1 = nch * (sp + 1) / S;  // whole chunks (nch % S == 0)
+  const int t = threadIdx.x, lane = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int wr = w / 4, wc = w % 4, r = lane & 31, h = lane >> 5;
+  const int prow = lane / G::CPR, pch = lane % G::CPR;
+  const size_t bV = (size_t)b * V;
+  const uint32_t lds_win = lds_addr(win), lds_ring = lds_addr(aring);
+
+  // weight pieces of this wave: I = 2 w + q (image I / API), as the LDS-DMA kernel
+  const uint16_t* abase[G::APW];
+#pragma unroll
+  for (int q = 0; q < G::APW; ++q) {
+    const int I = G::APW * w + q;
+    const int row = (I % G::API) * G::RPP + prow;
+    abase[q] = wh + (kSplitLo * (I / G::API)) + (size_t)(m0 + row) * 2 * K +
+               ((pch ^ G::swz(row)) << 3);
+  }
+  // this lane's two B columns (j): tap validity, and their window row H + col
+  uint32_t bval[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int v = v0 + wc * 64 + j * 32 + r;
+    const int x = v / R2, yy = (v / R) % R, z = v % R;
+    const uint32_t ax = (x > 0 ? 1u : 0u) | 2u | (x + 1 < R ? 4u : 0u);
+    const uint32_t ay = (yy > 0 ? 1u : 0u) | 2u | (yy + 1 < R ? 4u : 0u);
+    const uint32_t az = (z > 0 ? 1u : 0u) | 2u | (z + 1 < R ? 4u : 0u);
+    uint32_t m = 0u;
+#pragma unroll
+    for (int tp = 0; tp < 27; ++tp)
+      m |= (((ax >> (tp / 9)) & (ay >> ((tp / 3) % 3)) & (az >> (tp % 3))) & 1u) << tp;
+    bval[j] = m;
+  }
+
+  auto issue_a = [&](int c0, int tap, int slot) {
+    const int cof = ((c0 >> 5) << 6) + (c0 & 31);
+    const size_t aofs = (size_t)tap * M * 2 * K + cof;
+#pragma unroll
+    for (int q = 0; q < G::APW; ++q) {
+      const int I = G::APW * w + q;
+      glds16_asm(abase[q] + aofs,
+                 lds_ring + slot * kAStage + (I / G::API) * G::A + (I % G::API) * 1024);
+    }
+  };
+  // the window of chunk c0: WR rows x 2 images in 1-KiB pieces (16 rows), dealt
+  // round-robin to the waves; rows outside the batch volume are clamped (their
+  // products are masked)
+  const int wpieces = 2 * (WR / 16);
+  auto issue_win = [&](int c0) {
+    const int cof = ((c0 >> 5) << 6) + (c0 & 31);
+    for (int P = w; P < wpieces; P += 8) {  // wave-uniform loop
+      const int img = P / (WR / 16), pr = P % (WR / 16);
+      const int row = pr * 16 + prow;
+      const int gv = min(max(v0 - H + row, 0), V - 1);
+      const uint16_t* src =
+          xh + kSplitLo * img + (bV + gv) * 2 * K + cof + ((pch ^ G::swz(row)) << 3);
+      glds16_asm(src, lds_win + img * kWinImg + pr * 1024);
+    }
+  };
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
+
+  for (int ch = ch0; ch < ch1; ++ch) {
+    const int c0 = ch * 32;
+    if (ch > ch0) {
+      // every wave is done with the previous chunk's window and weight stages
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
+    issue_win(c0);
+#pragma unroll
+    for (int q = 0; q < NS - 1; ++q) issue_a(c0, q, q);
+    // B fragments (from the window, which stays put during the chunk) read one
+    // step ahead: step s + 1's while step s's MFMAs run
+    auto read_b = [&](int s, bf16x8 (&Bf)[2][4]) {
+      const int dx = s / 9 - 1, dy = (s / 3) % 3 - 1, dz = s % 3 - 1;
+      const int toff = H + dx * R2 + dy * R + dz;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int kc = 2 * kk + h;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int row = wc * 64 + j * 32 + r + toff;
+          const int off = row * G::RB + ((kc ^ G::swz(row)) << 4);
+          uint4 u0 = *reinterpret_cast<const uint4*>(win + off);
+          uint4 u1 = *reinterpret_cast<const uint4*>(win + kWinImg + off);
+          const uint32_t mk = ((bval[j] >> s) & 1u) ? 0xFFFFFFFFu : 0u;
+          u0.x &= mk; u0.y &= mk; u0.z &= mk; u0.w &= mk;
+          u1.x &= mk; u1.y &= mk; u1.z &= mk; u1.w &= mk;
+          Bf[kk][j] = __builtin_bit_cast(bf16x8, u0);
+          Bf[kk][2 + j] = __builtin_bit_cast(bf16x8, u1);
+        }
+      }
+    };
+    auto step = [&](int s, const bf16x8 (&Bc)[2][4], bf16x8 (&Bn)[2][4]) {
+      // this wave's pieces of step s (and the window) landed; step s + 1's stay
+      // in flight; the barrier makes everyone's visible and ends the reads of
+      // step s - 1, whose stage step s + 2 refills
+      // this wave's weight pieces of step s landed, the later ones issued so far
+      // (min(NS - 2, 26 - s) steps) stay in flight
+      switch (min(NS - 2, 26 - s)) {
+        case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+        case 1: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G::APW) : "memory"); break;
+        case 2: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * G::APW) : "memory"); break;
+        case 3: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * G::APW) : "memory"); break;
+        default: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * G::APW) : "memory"); break;
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (s + NS - 1 < 27) issue_a(c0, s + NS - 1, (s + NS - 1) % NS);
+      const uint8_t* ab = aring + (s % NS) * kAStage;
+      if (s + 1 < 27) read_b(s + 1, Bn);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int kc = 2 * kk + h;
+        bf16x8 ah[2], al[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const int row = wr * 64 + i * 32 + r;
+          const int off = row * G::RB + ((kc ^ G::swz(row)) << 4);
+          ah[i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(ab + off));
+          al[i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(ab + G::A + off));
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], Bc[kk][j], acc[i][j], 0, 0, 0);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], Bc[kk][2 + j], acc[i][j], 0, 0, 0);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], Bc[kk][j], acc[i][j], 0, 0, 0);
+      }
+    };
+    // the window landed (this wave's pieces: everything but step 1's weights),
+    // then everyone's: step 0's B fragments
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NS - 1) * G::APW) : "memory");
+    __builtin_amdgcn_s_barrier();
+    bf16x8 B0[2][4], B1[2][4];
+    read_b(0, B0);
+    int s = 0;
+    for (; s + 1 < 27; s += 2) {
+      step(s, B0, B1);
+      step(s + 1, B1, B0);
+    }
+    step(s, B0, B1);  // s = 26
+  }
+  float* __restrict__ yb = S == 1 ? y + (size_t)b * M * V : part + ((size_t)sp * nb + b) * M * V;
+  float biasv[2][16];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) load_bias16(S == 1 ? bias : nullptr, m0 + wr * 64 + i * 32, h, M, biasv[i]);
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int m = m0 + wr * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
+        nt_st(acc[i][j][e] + biasv[i][e], yb + (size_t)m * V + v0 + wc * 64 + j * 32 + r);
+      }
+}
+
+// ---------------------------------------------------------------------------
 // Forward / backward-data, SLAB form (r = 32, 16; dense unsplit launches).
 // Same tile (128 m x 256 voxels, 8 waves of 64 x 64), K-steps (32 channels,
 // chunk-major, taps 0..26 in order: the accumulation order of
@@ -2213,6 +2437,13 @@ static bool conv_slab() {
   return e == nullptr || e[0] != '0';
 }
 
+// Window form of the small-grid split-K launches (PCFM_CONV_WIN=0: the
+// LDS-DMA kernel that refetches B per tap)
+static bool conv_win() {
+  const char* e = getenv("PCFM_CONV_WIN");  // read per call: tests compare both forms
+  return e == nullptr || e[0] != '0';
+}
+
 static bool list_gn128(long long blocks256) {
   static const int mode = [] {
     const char* e = getenv("PCFM_CONV_LIST_GN");
@@ -2304,6 +2535,20 @@ static int igemm_cl(const void* xs, const void* wsplit, const float* bias, int b
       else
         hipLaunchKernelGGL(conv3_igemm_slab_kernel<16>, dim3((unsigned)glds_blocks), dim3(512),
                            SlabGeo<16>::LDS, st, xh, wh, zrow, bias, y, cin, cout);
+      return check_launch("conv3d_igemm_cl");
+    }
+    if (mm == 0 && vl == nullptr && cin % 32 == 0 && r <= 8 && win_rows(r) <= kWinRowsMax &&
+        (cin / 32) % S == 0 && conv_win()) {
+      const size_t lds = 2 * (size_t)kWinRowsMax * 64 + (size_t)kWinStages * 2 * kGM * 64;
+      const int e = allow_big_lds((const void*)conv3_igemm_win_kernel);
+      if (e) return e;
+      hipLaunchKernelGGL(conv3_igemm_win_kernel, dim3((unsigned)glds_blocks), dim3(512), lds, st,
+                         xh, wh, bias, y, cin, cout, r, S, part);
+      if (S > 1) {
+        const long long total4 = (long long)b * cout * V / 4;
+        hipLaunchKernelGGL(conv3_ksum_kernel, dim3((unsigned)ceil_div(total4, 256)), dim3(256), 0,
+                           st, (const float*)part, bias, S, cout, V, total4, y);
+      }
       return check_launch("conv3d_igemm_cl");
     }
     if (S == 1 && PCFM_CONV_GK == 32 && cin % 32 == 0 && vl == nullptr && conv_pp()) {

@@ -187,7 +187,8 @@ __device__ __forceinline__ void bn_bwd_fin(const float* part, int P, int c, floa
 
 // Statistics from a producer's epilogue (pw_gemm256_kernel with stats): part
 // float2 [C][P], the (mean, centred sum of squares) of P groups of up to 64
-// values, group p holding min(64, S - (p % G) 64) values (G = ceil(S / 64)).
+// values, group p holding min(gsz, S - (p % G) gsz) values (G = ceil(S / gsz);
+// gsz 64 from the 256-row tiles, 32 from the 128-row streaming form).
 // Four waves per channel: thread t combines groups t, t + 256, ... in order
 // (Chan's update, fp64; 4 groups' loads in flight at a time), then a fixed xor
 // tree per wave and the 4 wave results in wave order; thread 0 publishes mean /
@@ -209,9 +210,9 @@ __global__ void __launch_bounds__(256)
     bn_fin_parts_kernel(const float2* __restrict__ part, int P, int S, float eps, float momentum,
                         float* __restrict__ rmean, float* __restrict__ rvar,
                         long long* __restrict__ nbt, float* __restrict__ mean,
-                        float* __restrict__ invstd) {
+                        float* __restrict__ invstd, int gsz = 64) {
   const int c = blockIdx.x, t = threadIdx.x, l = t & 63, w = t >> 6;
-  const int G = (S + 63) / 64;
+  const int G = (S + gsz - 1) / gsz;
   double n = 0.0, mu = 0.0, m2 = 0.0;
   const float2* __restrict__ pc = part + (size_t)c * P;
   int p = t;
@@ -221,7 +222,7 @@ __global__ void __launch_bounds__(256)
     for (int u = 0; u < 4; ++u) v[u] = pc[p + u * 256];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const double nb = (double)min(64, S - ((p + u * 256) % G) * 64);
+      const double nb = (double)min(gsz, S - ((p + u * 256) % G) * gsz);
       const double nn = n + nb, d = (double)v[u].x - mu;
       mu += d * nb / nn;
       m2 += (double)v[u].y + d * d * n * nb / nn;
@@ -230,7 +231,7 @@ __global__ void __launch_bounds__(256)
   }
   for (; p < P; p += 256) {
     const float2 v = pc[p];
-    const double nb = (double)min(64, S - (p % G) * 64);
+    const double nb = (double)min(gsz, S - (p % G) * gsz);
     const double nn = n + nb, d = (double)v.x - mu;
     mu += d * nb / nn;
     m2 += (double)v.y + d * d * n * nb / nn;
@@ -1178,6 +1179,15 @@ bool gn_ok(int b, int c, int n, int g) {
          (long long)b * c < 65536 && (long long)(c / g) * n / 4 < (1LL << 31);
 }
 
+// group size of a producer's epilogue statistics: P = b * ceil(s / gsz) groups
+// per channel, gsz 64 (256-row pointwise tiles) or 32 (128-row streaming form);
+// 0 when P matches neither
+int parts_gsz(int P, int b, int s) {
+  if (P == b * ceil_div(s, 64)) return 64;
+  if (P == b * ceil_div(s, 32)) return 32;
+  return 0;
+}
+
 bool bn_ok(int b, int c, int s) {
   return b > 0 && c > 0 && s > 0 && s % 4 == 0 && (long long)b * c < 65536 &&
          (long long)b * c * s < (1LL << 40);
@@ -1223,15 +1233,16 @@ extern "C" int pcfm_bn_act_fwd_parts(const float* x, const float* part, int P, c
                                      float* running_var, long long* num_batches_tracked, float* y,
                                      float* mean, float* invstd, void* stream) {
   PCFM_CHECK_ARG(bn_ok(b, c, s), "bn_act_fwd_parts: bad shape b=%d c=%d s=%d", b, c, s);
-  PCFM_CHECK_ARG(part != nullptr && P == b * ceil_div(s, 64),
-                 "bn_act_fwd_parts: need b * ceil(s / 64) = %d groups per channel, got %d",
-                 b * ceil_div(s, 64), P);
+  const int gsz = parts_gsz(P, b, s);
+  PCFM_CHECK_ARG(part != nullptr && gsz > 0,
+                 "bn_act_fwd_parts: need b * ceil(s / 64) = %d or b * ceil(s / 32) = %d groups "
+                 "per channel, got %d", b * ceil_div(s, 64), b * ceil_div(s, 32), P);
   PCFM_CHECK_ARG((running_mean == nullptr) == (running_var == nullptr),
                  "bn_act_fwd_parts: running_mean and running_var must both be given or both NULL");
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(bn_fin_parts_kernel, dim3(c), dim3(256), 0, st,
                      reinterpret_cast<const float2*>(part), P, s, eps, momentum, running_mean,
-                     running_var, num_batches_tracked, mean, invstd);
+                     running_var, num_batches_tracked, mean, invstd, gsz);
   const BnFwdFin fin{nullptr, b, s, 0, eps, momentum, running_mean, running_var, nullptr};
   hipLaunchKernelGGL(bn_act_apply_kernel, dim3(bn_apply_blocks(s), b * c), dim3(256), 0, st, x,
                      fin, mean, invstd, gamma, beta, c, s / 4, slope, y);
@@ -1331,12 +1342,13 @@ extern "C" int pcfm_bn_fwd_stats(const float* x, const float* part, int P, int b
                  "bn_fwd_stats: running_mean and running_var must both be given or both NULL");
   hipStream_t st = (hipStream_t)stream;
   if (part != nullptr) {  // the producer's epilogue statistics (pcfm_pointwise_gemm_bnstats)
-    PCFM_CHECK_ARG(P == b * ceil_div(s, 64),
-                   "bn_fwd_stats: need b * ceil(s / 64) = %d groups per channel, got %d",
-                   b * ceil_div(s, 64), P);
+    const int gsz = parts_gsz(P, b, s);
+    PCFM_CHECK_ARG(gsz > 0,
+                   "bn_fwd_stats: need b * ceil(s / 64) = %d or b * ceil(s / 32) = %d groups "
+                   "per channel, got %d", b * ceil_div(s, 64), b * ceil_div(s, 32), P);
     hipLaunchKernelGGL(bn_fin_parts_kernel, dim3(c), dim3(256), 0, st,
                        reinterpret_cast<const float2*>(part), P, s, eps, momentum, running_mean,
-                       running_var, num_batches_tracked, mean, invstd);
+                       running_var, num_batches_tracked, mean, invstd, gsz);
   } else {
     PCFM_CHECK_ARG(ws_bytes >= pcfm_bn_workspace_bytes(b, c, s), "bn_fwd_stats: workspace too small");
     float* wp = (float*)ws;

@@ -468,11 +468,16 @@ __device__ __forceinline__ void pw_stream_load(const Parts& x, int b, int c0, in
     }
 }
 
-template <int NCH>  // Kpad / 32
+// stats != nullptr: per output channel m and 32-point group g of batch element
+// b (one wave's tile), the group's mean and centred sum of squares go to
+// stats[m * P + b * ceil(N / 32) + g] -- the 256-row tile's epilogue statistics
+// (pw256_epilogue) at 32-point groups.
+template <int NCH, bool ST = false>  // Kpad / 32; ST: the statistics epilogue
 __global__ void __launch_bounds__(kSW * 64)
     pw_stream128_kernel(const Parts x, const uint16_t* __restrict__ wh,
                         const uint16_t* __restrict__ wl, const float* __restrict__ bias,
-                        int bias_bstride, const Parts y, int K, int M, int N, int B) {
+                        int bias_bstride, const Parts y, int K, int M, int N, int B,
+                        float2* __restrict__ stats) {
   extern __shared__ __attribute__((aligned(16))) uint16_t sa[];  // [2][128][Kpad + 8]
   constexpr int Kpad = 32 * NCH, ldr = Kpad + 8, cpr = Kpad / 8;
   const int t = threadIdx.x, lane = t & 63;
@@ -647,6 +652,37 @@ __global__ void __launch_bounds__(kSW * 64)
         if (p < N) {
 #pragma unroll
           for (int e = 0; e < 16; ++e) out_store(yl + ((e & 3) + 8 * (e >> 2)) * N, acc[i][e] + bv[e]);
+        }
+        if (ST) {
+          const int p0 = p - n, nv = min(32, N - p0);
+          const int ngroups = (N + 31) / 32, P = B * ngroups;
+          const bool ok = p < N;
+          float v[32], sr = 0.0f;
+#pragma unroll
+          for (int e = 0; e < 16; ++e) {
+            const float v0 = acc[i][e] + bv[e];
+            const float s0 = __builtin_bit_cast(
+                float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v0), 0));
+            const float s1 = __builtin_bit_cast(
+                float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v0), 32));
+            const float sh = h ? s1 : s0;  // row (e, h)'s value at point p0
+            sr = n == e ? sh : sr;
+            const float d0 = ok ? v0 - sh : 0.0f;
+            v[e] = d0;
+            v[16 + e] = d0 * d0;
+          }
+          xpose_reduce_stage<32, 16>(v, n & 16);
+          xpose_reduce_stage<16, 8>(v, n & 8);
+          xpose_reduce_stage<8, 4>(v, n & 4);
+          xpose_reduce_stage<4, 2>(v, n & 2);
+          xpose_reduce_stage<2, 1>(v, n & 1);
+          const float q = swz_xor<16>(v[0]);
+          const int m = mg + (n & 3) + 8 * ((n >> 2) & 3) + 4 * h;
+          if (n < 16 && m < M) {
+            const float a = v[0], mu_s = a / (float)nv;
+            stats[(size_t)m * P + b * ngroups + p0 / 32] =
+                make_float2(sr + mu_s, fmaxf(__builtin_fmaf(-a, mu_s, q), 0.0f));
+          }
         }
       }
     }
@@ -1251,8 +1287,16 @@ static PwPath pw_path(int b, int cin, int cout, int n) {
   return big >= 2 * kCUs ? PwPath::Tile128 : PwPath::Tile64;
 }
 
-// Only the 256-row tiles have the statistics epilogue.
-static bool pw_path_has_stats(PwPath p) { return p == PwPath::Tile256 || p == PwPath::Glds256; }
+// The 256-row tiles (64-point groups) and the 128-row streaming form (32-point
+// groups) have the statistics epilogue.
+static bool pw_path_has_stats(PwPath p) {
+  if (p == PwPath::Stream128) {  // PCFM_PW_STREAM_STATS=0: measurement switch
+    const char* e = std::getenv("PCFM_PW_STREAM_STATS");
+    return PCFM_PW_STREAM_PF < 2 && (e == nullptr || e[0] != '0');
+  }
+  return p == PwPath::Tile256 || p == PwPath::Glds256;
+}
+static int pw_stats_group(PwPath p) { return p == PwPath::Stream128 ? 32 : 64; }
 
 static int pw_gemm_launch(const Parts& x, const void* wsplit, const float* bias, int bias_bstride,
                           int b, int cin, int cout, int n, const Parts& y, hipStream_t st,
@@ -1277,16 +1321,20 @@ static int pw_gemm_launch(const Parts& x, const void* wsplit, const float* bias,
     const int grid = (int)std::max(1LL, std::min((tiles + kSW - 1) / kSW, cap));
     const void* kfn = nullptr;
     switch (Kpad / 32) {
-#define PW_STREAM_CASE(NC) \
-  case NC: kfn = (const void*)pw_stream128_kernel<NC>; break;
+#define PW_STREAM_CASE(NC)                                                                 \
+  case NC:                                                                                 \
+    kfn = stats != nullptr ? (const void*)pw_stream128_kernel<NC, true>                    \
+                           : (const void*)pw_stream128_kernel<NC, false>;                  \
+    break;
       PW_STREAM_CASE(1) PW_STREAM_CASE(2) PW_STREAM_CASE(3) PW_STREAM_CASE(4)
       PW_STREAM_CASE(5) PW_STREAM_CASE(6) PW_STREAM_CASE(7) PW_STREAM_CASE(8)
 #undef PW_STREAM_CASE
     }
     const int e = allow_big_lds(kfn);
     if (e) return e;
-    void* args[] = {(void*)&x, (void*)&wh, (void*)&wl_img, (void*)&bias, (void*)&bias_bstride,
-                    (void*)&y, (void*)&cin, (void*)&cout, (void*)&n, (void*)&b};
+    void* args[] = {(void*)&x,    (void*)&wh,  (void*)&wl_img, (void*)&bias,
+                    (void*)&bias_bstride, (void*)&y, (void*)&cin, (void*)&cout,
+                    (void*)&n,    (void*)&b,   (void*)&stats};
     const hipError_t le = hipLaunchKernel(kfn, dim3(grid, slices), dim3(kSW * 64), args, lds, st);
     if (le != hipSuccess) {
       set_error("pointwise_gemm: launch failed");
@@ -1349,9 +1397,10 @@ extern "C" int pcfm_pointwise_gemm(const float* x, const void* wsplit, const flo
 // group): stats float2 [cout][b * ceil(n / 64)] (mean, centred sum of squares);
 // pcfm_pointwise_bnstats_groups() > 0 for the shapes that take this path.
 extern "C" int pcfm_pointwise_bnstats_groups(int b, int cin, int cout, int n) {
-  if (!pw_ok(b, cin, cout, n) || b <= 0 || n <= 0 || !pw_path_has_stats(pw_path(b, cin, cout, n)))
-    return 0;
-  return b * ceil_div(n, 64);
+  if (!pw_ok(b, cin, cout, n) || b <= 0 || n <= 0) return 0;
+  const PwPath p = pw_path(b, cin, cout, n);
+  if (!pw_path_has_stats(p)) return 0;
+  return b * ceil_div(n, pw_stats_group(p));
 }
 
 extern "C" int pcfm_pointwise_gemm_bnstats(const float* x, const void* wsplit, const float* bias,

@@ -56,14 +56,20 @@ def test_invalid_arguments_rejected_on_host():
                   0, None)
 
 
-def test_pointwise_bnstats_request_on_a_path_without_statistics_fails():
+def test_pointwise_bnstats_request_on_a_path_without_statistics_fails(monkeypatch):
     """The forward GEMM's shape -> kernel choice is one function (pointwise.hip
-    pw_path); only the 256-row tile writes BatchNorm statistics.  A statistics
-    request for a shape that takes another kernel is refused on the host
-    (nothing launched), instead of returning with the stats buffer unwritten."""
+    pw_path); the 256-row tiles (64-point groups) and the 128-row streaming form
+    (32-point groups) write BatchNorm statistics, the 128 / 64-row tiles do not.
+    A statistics request for a shape that takes such a kernel is refused on the
+    host (nothing launched), instead of returning with the stats buffer
+    unwritten."""
     lib = _lib.load()
     assert lib.pcfm_pointwise_bnstats_groups(8, 256, 256, 20000) == 8 * 313
-    for shape in ((8, 128, 128, 20000),   # the streaming 128-row form
+    assert lib.pcfm_pointwise_bnstats_groups(8, 128, 128, 20000) == 8 * 625
+    monkeypatch.setenv("PCFM_PW_STREAM_STATS", "0")  # the streaming form without its epilogue
+    assert lib.pcfm_pointwise_bnstats_groups(8, 128, 128, 20000) == 0
+    monkeypatch.delenv("PCFM_PW_STREAM_STATS")
+    for shape in ((8, 100, 128, 20000),   # ragged K: the 128-row tile
                   (1, 256, 256, 512)):    # too few tiles for the 256-row tile
         assert lib.pcfm_pointwise_bnstats_groups(*shape) == 0
         rc = lib.pcfm_pointwise_gemm_bnstats(None, None, None, *shape, None, None, None)

@@ -145,3 +145,43 @@ def test_slab_form_padding_counts(ops, r):
     n1 = 3 - (idx == 0).int() - (idx == r - 1).int()
     cnt = (n1[:, None, None] * n1[None, :, None] * n1[None, None, :]).float() * c
     assert torch.equal(y[0, 0], cnt) and torch.equal(y[0, c - 1], cnt)
+
+
+@pytest.mark.parametrize("b,cin,cout,r", [(8, 256, 256, 8), (2, 256, 128, 8), (4, 128, 256, 8),
+                                          (3, 128, 128, 8)])
+def test_window_form_is_bit_identical(ops, monkeypatch, b, cin, cout, r):
+    """The window form of the small-grid split-K GEMM (conv3_igemm_win_kernel: B
+    for all 27 taps from one staged window of the input per 32-channel chunk) runs
+    the LDS-DMA kernel's K-steps in the same order with the same operands (zeroed
+    fragments where that kernel reads its zero row): forward and backward-data
+    outputs bit-identical, incl. the border voxels, and the fp64 pin."""
+    g = torch.Generator(device="cuda").manual_seed(11 * r + cin + cout)
+    x = torch.randn(b, cin, r, r, r, device="cuda", generator=g)
+    w = torch.randn(cout, cin, 3, 3, 3, device="cuda", generator=g) / (27 * cin) ** 0.5
+    bias = torch.randn(cout, device="cuda", generator=g)
+    xs = ops.conv3d_split(x)
+    img, imgt = ops.conv3d_prep_weight(w, False), ops.conv3d_prep_weight(w, True)
+    gys = ops.conv3d_split(torch.randn(b, cout, r, r, r, device="cuda", generator=g))
+    out = {}
+    for win in ("1", "0"):
+        monkeypatch.setenv("PCFM_CONV_WIN", win)
+        out[win] = (ops.conv3d_igemm_split(xs, img, bias, b, cin, cout, r, "t"),
+                    ops.conv3d_igemm_split(gys, imgt, None, b, cout, cin, r, "t"))
+    assert torch.equal(out["1"][0], out["0"][0])
+    assert torch.equal(out["1"][1], out["0"][1])
+    y64 = torch.nn.functional.conv3d(x.double().cpu(), w.double().cpu(), bias.double().cpu(),
+                                     padding=1)
+    assert _rel(out["1"][0], y64) < TOL
+
+
+def test_window_form_padding_counts(ops):
+    """All-ones input and kernel at r = 8: every output is the number of in-grid
+    neighbours times C (the masked linear-index neighbours at all six faces)."""
+    c, r = 256, 8
+    x = torch.ones(2, c, r, r, r, device="cuda")
+    w = torch.ones(c, c, 3, 3, 3, device="cuda")
+    y = ops.conv3d_forward(x, w, None)
+    idx = torch.arange(r, device="cuda")
+    n1 = 3 - (idx == 0).int() - (idx == r - 1).int()
+    cnt = (n1[:, None, None] * n1[None, :, None] * n1[None, None, :]).float() * c
+    assert torch.equal(y[0, 0], cnt) and torch.equal(y[1, c - 1], cnt)

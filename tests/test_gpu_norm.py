@@ -360,10 +360,14 @@ def test_post_gn_film_fused_matches_two_nodes(ops, monkeypatch, b, c, n, groups)
     ReLU(BN(.)) read by the GroupNorm kernels from the conv output, never
     written) against the two-node form (SharedMLP node, then the GroupNorm-FiLM
     residual node).  The forward computes the same z bit for bit, so the output
-    and running statistics are equal; the BatchNorm backward sums come from the
-    GroupNorm backward's blocks instead of the statistics pass (another
-    summation order): gradients within 1e-5 of the two-node form's (relative to
-    their rms)."""
+    and running statistics are equal.  The BatchNorm backward sums come from the
+    GroupNorm backward's blocks instead of the statistics pass (another summation
+    order): every gradient within 1e-5 of the two-node form's in norm
+    (||d|| / ||ref||) and 1e-4 in max |d| / rms; the conv bias, 0 up to rounding
+    behind a training-mode BatchNorm, on the weight gradient's scale.  (An fp64
+    evaluation is no reference here: at 4e7 elements some ReLU inputs round to the
+    other side of 0 in fp32, moving single gradient entries by O(1) in both
+    forms alike.)"""
     import modules.norm_act as na
     from modules.shared_mlp import SharedMLP
     torch.manual_seed(7)
@@ -388,20 +392,25 @@ def test_post_gn_film_fused_matches_two_nodes(ops, monkeypatch, b, c, n, groups)
     assert isinstance(ob.grad_fn, na._PostGNFiLMRes._backward_cls)
     assert not isinstance(oa.grad_fn, na._PostGNFiLMRes._backward_cls)
     assert torch.equal(oa, ob)
+    for m_ref, m in zip(ref, mods):
+        for (name, b_ref), bb in zip(m_ref.named_buffers(), m.buffers()):
+            assert torch.equal(b_ref, bb), name
     go = torch.randn_like(oa)
     oa.backward(go)
     ob.backward(go)
-    errs = {"x": _relerr(xb.grad, xa.grad), "gamma": _relerr(gam.grad, gam2.grad),
-            "beta": _relerr(bet.grad, bet2.grad)}
-    for m_ref, m in zip(ref, mods):
-        for (name, p_ref), p in zip(m_ref.named_parameters(), m.parameters()):
-            errs[name] = _relerr(p.grad, p_ref.grad)
-        for (name, b_ref), bb in zip(m_ref.named_buffers(), m.buffers()):
-            assert torch.equal(b_ref, bb), name
-    # the conv bias gradient is sum(dL/dy) behind a training-mode BatchNorm: 0 up to
-    # rounding in both forms, so it is compared on the scale of the weight gradient
-    # (sum dy x^T with x ~ N(0, 1)) instead of its own rms
-    db, db_ref = post.layers[0].bias.grad, ref[0].layers[0].bias.grad
-    errs["layers.0.bias"] = ((db - db_ref).abs().max()
-                             / ref[0].layers[0].weight.grad.pow(2).mean().sqrt()).item()
-    assert max(errs.values()) < 1e-5, errs
+    conv, bn = post.layers[0], post.layers[1]
+    names = ["x", "conv.weight", "conv.bias", "bn.weight", "bn.bias", "gn.weight", "gn.bias",
+             "gamma", "beta"]
+    got_u = [xa.grad, ref[0].layers[0].weight.grad, ref[0].layers[0].bias.grad,
+             ref[0].layers[1].weight.grad, ref[0].layers[1].bias.grad, ref[1].weight.grad,
+             ref[1].bias.grad, gam2.grad, bet2.grad]
+    got_f = [xb.grad, conv.weight.grad, conv.bias.grad, bn.weight.grad, bn.bias.grad,
+             norm.weight.grad, norm.bias.grad, gam.grad, bet.grad]
+    report = {}
+    for nm, gu, gf in zip(names, got_u, got_f):
+        d = (gf.double() - gu.double())
+        scale = got_u[1].double() if nm == "conv.bias" else gu.double()
+        rel_norm = (d.norm() / scale.norm().clamp_min(1e-30)).item()
+        rel_max = (d.abs().max() / scale.pow(2).mean().sqrt().clamp_min(1e-30)).item()
+        report[nm] = (rel_norm, rel_max)
+        assert rel_norm < 1e-5 and rel_max < 1e-4, (nm, report)
