@@ -23,7 +23,6 @@
 #include <algorithm>
 #include <cstdlib>
 #include <mutex>
-#include <type_traits>
 
 #include "mfma_x3.hpp"
 
@@ -2103,13 +2102,6 @@ __global__ void __launch_bounds__(kW3Threads)
       const uint32_t m0 = (dz < 0 && z0 == 0) ? (mall & 0xFFFF0000u) : mall;
       const uint32_t m3 = (dz > 0 && z0 + 8 == R) ? (mall & 0x0000FFFFu) : mall;
       bf16x8 ah[2], al[2], bh[2], bl[2];
-#ifdef PCFM_EXP_WG3_NOLDS
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const uint4 u = make_uint4(lane + kk, m0, mall, m3 + i);
-        ah[i] = al[i] = bh[i] = bl[i] = __builtin_bit_cast(bf16x8, u);
-      }
-#else
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         ah[i] = tr_operand_rows(iAh, kk * 16, wr * 64 + i * 32, lane);
@@ -2122,22 +2114,6 @@ __global__ void __launch_bounds__(kW3Threads)
         bl[j] = mask_k8(tr_operand_rows(iBl, kk * 16 + 1 + dz, wc * 64 + j * 32, lane), m0, mall,
                         m3);
       }
-#endif
-#ifdef PCFM_EXP_WG3_NOMFMA
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const uint4 a = __builtin_bit_cast(uint4, ah[i]), c = __builtin_bit_cast(uint4, al[i]);
-          const uint4 bb = __builtin_bit_cast(uint4, bh[j]), d = __builtin_bit_cast(uint4, bl[j]);
-          acc[i][j][kk & 15] += __builtin_bit_cast(
-              float, (a.x ^ a.y ^ a.z ^ a.w ^ c.x ^ c.y ^ c.z ^ c.w ^ bb.x ^ bb.y ^ bb.z ^ bb.w ^
-                      d.x ^ d.y ^ d.z ^ d.w) & 0x3FFFFFFFu);
-        }
-    }
-    if (false) {
-      bf16x8 ah[2], al[2], bh[2], bl[2];
-#endif
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -2170,301 +2146,6 @@ __global__ void __launch_bounds__(kW3Threads)
         const int ci = ci0 + wc * 64 + j * 32 + r;
         pb[(size_t)co * cin + ci] = acc[i][j][e];
       }
-}
-
-// ---------------------------------------------------------------------------
-// The three-tap weight gradient on one wave per SIMD (opt-in PCFM_WGRAD3P=1).
-// Same block tile (128 cout x 128 cin x the three dz taps of one (dx, dy)),
-// the same LDS images and the same chunk order as conv3_wgrad3_kernel, but
-// each of the 4 waves owns one 64x64 quadrant for ALL three dz: the dY
-// fragments of a K-slice (the A operand, the same rows for every dz) are read
-// from LDS once for three taps, so a 64-voxel step reads 256 KiB of LDS
-// instead of 384 KiB; each wave holds 12 accumulators (192 registers).  With
-// one wave per SIMD nothing else hides latency, so the step is software-
-// pipelined in 12 groups (K-slice kk, dz) of 12 MFMAs: group g's MFMAs run
-// while group g + 1's fragments are read -- across the step boundary too: the
-// barrier of step st sits before its last group's MFMAs, which cover the first
-// reads of step st + 1 -- and the rows of step st + 2 are loaded into registers
-// (buffer loads, one fixed 32-bit lane offset per piece; no LDS-DMA issue cost
-// on the only wave of the SIMD) a piece or two per group, each stored to LDS
-// in the same group of step st + 1.  Every accumulator sees its MFMAs in
-// conv3_wgrad3_kernel's order (chunks, slices, hi*hi, hi*lo, lo*hi), so the
-// partials are bit-identical to it (tests/test_gpu_conv3d.py).
-// Measured (round 5, profiles/r05_ab_wgrad_one_wave.jsonl): 634 vs 616 us at
-// C128 R32 (B = 8) for the 12-wave form; with the loads and stores removed
-// 480 us, with neither loads nor fragment reads 364 us (the 12-wave form's
-// figure too: the MFMA-issue floor of both).  Forcing the next group's reads
-// ahead of the MFMAs (sched_group_barrier) made it slower (710 us), later
-// (after 8 MFMAs) 648 us.  The staging and the one wave's exposed LDS latency
-// cost more than the third of the fragment reads it saves: opt-in.
-// ---------------------------------------------------------------------------
-constexpr int kW3PThreads = 256;
-
-constexpr int kW3PQ = (kW3Pieces + 3) / 4;  // 1-KiB pieces per wave per step (17)
-
-__global__ void __launch_bounds__(kW3PThreads)
-    conv3_wgrad3p_kernel(const uint16_t* __restrict__ xh, const uint16_t* __restrict__ gh,
-                         int B, int cin, int cout, int R, int S, float* __restrict__ part,
-                         const int* __restrict__ lists, const int* __restrict__ counts, int cap) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  const int V = R * R * R, R2 = R * R;
-  const int nco = cout / kMT;
-  int id = (int)blockIdx.x;
-  {
-    const int nwg = (int)gridDim.x, q = nwg / 8, rr = nwg % 8, xcd = id % 8;
-    id = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + id / 8;
-  }
-  const int pair = id % 9;
-  id /= 9;
-  const int sp = id % S;
-  id /= S;
-  const int co0 = (id % nco) * kMT;
-  const int ci0 = (id / nco) * kMT;
-  const int cpb = V / kWV, nchunk = B * cpb;
-  const int* __restrict__ lst = lists != nullptr ? lists + (size_t)(pair * S + sp) * cap : nullptr;
-  const int nst = lists != nullptr ? counts[pair * S + sp]
-                                   : (sp < nchunk ? (nchunk - sp + S - 1) / S : 0);
-  const int dx = pair / 3 - 1, dy_ = pair % 3 - 1;
-  const int off = dx * R2 + dy_ * R;
-
-  const int t = threadIdx.x, lane = t & 63;
-  const int w = __builtin_amdgcn_readfirstlane(t >> 6);  // 0..3
-  const int wr = w >> 1, wc = w & 1;
-  const int h = lane >> 5;
-  const int lgR = 31 - __builtin_clz(R);
-
-  // the step's rows: piece I = w + 4 q (conv3_wgrad3_kernel's pieces), lane ->
-  // row 4 P + lane / 16, LDS chunk lane % 16 holding logical chunk
-  // (lane % 16) ^ swizzle, i.e. the bytes its LDS-DMA would have written
-  StageVec<kW3PQ> stg;  // not a uint4 array: hipcc puts one captured by a lambda in scratch
-  // piece q (< kW3PQ; the last one only for waves 0, 1) of the step of chunk c,
-  // through buffer descriptors sized to the tensors: a 32-bit lane offset per
-  // piece (fixed) plus a wave-uniform step offset, and no clamping -- an X row
-  // before the first voxel (negative offset) or past the last is read as 0, one
-  // of the next batch item's volume is real data; both are masked at use
-  const __amdgpu_buffer_rsrc_t rgy = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<uint16_t*>(gh), (short)0, B * V * 4 * cout, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<uint16_t*>(xh), (short)0, B * V * 4 * cin, 0x00020000);
-  int lpart[kW3PQ];
-#pragma unroll
-  for (int q = 0; q < kW3PQ; ++q) {
-    const int I = w + 4 * q;
-    const bool isA = I < 2 * kW3APieces;
-    const int I2 = isA ? I : I - 2 * kW3APieces;
-    const int np = isA ? kW3APieces : kW3BPieces;
-    const int img = I2 / np, P = I2 % np;
-    const int row = 4 * P + (lane >> 4);
-    const int ch = (lane & 15) ^ (((row & 3) << 2) | ((row >> 2) & 3));
-    const int cc = (isA ? co0 : ci0) + ch * 8;
-    const int cof = ((cc >> 5) << 6) + (cc & 31) + (img ? kSplitLo : 0);
-    lpart[q] = (row * 2 * (isA ? cout : cin) + cof) * 2;
-  }
-  auto load_piece = [&](int q, int c) __attribute__((always_inline)) {
-    const int b = c / cpb, v0 = (c % cpb) * kWV;
-    uint4 v;
-    if (w + 4 * q < 2 * kW3APieces) {
-      v = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
-                                        rgy, lpart[q] + (b * V + v0) * 4 * cout, 0, 0));
-    } else {
-      v = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(
-                                        rx, lpart[q] + (b * V + v0 + off - 1) * 4 * cin, 0, 0));
-    }
-    sv_put<kW3PQ>(stg, q, v);
-  };
-  auto store_piece = [&](int q, uint8_t* buf) __attribute__((always_inline)) {
-    const int I = w + 4 * q;
-    const bool isA = I < 2 * kW3APieces;
-    const int I2 = isA ? I : I - 2 * kW3APieces;
-    const int np = isA ? kW3APieces : kW3BPieces;
-    const int img = I2 / np, P = I2 % np;
-    uint8_t* dst = buf + (isA ? img * kW3AImg : 2 * kW3AImg + img * kW3BImg) + P * 1024;
-    *reinterpret_cast<uint4*>(dst + lane * 16) = sv_get<kW3PQ>(stg, q);
-  };
-  const bool last_piece = w + 4 * (kW3PQ - 1) < kW3Pieces;  // wave-uniform
-  auto load_step = [&](int c) __attribute__((always_inline)) {
-#pragma unroll
-    for (int q = 0; q < kW3PQ - 1; ++q) load_piece(q, c);
-    if (last_piece) load_piece(kW3PQ - 1, c);
-  };
-  auto store_step = [&](uint8_t* buf) __attribute__((always_inline)) {
-#pragma unroll
-    for (int q = 0; q < kW3PQ - 1; ++q) store_piece(q, buf);
-    if (last_piece) store_piece(kW3PQ - 1, buf);
-  };
-  // K-slice kk's fragments of the step at v0 in buf: the dY pair (hi, lo) of
-  // both row tiles, and per dz the X pair of both column tiles (masked)
-  auto load_a = [&](bf16x8 (&ah)[2], bf16x8 (&al)[2], const uint8_t* buf, int kk) __attribute__((always_inline)) {
-#ifdef PCFM_EXP_W3P_NOLDS
-    ah[0] = ah[1] = al[0] = al[1] = __builtin_bit_cast(bf16x8, make_uint4(lane, kk, 1, 2));
-    return;
-#endif
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      ah[i] = tr_operand_rows(buf, kk * 16, wr * 64 + i * 32, lane);
-      al[i] = tr_operand_rows(buf + kW3AImg, kk * 16, wr * 64 + i * 32, lane);
-    }
-  };
-  // (raw: the tap's masks are applied right before the MFMAs, so that reading
-  // the next group's fragments never waits for them)
-  auto load_b = [&](bf16x8 (&bh)[2], bf16x8 (&bl)[2], uint32_t (&m)[3], const uint8_t* buf,
-                    int v0, int kk, int d) __attribute__((always_inline)) {
-    const uint8_t* iBh = buf + 2 * kW3AImg;
-    const int vk = v0 + kk * 16 + 8 * h;
-    const int xq = vk >> (2 * lgR), yq = (vk >> lgR) & (R - 1), z0 = vk & (R - 1);
-    const bool xyok = (unsigned)(xq + dx) < (unsigned)R && (unsigned)(yq + dy_) < (unsigned)R;
-    const uint32_t mall = xyok ? 0xFFFFFFFFu : 0u;
-    m[0] = (d == 0 && z0 == 0) ? (mall & 0xFFFF0000u) : mall;
-    m[1] = mall;
-    m[2] = (d == 2 && z0 + 8 == R) ? (mall & 0x0000FFFFu) : mall;
-#ifdef PCFM_EXP_W3P_NOLDS
-    bh[0] = bh[1] = bl[0] = bl[1] = __builtin_bit_cast(bf16x8, make_uint4(lane, kk, d, 2));
-    return;
-#endif
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      bh[j] = tr_operand_rows(iBh, kk * 16 + d, wc * 64 + j * 32, lane);
-      bl[j] = tr_operand_rows(iBh + kW3BImg, kk * 16 + d, wc * 64 + j * 32, lane);
-    }
-  };
-
-  f32x16 acc[3][2][2];
-#pragma unroll
-  for (int d = 0; d < 3; ++d)
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) acc[d][i][j][e] = 0.0f;
-  // the 12 MFMAs of (slice, dz): hi*hi, hi*lo, lo*hi per accumulator
-  auto mfmas = [&](f32x16 (&c)[2][2], const bf16x8 (&ah)[2], const bf16x8 (&al)[2],
-                   const bf16x8 (&bhr)[2], const bf16x8 (&blr)[2], const uint32_t (&m)[3]) __attribute__((always_inline)) {
-    bf16x8 bh[2], bl[2];
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      bh[j] = mask_k8(bhr[j], m[0], m[1], m[2]);
-      bl[j] = mask_k8(blr[j], m[0], m[1], m[2]);
-    }
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-        c[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], c[i][j], 0, 0, 0);
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-        c[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], c[i][j], 0, 0, 0);
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-        c[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], c[i][j], 0, 0, 0);
-  };
-
-  auto chunk_of = [&](int st) __attribute__((always_inline)) { return lst != nullptr ? lst[st] : sp + st * S; };
-  // fragment registers: A of the current / next slice, B of the current / next group
-  bf16x8 ah[2][2], al[2][2], bh[2][2], bl[2][2];
-  uint32_t bm[2][3];
-  int cur_c = nst > 0 ? chunk_of(0) : 0;
-  if (nst > 0) {
-    load_step(cur_c);
-    store_step(lds);
-    if (nst > 1) load_step(chunk_of(1));
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    load_a(ah[0], al[0], lds, 0);
-    load_b(bh[0], bl[0], bm[0], lds, (cur_c % cpb) * kWV, 0, 0);
-  }
-  for (int st = 0; st < nst; ++st) {
-    const uint8_t* cur = lds + (st & 1) * kW3Buf;
-    uint8_t* nxt = lds + ((st + 1) & 1) * kW3Buf;
-    const int v0 = (cur_c % cpb) * kWV;
-    const bool more = st + 1 < nst;
-    const int next_c = more ? chunk_of(st + 1) : 0;
-    // step st + 1's rows (in registers since step st - 1) into the free buffer,
-    // then step st + 2's rows into the registers
-    // step st + 2's chunk (clamped to the last: its rows are loaded and stored
-    // to the free buffer unused, so the pieces need no branches)
-    const int c2 = chunk_of(min(st + 2, nst - 1));
-    // 12 groups (slice kk, dz d) of 12 MFMAs; group g's MFMAs run while group
-    // g + 1's fragments are read.  Register sets: A by slice parity, B by group parity.
-    // (the groups as a generic lambda over compile-time g: loops this large are
-    // not fully unrolled, and a runtime piece index puts the staging vector in scratch)
-    auto group = [&](auto gc) __attribute__((always_inline)) {
-        constexpr int g = decltype(gc)::value;
-        constexpr int kk = g / 3, d = g % 3;
-        constexpr int ca = kk & 1, cb = g & 1;
-#ifndef PCFM_EXP_W3P_NOLOAD
-        // staging: piece q of step st + 1 (loaded during step st - 1) into the
-        // free buffer, then piece q of step st + 2 into its registers -- 17
-        // pieces over the 12 groups (2, 2, 2, 2, 2, then 1 each), between MFMAs
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          const int q = g < 5 ? 2 * g + u : 10 + (g - 5);
-          if ((u == 0 || g < 5) && q < kW3PQ - 1) {
-            store_piece(q, nxt);
-            load_piece(q, c2);
-          } else if ((u == 0 || g < 5) && q == kW3PQ - 1 && last_piece) {
-            store_piece(q, nxt);
-            load_piece(q, c2);
-          }
-        }
-#endif
-        if constexpr (g == 11) {
-          // every wave's last fragments of this step and its stores of step
-          // st + 1 are in place: the buffers swap
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          __builtin_amdgcn_s_barrier();
-          asm volatile("" ::: "memory");
-          if (more) {
-            const int nv0 = (next_c % cpb) * kWV;
-            load_a(ah[ca ^ 1], al[ca ^ 1], nxt, 0);
-            load_b(bh[cb ^ 1], bl[cb ^ 1], bm[cb ^ 1], nxt, nv0, 0, 0);
-          }
-        } else if constexpr (d < 2) {
-          load_b(bh[cb ^ 1], bl[cb ^ 1], bm[cb ^ 1], cur, v0, kk, d + 1);
-        } else {
-          load_a(ah[ca ^ 1], al[ca ^ 1], cur, kk + 1);
-          load_b(bh[cb ^ 1], bl[cb ^ 1], bm[cb ^ 1], cur, v0, kk + 1, 0);
-        }
-        // the reads above stay above (the IR may not sink them to their use in
-        // the next group), the MFMAs below stay in this group
-        asm volatile("" ::: "memory");
-        mfmas(acc[d], ah[ca], al[ca], bh[cb], bl[cb], bm[cb]);
-        __builtin_amdgcn_sched_barrier(0);
-    };
-    group(std::integral_constant<int, 0>{});
-    group(std::integral_constant<int, 1>{});
-    group(std::integral_constant<int, 2>{});
-    group(std::integral_constant<int, 3>{});
-    group(std::integral_constant<int, 4>{});
-    group(std::integral_constant<int, 5>{});
-    group(std::integral_constant<int, 6>{});
-    group(std::integral_constant<int, 7>{});
-    group(std::integral_constant<int, 8>{});
-    group(std::integral_constant<int, 9>{});
-    group(std::integral_constant<int, 10>{});
-    group(std::integral_constant<int, 11>{});
-    cur_c = next_c;
-  }
-  const int r = lane & 31;
-#pragma unroll
-  for (int d = 0; d < 3; ++d) {
-    float* pb = part + ((size_t)sp * 27 + pair * 3 + d) * cout * cin;
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) {
-          const int co = co0 + wr * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
-          const int ci = ci0 + wc * 64 + j * 32 + r;
-          pb[(size_t)co * cin + ci] = acc[d][i][j][e];
-        }
-  }
 }
 
 // dw[co][ci][tap] = sum_s part[s][tap][co][ci], in split order.  A block owns
@@ -2527,13 +2208,6 @@ bool conv3_wgrad3_ok(int R) {
 #else
   return R >= 8 && (R & (R - 1)) == 0;  // 8-voxel z runs, shift-decoded voxel index
 #endif
-}
-
-// the one-wave-per-SIMD form of the three-tap weight gradient: opt-in
-// (PCFM_WGRAD3P=1), measured slower than the 12-wave form
-bool conv3_wgrad3p() {
-  const char* e = std::getenv("PCFM_WGRAD3P");
-  return e != nullptr && e[0] == '1';
 }
 
 int conv3_wgrad_splits(int B, int cin, int cout, int R) {
@@ -3035,16 +2709,9 @@ static int wgrad_cl(const void* xs, const void* gys, int b, int cin, int cout, i
       hipLaunchKernelGGL(conv3_wgrad_lists_kernel, dim3(9, S), dim3(64), 0, st, cmask,
                          b * (V / kWV), S, cap, lists, counts);
     }
-    if (conv3_wgrad3p()) {
-      const int e2 = allow_big_lds((const void*)conv3_wgrad3p_kernel);
-      if (e2) return e2;
-      hipLaunchKernelGGL(conv3_wgrad3p_kernel, dim3(tiles / 3 * S), dim3(kW3PThreads), 2 * kW3Buf,
-                         st, xh, gh, b, cin, cout, r, S, (float*)ws, lists, counts, cap);
-    } else {
-      hipLaunchKernelGGL(conv3_wgrad3_kernel, dim3(tiles / 3 * S), dim3(kW3Threads), 2 * kW3Buf,
-                         st, xh, xh + kSplitLo, gh, gh + kSplitLo, b, cin, cout, r, S, (float*)ws,
-                         lists, counts, cap);
-    }
+    hipLaunchKernelGGL(conv3_wgrad3_kernel, dim3(tiles / 3 * S), dim3(kW3Threads), 2 * kW3Buf, st,
+                       xh, xh + kSplitLo, gh, gh + kSplitLo, b, cin, cout, r,
+                       S, (float*)ws, lists, counts, cap);
   } else {
     hipLaunchKernelGGL(conv3_wgrad_cl_kernel, dim3(tiles * S), dim3(256), 0, st, xh,
                        xh + kSplitLo, gh, gh + kSplitLo, b, cin, cout, r, S,

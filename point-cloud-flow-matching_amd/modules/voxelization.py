@@ -21,14 +21,19 @@ class Voxelization(nn.Module):
         self.normalize = normalize
         self.eps = eps
 
-    def _grid_coords(self, coords: torch.Tensor) -> torch.Tensor:
+    def _unit_coords(self, coords: torch.Tensor) -> torch.Tensor:
+        # the resolution-independent part (shared by the stages' voxelizations)
         centred = coords - coords.mean(2, keepdim=True)
         if self.normalize:
             radius = centred.norm(dim=1, keepdim=True).max(dim=2, keepdim=True).values
-            unit = centred / (radius * 2.0 + self.eps) + 0.5
-        else:
-            unit = (centred + 1) / 2.0
+            return centred / (radius * 2.0 + self.eps) + 0.5
+        return (centred + 1) / 2.0
+
+    def _scale_coords(self, unit: torch.Tensor) -> torch.Tensor:
         return torch.clamp(unit * self.r, 0, self.r - 1)
+
+    def _grid_coords(self, coords: torch.Tensor) -> torch.Tensor:
+        return self._scale_coords(self._unit_coords(coords))
 
     def _coords(self, coords):
         # shared per points on a HIP device (pcfm.plans): a stage's PVConv

@@ -4,7 +4,8 @@ The hybrid backbone runs two PVConv blocks per stage on the SAME points
 (reference models.py:371-389 `_PVStage`; PVConv returns its `coords` unchanged,
 third_party/pvcnn/modules/pvconv.py:35-39), so everything that depends only on
 the coordinates is computed once per stage instead of once per block:
-  * the voxel-grid coordinates (Voxelization's normalise + round),
+  * the voxel-grid coordinates (Voxelization's normalise + round; the
+    resolution-independent [0, 1] coordinates are shared across the stages too),
   * the voxelization plan (stable sort of the points by voxel, work units;
     also the backward's ind / cnt),
   * the devoxelization's corner indices / weights (inds, wgts) and
@@ -85,9 +86,17 @@ def grid_coords(vox, coords: torch.Tensor):
     hit = _cache.get(coords, tag) if _on(coords) else None
     if hit is not None:
         return hit
-    norm = vox._grid_coords(coords.detach())
-    val = (norm, torch.round(norm).to(torch.int32))
-    return _cache.put(coords, tag, val) if _on(coords) else val
+    if not _on(coords):
+        norm = vox._grid_coords(coords.detach())
+        return norm, torch.round(norm).to(torch.int32)
+    # the normalised [0, 1] coordinates do not depend on the resolution: one
+    # computation for every stage's voxelization of the same points
+    utag = ("unit", bool(vox.normalize), float(vox.eps))
+    unit = _cache.get(coords, utag)
+    if unit is None:
+        unit = _cache.put(coords, utag, vox._unit_coords(coords.detach()))
+    norm = vox._scale_coords(unit)
+    return _cache.put(coords, tag, (norm, torch.round(norm).to(torch.int32)))
 
 
 def voxel_plan(vox_coords: torch.Tensor, r: int):

@@ -186,51 +186,3 @@ def test_window_form_padding_counts(ops):
     cnt = (n1[:, None, None] * n1[None, :, None] * n1[None, None, :]).float() * c
     assert torch.equal(y[0, 0], cnt) and torch.equal(y[1, c - 1], cnt)
 
-
-@pytest.mark.parametrize("b,cin,cout,r", [(8, 128, 128, 32), (8, 256, 256, 16), (8, 256, 256, 8),
-                                          (2, 128, 256, 16), (3, 256, 128, 8), (1, 128, 128, 8)])
-def test_wgrad_one_wave_per_simd_form_is_bit_identical(ops, monkeypatch, b, cin, cout, r):
-    """The one-wave-per-SIMD three-tap weight gradient (conv3_wgrad3p_kernel: each
-    wave owns a 64x64 quadrant for all three dz taps, software-pipelined) gives
-    every accumulator its MFMAs in the 12-wave kernel's order: the weight
-    gradient bit-identical to it, and to the fp64 pin, incl. the split tails
-    (b * r^3 / 64 steps not a multiple of the split count)."""
-    g = torch.Generator(device="cuda").manual_seed(3 * r + cin + 7 * cout + b)
-    x = torch.randn(b, cin, r, r, r, device="cuda", generator=g)
-    dy = torch.randn(b, cout, r, r, r, device="cuda", generator=g)
-    xs, gys = ops.conv3d_split(x), ops.conv3d_split(dy)
-    out = {}
-    for form in ("1", "0"):
-        monkeypatch.setenv("PCFM_WGRAD3P", form)
-        out[form] = ops.conv3d_wgrad_split(xs, gys, b, cin, cout, r)
-    assert torch.equal(out["1"], out["0"])
-    ref = torch.nn.grad.conv3d_weight(x.double().cpu(), (cout, cin, 3, 3, 3), dy.double().cpu(),
-                                      padding=1)
-    assert _rel(out["1"], ref) < TOL
-
-
-@pytest.mark.parametrize("r,surface", [(32, False), (16, True)])
-def test_wgrad_one_wave_per_simd_form_occupancy_lists(ops, monkeypatch, r, surface):
-    """The chunk-list (occupancy-masked) launches of both weight-gradient forms
-    agree bit for bit."""
-    b, c, n = 4, 128, 6000
-    g = torch.Generator(device="cuda").manual_seed(r + c)
-    pts = torch.randn(b, 3, n, device="cuda", generator=g)
-    if surface:
-        pts = pts / pts.norm(dim=1, keepdim=True)
-    c0 = pts - pts.mean(2, keepdim=True)
-    unit = c0 / (2 * c0.norm(dim=1, keepdim=True).max(2, keepdim=True).values + 1e-6) + 0.5
-    vox = torch.round(torch.clamp(unit * r, 0, r - 1)).int().contiguous()
-    grid, _, cnt = ops.avg_voxelize_forward(torch.randn(b, c, n, device="cuda", generator=g),
-                                            vox, r)
-    occ = ops.conv3d_occupancy(cnt, r)
-    assert occ is not None
-    grid = grid.view(b, c, r, r, r)
-    xs = ops.conv3d_split(grid.contiguous())
-    g = torch.Generator(device="cuda").manual_seed(r)
-    gys = ops.conv3d_split(torch.randn(b, c, r, r, r, device="cuda", generator=g))
-    out = {}
-    for form in ("1", "0"):
-        monkeypatch.setenv("PCFM_WGRAD3P", form)
-        out[form] = ops.conv3d_wgrad_split(xs, gys, b, c, c, r, occ=occ)
-    assert torch.equal(out["1"], out["0"])
