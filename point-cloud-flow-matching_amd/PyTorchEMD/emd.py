@@ -5,11 +5,20 @@ matchcost_backward, PyTorchEMD/cuda/emd.cpp:8-27) on the gfx950 library; float
 and double inputs are both supported, like the reference's
 AT_DISPATCH_FLOATING_TYPES.  CPU tensors run the pure-PyTorch backend
 (pcfm.cpu_ops) where the reference asserts "Only support cuda currently."
-(emd.py:13).
+(emd.py:13).  PCFM_TORCH_BACKEND=1 selects the torch C++ extension
+`PyTorchEMD/emd_cuda*.so` (csrc/torch_losses.cpp; HIP tensors only) as
+`emd_cuda`; the forward keeps the fused match + cost call.
 """
+import os
+
 import torch
 
-from pcfm.ops import approxmatch_cost_forward, emd_cuda
+from pcfm.ops import approxmatch_cost_forward
+
+if os.environ.get("PCFM_TORCH_BACKEND") == "1":
+    from PyTorchEMD import emd_cuda  # the torch-extension module
+else:
+    from pcfm.ops import emd_cuda
 
 __all__ = ["emd_cuda", "EarthMoverDistanceFunction", "earth_mover_distance"]
 

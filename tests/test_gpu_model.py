@@ -1,6 +1,7 @@
 """GPU: the drop-in modules and the flow model on the HIP path against the
 reference-Python goldens, and the train step at small scale."""
 import math
+import os
 
 import numpy as np
 import pytest
@@ -29,7 +30,10 @@ def _param_sums(module):
 def test_native_library_is_what_runs():
     import modules.functional.backend as be
     from pcfm import _lib, ops
-    assert be._backend is ops.backend
+    if os.environ.get("PCFM_TORCH_BACKEND") == "1":  # the torch-extension binding
+        assert be._backend is be._torch_backend is not None
+    else:
+        assert be._backend is ops.backend
     lib = _lib.load()
     assert lib._name.endswith("libpcfm_hip.so")
 

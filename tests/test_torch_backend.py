@@ -78,3 +78,65 @@ def test_extension_matches_ctypes_binding():
         o2 = ext.grouping_forward(feat, idx)
     s.synchronize()
     assert torch.equal(o2, ct.grouping_forward(feat, idx))
+
+
+def _loss_exts():
+    import importlib
+    try:
+        return (importlib.import_module("chamfer3D.chamfer_3D"),
+                importlib.import_module("PyTorchEMD.emd_cuda"))
+    except ImportError:
+        pytest.skip("chamfer_3D / emd_cuda extensions not built (csrc/build_torch_backend.py)")
+
+
+def test_loss_extensions_export_the_reference_names():
+    ch, emd = _loss_exts()
+    # chamfer_cuda.cpp:29-32 and PyTorchEMD/cuda/emd.cpp:23-27
+    assert sorted(n for n in dir(ch) if not n.startswith("_")) == ["backward", "forward"]
+    assert sorted(n for n in dir(emd) if not n.startswith("_")) == [
+        "approxmatch_forward", "matchcost_backward", "matchcost_forward"]
+    # the reference's chamfer returns 0 (after printing) on bad input
+    z = torch.zeros(1, 4, 3)
+    assert ch.forward(z, z, torch.zeros(1, 4), torch.zeros(1, 4), torch.zeros(1, 4, dtype=torch.int32),
+                      torch.zeros(1, 4, dtype=torch.int32)) == 0
+
+
+@pytest.mark.gpu
+def test_loss_extensions_match_ctypes_bindings():
+    from pcfm import _lib
+    from pcfm import ops
+    _lib.load()
+    ch, emd = _loss_exts()
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(5)
+    b, n, m = 2, 700, 500
+    x1 = torch.rand(b, n, 3, device=dev, generator=g)
+    x2 = torch.rand(b, m, 3, device=dev, generator=g)
+
+    def outs():
+        return (torch.empty(b, n, device=dev), torch.empty(b, m, device=dev),
+                torch.empty(b, n, device=dev, dtype=torch.int32),
+                torch.empty(b, m, device=dev, dtype=torch.int32))
+    a, c = outs(), outs()
+    assert ch.forward(x1, x2, *a) == 1 and ops.chamfer_3D.forward(x1, x2, *c) == 1
+    for p, q in zip(a, c):
+        assert torch.equal(p, q)
+    gd1, gd2 = torch.randn(b, n, device=dev, generator=g), torch.randn(b, m, device=dev, generator=g)
+    ga = (torch.zeros_like(x1), torch.zeros_like(x2))  # the backward accumulates
+    gc = (torch.zeros_like(x1), torch.zeros_like(x2))
+    assert ch.backward(x1, x2, *ga, gd1, gd2, a[2], a[3]) == 1
+    assert ops.chamfer_3D.backward(x1, x2, *gc, gd1, gd2, c[2], c[3]) == 1
+    # the backward scatters with float atomics, as the reference's NmDistanceGradKernel
+    # (chamfer3D.cu:155-195): the summation order, so the last bits, vary run to run
+    for p, q in zip(ga, gc):
+        assert torch.allclose(p, q, rtol=1e-5, atol=1e-6)
+    for dt in (torch.float32, torch.float64):
+        y1, y2 = x1.to(dt), x2.to(dt)
+        mt = emd.approxmatch_forward(y1, y2)
+        assert torch.equal(mt, ops.emd_cuda.approxmatch_forward(y1, y2))
+        assert torch.equal(emd.matchcost_forward(y1, y2, mt), ops.emd_cuda.matchcost_forward(y1, y2, mt))
+        gcost = torch.rand(b, device=dev, dtype=dt, generator=g) if dt == torch.float32 else \
+            torch.rand(b, device=dev, generator=g).to(dt)
+        for p, q in zip(emd.matchcost_backward(gcost, y1, y2, mt),
+                        ops.emd_cuda.matchcost_backward(gcost, y1, y2, mt)):
+            assert torch.equal(p, q)
