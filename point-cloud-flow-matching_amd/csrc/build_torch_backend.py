@@ -34,7 +34,8 @@ def output_path(name: str = "_pvcnn_backend") -> str:
     return os.path.join(MODULES[name][1], name + sysconfig.get_config_var("EXT_SUFFIX"))
 
 
-def build_one(name: str, force: bool = False) -> str:
+def _command(name: str, force: bool):
+    """(g++ command line or None when up to date, output path)"""
     src_name, out_dir, defs = MODULES[name]
     src = os.path.join(HERE, src_name)
     lib = os.path.join(HERE, "libpcfm_hip.so")
@@ -44,7 +45,7 @@ def build_one(name: str, force: bool = False) -> str:
         raise RuntimeError(f"{lib} missing: run make -C {HERE} first")
     if (not force and os.path.exists(out)
             and os.path.getmtime(out) >= max(os.path.getmtime(p) for p in (src, lib, hdr, __file__))):
-        return out
+        return None, out
     abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
     cmd = ["g++", "-O2", "-std=c++17", "-fPIC", "-shared", src, "-o", out, *defs,
            f"-D_GLIBCXX_USE_CXX11_ABI={abi}", f"-DTORCH_EXTENSION_NAME={name}",
@@ -56,12 +57,17 @@ def build_one(name: str, force: bool = False) -> str:
     rel = os.path.relpath(HERE, out_dir)
     cmd += ["-L" + HERE, "-l:libpcfm_hip.so", f"-Wl,-rpath,$ORIGIN/{rel}",
             "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_python"]
-    subprocess.run(cmd, check=True)
-    return out
+    return cmd, out
 
 
 def build(force: bool = False) -> list:
-    return [build_one(name, force) for name in MODULES]
+    """Compile the modules that are out of date, concurrently (one g++ each)."""
+    jobs = [_command(name, force) for name in MODULES]
+    procs = [(subprocess.Popen(cmd), cmd) for cmd, _ in jobs if cmd is not None]
+    bad = [cmd for p, cmd in procs if p.wait() != 0]
+    if bad:
+        raise RuntimeError("torch-extension build failed: " + " ".join(bad[0]))
+    return [out for _, out in jobs]
 
 
 if __name__ == "__main__":
