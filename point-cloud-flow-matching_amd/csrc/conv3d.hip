@@ -1992,6 +1992,10 @@ __global__ void __launch_bounds__(kW3Threads)
                         int B, int cin, int cout, int R, int S, float* __restrict__ part,
                         const int* __restrict__ lists, const int* __restrict__ counts, int cap) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  // 12 waves = 3 per SIMD at 168 VGPRs each: the CU's whole register file, so
+  // no other kernel's wave shares a CU with this block
+  static_assert(kW3Threads == 768, "three waves per SIMD");
+  PCFM_CLAIM_VGPRS(167);
   const int V = R * R * R, R2 = R * R;
   const int nco = cout / kMT;
   int id = (int)blockIdx.x;

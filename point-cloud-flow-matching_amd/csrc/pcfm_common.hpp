@@ -37,6 +37,14 @@ constexpr int kLdsBytesMax = 160 * 1024;
 // Raise the dynamic-LDS cap of one kernel to the gfx950 maximum once.
 int allow_big_lds(const void* kernel);
 
+// Whole-CU residency for a kernel whose block puts W waves on each SIMD: naming
+// register v(512 / W - 1) in a clobber makes the kernel descriptor allocate
+// 512 / W VGPRs per lane (granule 8), so the block's waves take every register
+// of the CU's four SIMDs and no wave of another kernel (any kernel that needs
+// more than 8 VGPRs) can be resident on the CU beside them.  Used by the
+// LDS-DMA weight gradient ("co-residence").
+#define PCFM_CLAIM_VGPRS(last) asm volatile("" ::: "v" #last)
+
 // Split operands (bf16 hi / lo of an fp32 tensor, channels-last rows of C
 // channels, C % 32 == 0) are stored interleaved per 32-channel group: row r
 // holds [hi c0..c31 | lo c0..c31 | hi c32..c63 | lo c32..c63 | ...], so the

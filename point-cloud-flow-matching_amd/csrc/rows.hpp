@@ -111,14 +111,9 @@ struct ProvDevox {
         wgts_out[o] = wt[k];
       }
     }
-    // the rows are READ at clamped corners: for coordinates in [0, r - 1] (what
-    // Voxelization hands over) every corner is inside the volume and nothing
-    // changes; a corner outside -- coordinates out of range, or a value gone
-    // wrong in flight (kernels sharing CUs) -- reads a row
-    // of this batch element instead of faulting on another allocation (the
-    // stored pairs above stay the reference's unclamped ones)
-#pragma unroll
-    for (int k = 0; k < 8; ++k) id[k] = min(max(id[k], 0), r3 - 1);
+    // A corner whose linear index leaves [0, r^3) (coordinates outside [0, r-1])
+    // contributes nothing: (0, 0), as the oracle and the backward's ProvIdx8
+    // treat the stored pair, so forward and backward agree on every point.
 #ifndef PCFM_DEVOX_CHECK_EACH
     // every corner is inside the volume when the low cell and the high offsets
     // are (the usual case: coords in [0, r-1]); only then are the 8 checks skipped

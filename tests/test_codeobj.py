@@ -39,6 +39,24 @@ def test_shipped_library_has_no_packed_fp32(tmp_path):
     assert not bad, f"packed fp32 in the shipped library: {bad}"
 
 
+@needs_tools
+@pytest.mark.skipif(not os.path.exists(LIB), reason="libpcfm_hip.so not built")
+def test_weight_gradient_claims_its_cus(tmp_path):
+    """conv3_wgrad3 (768 threads = 3 waves per SIMD, LDS-DMA) allocates 168 VGPRs
+    per lane, 504 of each SIMD's 512: no wave of another kernel needing more than
+    8 can share a CU with it (PCFM_CLAIM_VGPRS)."""
+    found = 0
+    for co in codeobj.extract(LIB, str(tmp_path)):
+        res = codeobj.kernel_resources(co)
+        for k, v in res.items():
+            if "conv3_wgrad3_kernel" in k:
+                regs = codeobj.descriptor_registers(co, k)
+                assert v["wg"] == 768 and regs["alloc"] == 168, (k, v, regs)
+                assert v["scratch"] == 0
+                found += 1
+    assert found == 1
+
+
 def _librccl():
     import torch
     p = os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")

@@ -125,6 +125,37 @@ def test_trilinear_devoxelize(b, c, n, r, training):
     np.testing.assert_allclose(np_(gx), e_gx, rtol=1e-5, atol=1e-6 * scale)
 
 
+@pytest.mark.parametrize("r,c", [(8, 256), (16, 64), (32, 8)])
+def test_devox_coords_outside_the_volume(r, c):
+    """Coordinates outside [0, r-1]: a corner whose linear index leaves [0, r^3)
+    contributes 0 (the oracle; the backward's stored-pair check), the stored
+    pairs stay the reference's unclamped ones, and forward and backward agree
+    (the backward is the forward's adjoint on every point).  One shape per
+    gather form: 4-channel (r 8, 16), 1-channel (r 32)."""
+    from pcfm import ops
+    g = rng(900 + r)
+    b, n = 2, 3000
+    pts = (g.random((b, 3, n)) * (r + 3) - 1.5).astype(np.float32)  # ~30 % outside
+    grid = g.standard_normal((b, c, r ** 3)).astype(np.float32)
+    out, inds, wgts = ops.trilinear_devoxelize_forward(r, True, cu(pts), cu(grid))
+    e_out, e_inds, e_wgts = O.trilinear_devoxelize_fwd(pts, grid, r, True)
+    np.testing.assert_array_equal(np_(inds), e_inds)
+    np.testing.assert_array_equal(np_(wgts), e_wgts)
+    np.testing.assert_array_equal(np_(out), e_out)
+    eval_out, _, _ = ops.trilinear_devoxelize_forward(r, False, cu(pts), cu(grid))
+    np.testing.assert_array_equal(np_(eval_out), e_out)
+    scale = torch.rand(b, c, device=DEV)
+    add = torch.randn(b, c, n, device=DEV)
+    o2, _, _ = ops.trilinear_devoxelize_scale_add(r, True, cu(pts), cu(grid), scale, add)
+    ref2 = torch.from_numpy(e_out).to(DEV) * scale[:, :, None] + add
+    torch.testing.assert_close(o2, ref2, rtol=0, atol=0)
+    gy = g.standard_normal((b, c, n)).astype(np.float32)
+    gx = ops.trilinear_devoxelize_backward(cu(gy), inds, wgts, r)
+    lhs = float((np_(out).astype(np.float64) * gy).sum())
+    rhs = float((grid.astype(np.float64) * np_(gx)).sum())
+    assert abs(lhs - rhs) <= 1e-5 * max(1.0, abs(lhs)), (lhs, rhs)
+
+
 def test_devox_full_size_properties():
     """C2 stage-1 size: forward linear in the grid, backward its adjoint."""
     from pcfm import ops
