@@ -6,8 +6,9 @@ and double inputs are both supported, like the reference's
 AT_DISPATCH_FLOATING_TYPES.  CPU tensors run the pure-PyTorch backend
 (pcfm.cpu_ops) where the reference asserts "Only support cuda currently."
 (emd.py:13).  PCFM_TORCH_BACKEND=1 selects the torch C++ extension
-`PyTorchEMD/emd_cuda*.so` (csrc/torch_losses.cpp; HIP tensors only) as
-`emd_cuda`; the forward keeps the fused match + cost call.
+`PyTorchEMD/emd_ext*.so` (csrc/torch_losses.cpp; the reference's extension name,
+backend.py:11-12) as `emd_cuda` for HIP tensors, CPU tensors still going to the
+CPU backend; the forward keeps the fused match + cost call.
 """
 import os
 
@@ -15,10 +16,13 @@ import torch
 
 from pcfm.ops import approxmatch_cost_forward
 
+from pcfm.ops import emd_cuda
+
 if os.environ.get("PCFM_TORCH_BACKEND") == "1":
-    from PyTorchEMD import emd_cuda  # the torch-extension module
-else:
-    from pcfm.ops import emd_cuda
+    from PyTorchEMD.backend import emd_cuda_dynamic as _ext  # the torch-extension module
+    from pcfm.ops import host_routed
+    emd_cuda = host_routed(_ext, emd_cuda,
+                           ["approxmatch_forward", "matchcost_forward", "matchcost_backward"])
 
 __all__ = ["emd_cuda", "EarthMoverDistanceFunction", "earth_mover_distance"]
 

@@ -7,7 +7,8 @@ the autograd Function allocates its outputs directly on the device instead of
 the reference's CPU torch.zeros + .to(device) round trip (:53-63, :77-81).
 By default `chamfer_3D` is the ctypes binding (pcfm.ops.chamfer_3D, which also
 runs CPU tensors); PCFM_TORCH_BACKEND=1 selects the torch C++ extension
-`chamfer3D/chamfer_3D*.so` (csrc/torch_losses.cpp; HIP tensors only).
+`chamfer3D/chamfer_3D*.so` (csrc/torch_losses.cpp) for HIP tensors, CPU
+tensors still going to the ctypes binding's CPU backend.
 """
 import os
 
@@ -15,10 +16,12 @@ import torch
 from torch import nn
 from torch.autograd import Function
 
+from pcfm.ops import chamfer_3D
+
 if os.environ.get("PCFM_TORCH_BACKEND") == "1":
-    from chamfer3D import chamfer_3D  # the torch-extension module
-else:
-    from pcfm.ops import chamfer_3D
+    from chamfer3D import chamfer_3D as _ext  # the torch-extension module
+    from pcfm.ops import host_routed
+    chamfer_3D = host_routed(_ext, chamfer_3D, ["forward", "backward"])
 
 __all__ = ["chamfer_3D", "chamfer_3DFunction", "chamfer_3DDist", "chamfer_3DFunction_noGrad",
            "chamfer_3DDist_nograd"]

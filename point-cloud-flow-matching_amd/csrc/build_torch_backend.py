@@ -4,6 +4,8 @@ Python package that mirrors the reference module it replaces:
     _pvcnn_backend  (csrc/torch_backend.cpp)  -> modules/functional/
     chamfer_3D      (csrc/torch_losses.cpp)   -> chamfer3D/
     emd_cuda        (csrc/torch_losses.cpp)   -> PyTorchEMD/
+    emd_ext         (csrc/torch_losses.cpp)   -> PyTorchEMD/  (the reference's
+                    extension name, PyTorchEMD/setup.py:26-29, backend.py:11-12)
 
     python point-cloud-flow-matching_amd/csrc/build_torch_backend.py [--force]
 
@@ -27,6 +29,7 @@ MODULES = {
     "_pvcnn_backend": ("torch_backend.cpp", os.path.join(PKG, "modules", "functional"), []),
     "chamfer_3D": ("torch_losses.cpp", os.path.join(PKG, "chamfer3D"), ["-DPCFM_TORCH_MODULE=1"]),
     "emd_cuda": ("torch_losses.cpp", os.path.join(PKG, "PyTorchEMD"), ["-DPCFM_TORCH_MODULE=2"]),
+    "emd_ext": ("torch_losses.cpp", os.path.join(PKG, "PyTorchEMD"), ["-DPCFM_TORCH_MODULE=2"]),
 }
 
 

@@ -16,6 +16,7 @@
 
 #include <c10/hip/HIPStream.h>
 
+#include <initializer_list>
 #include <string>
 #include <vector>
 
@@ -37,6 +38,23 @@ void check_rc(int rc, const char* op) {
   TORCH_CHECK(rc == PCFM_OK, op, " failed (", rc, "): ", pcfm_last_error());
 }
 
+// shape and device checks matching pcfm.ops' (a caller mistake is a
+// TORCH_CHECK error, never an out-of-bounds kernel access)
+void check_shape(const at::Tensor& t, const char* name, std::initializer_list<int64_t> shape) {
+  TORCH_CHECK(t.dim() == (int64_t)shape.size(), name, " must have ", shape.size(),
+              " dimensions, got ", t.sizes());
+  int64_t d = 0;
+  for (int64_t want : shape) {
+    TORCH_CHECK(want < 0 || t.size(d) == want, name, " has shape ", t.sizes(), ": dimension ", d,
+                " must be ", want);
+    ++d;
+  }
+}
+
+void check_same_device(const at::Tensor& a, const at::Tensor& b, const char* name) {
+  TORCH_CHECK(a.device() == b.device(), name, " is on ", b.device(), ", expected ", a.device());
+}
+
 at::Tensor workspace(size_t bytes, const at::Tensor& like) {
   return at::empty({(int64_t)std::max<size_t>(bytes, 1)}, like.options().dtype(at::kByte));
 }
@@ -46,6 +64,10 @@ std::vector<at::Tensor> avg_voxelize_forward(const at::Tensor& features, const a
                                              const int resolution) {
   check_hip(features, "features", at::kFloat);
   check_hip(coords, "coords", at::kInt);
+  check_shape(features, "features", {-1, -1, -1});
+  check_shape(coords, "coords", {features.size(0), 3, features.size(2)});
+  check_same_device(features, coords, "coords");
+  TORCH_CHECK(resolution > 0 && resolution <= 1024, "resolution must be in [1, 1024]");
   const int b = features.size(0), c = features.size(1), n = features.size(2);
   const int r = resolution, s = r * r * r;
   auto out = at::empty({b, c, s}, features.options());
@@ -65,6 +87,11 @@ at::Tensor avg_voxelize_backward(const at::Tensor& grad_y, const at::Tensor& ind
   check_hip(grad_y, "grad_y", at::kFloat);
   check_hip(indices, "indices", at::kInt);
   check_hip(cnt, "cnt", at::kInt);
+  check_shape(grad_y, "grad_y", {-1, -1, -1});
+  check_shape(indices, "indices", {grad_y.size(0), -1});
+  check_shape(cnt, "cnt", {grad_y.size(0), grad_y.size(2)});
+  check_same_device(grad_y, indices, "indices");
+  check_same_device(grad_y, cnt, "cnt");
   const int b = grad_y.size(0), c = grad_y.size(1), s = grad_y.size(2);
   const int n = indices.size(1);
   auto grad_x = at::empty({b, c, n}, grad_y.options());
@@ -81,6 +108,10 @@ std::vector<at::Tensor> trilinear_devoxelize_forward(const int r, const bool is_
                                                      const at::Tensor& features) {
   check_hip(features, "features", at::kFloat);
   check_hip(coords, "coords", at::kFloat);
+  TORCH_CHECK(r > 0 && r <= 1024, "r must be in [1, 1024]");
+  check_shape(features, "features", {-1, -1, (int64_t)r * r * r});
+  check_shape(coords, "coords", {features.size(0), 3, -1});
+  check_same_device(features, coords, "coords");
   const int b = features.size(0), c = features.size(1), n = coords.size(2);
   auto outs = at::empty({b, c, n}, features.options());
   at::Tensor inds, wgts;
@@ -106,6 +137,12 @@ at::Tensor trilinear_devoxelize_backward(const at::Tensor& grad_y, const at::Ten
   check_hip(grad_y, "grad_y", at::kFloat);
   check_hip(indices, "indices", at::kInt);
   check_hip(weights, "weights", at::kFloat);
+  TORCH_CHECK(r > 0 && r <= 1024, "r must be in [1, 1024]");
+  check_shape(grad_y, "grad_y", {-1, -1, -1});
+  check_shape(indices, "indices", {grad_y.size(0), 8, grad_y.size(2)});
+  check_shape(weights, "weights", {grad_y.size(0), 8, grad_y.size(2)});
+  check_same_device(grad_y, indices, "indices");
+  check_same_device(grad_y, weights, "weights");
   const int b = grad_y.size(0), c = grad_y.size(1), n = grad_y.size(2);
   auto grad_x = at::empty({b, c, (int64_t)r * r * r}, grad_y.options());
   auto ws = workspace(pcfm_trilinear_devoxelize_bwd_workspace_bytes(b, c, n, r), grad_y);
@@ -122,6 +159,10 @@ at::Tensor ball_query(const at::Tensor& centers_coords, const at::Tensor& points
                       const float radius, const int num_neighbors) {
   check_hip(centers_coords, "centers_coords", at::kFloat);
   check_hip(points_coords, "points_coords", at::kFloat);
+  check_shape(centers_coords, "centers_coords", {-1, 3, -1});
+  check_shape(points_coords, "points_coords", {centers_coords.size(0), 3, -1});
+  check_same_device(centers_coords, points_coords, "points_coords");
+  TORCH_CHECK(num_neighbors >= 0, "num_neighbors must be >= 0");
   const int b = centers_coords.size(0), m = centers_coords.size(2), n = points_coords.size(2);
   auto idx = at::zeros({b, m, num_neighbors}, centers_coords.options().dtype(at::kInt));
   check_rc(pcfm_ball_query(centers_coords.data_ptr<float>(), points_coords.data_ptr<float>(), b,
@@ -135,6 +176,9 @@ at::Tensor ball_query(const at::Tensor& centers_coords, const at::Tensor& points
 at::Tensor grouping_forward(const at::Tensor& features, const at::Tensor& indices) {
   check_hip(features, "features", at::kFloat);
   check_hip(indices, "indices", at::kInt);
+  check_shape(features, "features", {-1, -1, -1});
+  check_shape(indices, "indices", {features.size(0), -1, -1});
+  check_same_device(features, indices, "indices");
   const int b = features.size(0), c = features.size(1), n = features.size(2);
   const int m = indices.size(1), u = indices.size(2);
   auto out = at::empty({b, c, m, u}, features.options());
@@ -148,6 +192,10 @@ at::Tensor grouping_forward(const at::Tensor& features, const at::Tensor& indice
 at::Tensor grouping_backward(const at::Tensor& grad_y, const at::Tensor& indices, const int n) {
   check_hip(grad_y, "grad_y", at::kFloat);
   check_hip(indices, "indices", at::kInt);
+  check_shape(grad_y, "grad_y", {-1, -1, -1, -1});
+  check_shape(indices, "indices", {grad_y.size(0), grad_y.size(2), grad_y.size(3)});
+  check_same_device(grad_y, indices, "indices");
+  TORCH_CHECK(n >= 0, "n must be >= 0");
   const int b = grad_y.size(0), c = grad_y.size(1);
   const int m = indices.size(1), u = indices.size(2);
   auto grad_x = at::empty({b, c, n}, grad_y.options());

@@ -707,6 +707,25 @@ emd_cuda = types.SimpleNamespace(approxmatch_forward=approxmatch_forward,
                                  matchcost_backward=matchcost_backward)
 
 
+def host_routed(ext, host, names):
+    """A binding namespace that calls the torch C++ extension `ext` (HIP tensors
+    only: csrc/torch_backend.cpp, torch_losses.cpp) and sends a call whose tensor
+    arguments are all CPU tensors to `host` (this module's binding, which runs
+    them on pcfm.cpu_ops, BASELINE configs[0]) -- so PCFM_TORCH_BACKEND=1 keeps the
+    CPU path working.  `.extension` is the extension module itself."""
+    def route(name):
+        on_dev, on_host = getattr(ext, name), getattr(host, name)
+
+        def call(*args):
+            ts = [a for a in args if isinstance(a, torch.Tensor)]
+            return (on_host if ts and not any(t.is_cuda for t in ts) else on_dev)(*args)
+        call.__name__ = name
+        return call
+    ns = types.SimpleNamespace(**{n: route(n) for n in names})
+    ns.extension = ext
+    return ns
+
+
 # --------------------------------------------------------------------------
 # Voxel convolution (PVConv's Conv3d k=3 s=1 p=1) on the bf16x3 matrix-core
 # path -- include/pcfm.h "Voxel convolution".

@@ -31,7 +31,7 @@ def test_native_library_is_what_runs():
     import modules.functional.backend as be
     from pcfm import _lib, ops
     if os.environ.get("PCFM_TORCH_BACKEND") == "1":  # the torch-extension binding
-        assert be._backend is be._torch_backend is not None
+        assert be._backend.extension is be._torch_backend is not None
     else:
         assert be._backend is ops.backend
     lib = _lib.load()

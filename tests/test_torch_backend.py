@@ -99,6 +99,63 @@ def test_loss_extensions_export_the_reference_names():
     z = torch.zeros(1, 4, 3)
     assert ch.forward(z, z, torch.zeros(1, 4), torch.zeros(1, 4), torch.zeros(1, 4, dtype=torch.int32),
                       torch.zeros(1, 4, dtype=torch.int32)) == 0
+    # the reference's own extension name (PyTorchEMD/setup.py:26-29, backend.py:11-12),
+    # as a module and through the drop-in backend.py's `emd_cuda_dynamic`
+    import importlib
+    ext = importlib.import_module("PyTorchEMD.emd_ext")
+    assert sorted(n for n in dir(ext) if not n.startswith("_")) == [
+        "approxmatch_forward", "matchcost_backward", "matchcost_forward"]
+    from PyTorchEMD.backend import emd_cuda_dynamic
+    assert emd_cuda_dynamic is ext
+
+
+def test_extensions_check_shapes_before_any_launch():
+    """A caller's shape or device mistake is a TORCH_CHECK error (chamfer: status
+    0 after the message, as chamfer_cuda.cpp does), never a kernel launch.  The
+    checks run before the HIP-tensor check can matter only on a GPU box, so the
+    messages are matched where the order allows it on the CPU too."""
+    ch, emd = _loss_exts()
+    be = _ext()
+    z = torch.zeros(1, 4, 3)
+    # wrong idx2 shape: 0 on the CPU (host tensor) and on the GPU (shape)
+    assert ch.forward(z, z, torch.zeros(1, 4), torch.zeros(1, 4),
+                      torch.zeros(1, 4, dtype=torch.int32), torch.zeros(1, 5, dtype=torch.int32)) == 0
+    with pytest.raises(RuntimeError):
+        emd.matchcost_forward(z.double(), z.double(), torch.zeros(1, 3, 4, dtype=torch.float64))
+    with pytest.raises(RuntimeError):
+        be.trilinear_devoxelize_backward(torch.zeros(1, 2, 5), torch.zeros(1, 8, 4, dtype=torch.int32),
+                                         torch.zeros(1, 8, 5), 2)
+
+
+def test_torch_backend_flag_keeps_the_cpu_path(monkeypatch):
+    """PCFM_TORCH_BACKEND=1: HIP tensors go to the extensions, CPU tensors still
+    run the pure-PyTorch backend (pcfm.ops.host_routed)."""
+    import importlib
+    _ext()
+    _loss_exts()
+    monkeypatch.setenv("PCFM_TORCH_BACKEND", "1")
+    import modules.functional.backend as be
+    import chamfer3D.dist_chamfer_3D as dc
+    import PyTorchEMD.emd as pe
+    try:
+        for m in (be, dc, pe):
+            importlib.reload(m)
+        assert be._backend.extension is be._torch_backend
+        feat = torch.randn(2, 3, 50)
+        coords = torch.randint(0, 4, (2, 3, 50), dtype=torch.int32)
+        out, ind, cnt = be._backend.avg_voxelize_forward(feat, coords, 4)
+        from pcfm import cpu_ops
+        e_out, e_ind, e_cnt = cpu_ops.avg_voxelize_forward(feat, coords, 4)
+        assert torch.equal(ind, e_ind) and torch.equal(cnt, e_cnt) and torch.allclose(out, e_out)
+        a, b = torch.randn(2, 30, 3), torch.randn(2, 20, 3)
+        d1, d2, i1, i2 = dc.chamfer_3DDist()(a, b)
+        assert d1.shape == (2, 30) and i2.dtype == torch.int32
+        cost = pe.earth_mover_distance(a, b, transpose=False)
+        assert cost.shape == (2,) and torch.isfinite(cost).all()
+    finally:
+        monkeypatch.delenv("PCFM_TORCH_BACKEND")
+        for m in (be, dc, pe):
+            importlib.reload(m)
 
 
 @pytest.mark.gpu
@@ -140,3 +197,34 @@ def test_loss_extensions_match_ctypes_bindings():
         for p, q in zip(emd.matchcost_backward(gcost, y1, y2, mt),
                         ops.emd_cuda.matchcost_backward(gcost, y1, y2, mt)):
             assert torch.equal(p, q)
+
+
+@pytest.mark.gpu
+def test_extensions_reject_wrong_shapes_on_the_gpu():
+    """HIP tensors of the wrong shape or on mixed devices: a TORCH_CHECK error (or
+    chamfer's 0), matching the ctypes binding's checks -- no kernel runs."""
+    ch, emd = _loss_exts()
+    be = _ext()
+    d = "cuda"
+    z = torch.zeros(1, 4, 3, device=d)
+    i4 = torch.zeros(1, 4, dtype=torch.int32, device=d)
+    assert ch.forward(z, z, torch.zeros(1, 4, device=d), torch.zeros(1, 4, device=d), i4,
+                      torch.zeros(1, 5, dtype=torch.int32, device=d)) == 0
+    assert ch.forward(z, z, torch.zeros(1, 4, device=d), torch.zeros(1, 4), i4, i4) == 0
+    with pytest.raises(RuntimeError, match="match"):
+        emd.matchcost_forward(z, z, torch.zeros(1, 3, 4, device=d))
+    with pytest.raises(RuntimeError, match="grad_cost"):
+        emd.matchcost_backward(torch.zeros(2, device=d), z, z, torch.zeros(1, 4, 4, device=d))
+    with pytest.raises(RuntimeError, match="features"):
+        be.trilinear_devoxelize_forward(4, True, torch.zeros(1, 3, 9, device=d),
+                                        torch.zeros(1, 2, 63, device=d))
+    with pytest.raises(RuntimeError, match="indices"):
+        be.trilinear_devoxelize_backward(torch.zeros(1, 2, 5, device=d),
+                                         torch.zeros(1, 8, 4, dtype=torch.int32, device=d),
+                                         torch.zeros(1, 8, 5, device=d), 2)
+    with pytest.raises(RuntimeError, match="coords"):
+        be.avg_voxelize_forward(torch.zeros(1, 2, 5, device=d),
+                                torch.zeros(1, 3, 4, dtype=torch.int32, device=d), 2)
+    with pytest.raises(RuntimeError, match="indices"):
+        be.grouping_backward(torch.zeros(1, 2, 3, 4, device=d),
+                             torch.zeros(1, 3, 5, dtype=torch.int32, device=d), 10)
