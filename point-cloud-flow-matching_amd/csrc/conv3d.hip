@@ -1352,411 +1352,11 @@ __global__ void __launch_bounds__(512)
     }
 }
 
-// ---------------------------------------------------------------------------
-// Forward / backward-data, BRICK form (r = 32, 16; unsplit launches).  The
-// LDS-DMA kernel above fetches its B operand (the 256 input rows a tap
-// reads) once per tap: 27 re-fetches of nearly the same rows per channel
-// chunk, 2/3 of the bytes every step moves, and the L2 / Infinity-cache
-// latency of those fetches, not the matrix work, sets its pace (a block
-// alone on the chip runs 3x slower per tile than among the neighbours that
-// share its rows in L2).  Here the 256 output voxels are a brick
-// BX x BY x BZ (2x4x32 at r = 32, 2x8x16 at r = 16) and its halo brick
-// (BX+2)(BY+2)(BZ+2) rows x 16 channels (hi | lo, 64 B per row) is staged
-// in LDS once per 16-channel chunk; all 27 taps read their B fragments from
-// it at a per-tap row offset.  Per step only the weight slice (128 rows x 16
-// channels, 8 KiB) moves by LDS-DMA.  The next chunk's halo brick is
-// prefetched into the other of two brick buffers while this one computes.
-// K-steps: 16-channel chunk major, taps 0..26 within a chunk, three bf16
-// products per step (fixed order: deterministic; the sum order differs from
-// the LDS-DMA kernel's 32-channel steps, so the two agree to fp32 rounding).
-// ---------------------------------------------------------------------------
-template <int R_>
-struct BrickGeo {
-  static constexpr int BZ = R_ >= 32 ? 32 : R_;
-  static constexpr int BX = 2;
-  static constexpr int BY = 256 / (BX * BZ);
-  static constexpr int HX = BX + 2, HY = BY + 2, HZ = BZ + 2;
-  static constexpr int HROWS = HX * HY * HZ;
-  static constexpr int QB = (HROWS + 127) / 128;     // brick pieces per wave (16 rows each)
-  static constexpr int BROWS = QB * 128;              // rows incl. padding
-  static constexpr int BBYTES = BROWS * 64;           // one brick buffer
-  static constexpr int ABYTES = 128 * 32 * 2;         // one weight stage: hi | lo, 32-B rows
-  static constexpr int NA = 3;                        // weight stages
-  static constexpr int LDS = 2 * BBYTES + NA * ABYTES;
-  static_assert(BX * BY * BZ == 256 && LDS <= 160 * 1024, "brick geometry");
-};
-
-// 16-B chunk swizzles: weight rows (32 B: chunks 0..1) and brick rows (64 B:
-// chunks 0..3 = hi 0-7, hi 8-15, lo 0-7, lo 8-15); conflict-free ds_read_b128
-// for 16 rows in a run (the brick's z runs)
-__device__ __forceinline__ int swzA16(int row) { return (row >> 3) & 1; }
-__device__ __forceinline__ int swzB16(int row) { return (row >> 2) & 3; }
-
-// s_waitcnt vmcnt(n) for a wave-uniform n (an immediate per case)
-__device__ __forceinline__ void wait_vm(int n) {
-  switch (n) {
-#define PCFM_VMW(k) \
-  case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
-    PCFM_VMW(0) PCFM_VMW(1) PCFM_VMW(2) PCFM_VMW(3) PCFM_VMW(4) PCFM_VMW(5) PCFM_VMW(6)
-    PCFM_VMW(7) PCFM_VMW(8) PCFM_VMW(9) PCFM_VMW(10) PCFM_VMW(11) PCFM_VMW(12) PCFM_VMW(13)
-    PCFM_VMW(14) PCFM_VMW(15)
-#undef PCFM_VMW
-    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
-  }
-}
-
-template <int R_>
-__global__ void __launch_bounds__(512)
-    conv3_igemm_brick_kernel(const uint16_t* __restrict__ xs, const uint16_t* __restrict__ ws,
-                             const uint16_t* __restrict__ zrow, const float* __restrict__ bias,
-                             float* __restrict__ y, int K, int M) {
-  using Gm = BrickGeo<R_>;
-  constexpr int R = R_, R2 = R * R, V = R * R * R;
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  uint8_t* const bricks = lds;                       // 2 x BBYTES
-  uint8_t* const astages = lds + 2 * Gm::BBYTES;     // NA x ABYTES
-  int id = (int)blockIdx.x;
-  {
-    const int nwg = (int)gridDim.x, q = nwg / 8, rr = nwg % 8, xcd = id % 8;
-    id = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + id / 8;
-  }
-  const int nmt = M / 128;
-  constexpr int NTX = R / Gm::BX, NTY = R / Gm::BY, NTZ = R / Gm::BZ;
-  const int m0 = (id % nmt) * 128;
-  id /= nmt;
-  const int tz = id % NTZ;
-  id /= NTZ;
-  const int ty = id % NTY;
-  id /= NTY;
-  const int tx = id % NTX;
-  const int b = id / NTX;
-  const int x0 = tx * Gm::BX, y0 = ty * Gm::BY, z0 = tz * Gm::BZ;
-  const int t = threadIdx.x, lane = t & 63;
-  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int wr = w >> 2, wc = w & 3, r = lane & 31, h = lane >> 5;
-  const int nch = K / 16, N = 27 * nch;
-  const size_t bV = (size_t)b * V;
-
-  // weight piece of this wave: rows 16 w + lane / 2 of the 128-row slice,
-  // image (hi, lo) = w / 4 ... one piece = 32 rows x 32 B; 8 pieces = 4 hi + 4 lo
-  const int aimg = w >> 2, arow = (w & 3) * 32 + (lane >> 1), apch = lane & 1;
-  const uint16_t* const abase =
-      ws + (size_t)(m0 + arow) * 2 * K + ((apch ^ swzA16(arow)) << 3) + (aimg ? kSplitLo : 0);
-  auto issue_a = [&](int g) {  // step g = chunk * 27 + tap
-    const int c = g / 27, tap = g - c * 27;
-    const int c0 = c * 16;
-    const size_t off = (size_t)tap * M * 2 * K + ((c0 >> 5) << 6) + (c0 & 31);
-    glds16_asm(abase + off, lds_addr(astages + (g % Gm::NA) * Gm::ABYTES + aimg * 4096 +
-                                     (w & 3) * 1024));
-  };
-  // brick pieces: piece P = w + 8 q covers halo rows 16 P .. 16 P + 15; lane ->
-  // row 16 P + lane / 4, physical chunk lane % 4 (logical = physical ^ swz)
-  auto issue_brick = [&](int c, int buf) {
-    const int c0 = c * 16;
-#pragma unroll
-    for (int q = 0; q < Gm::QB; ++q) {
-      const int P = w + 8 * q;
-      const int row = 16 * P + (lane >> 2);
-      const int lc = (lane & 3) ^ swzB16(row);
-      const int hz = row % Gm::HZ, hy = (row / Gm::HZ) % Gm::HY, hx = row / (Gm::HZ * Gm::HY);
-      const int gx = x0 - 1 + hx, gy = y0 - 1 + hy, gz = z0 - 1 + hz;
-      const bool inb = row < Gm::HROWS && (unsigned)gx < (unsigned)R && (unsigned)gy < (unsigned)R &&
-                       (unsigned)gz < (unsigned)R;
-      const int ch = c0 + (lc & 1) * 8;
-      const uint16_t* src = inb ? xs + split_off(bV + (size_t)gx * R2 + gy * R + gz, ch, K) +
-                                      ((lc >> 1) ? kSplitLo : 0)
-                                : zrow;
-      glds16_asm(src, lds_addr(bricks + buf * Gm::BBYTES + P * 1024));
-    }
-  };
-  // halo row of this lane's output voxel for MFMA column tile j (tap 0,0,0 = +0)
-  int hb[2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int vt = wc * 64 + j * 32 + r;
-    const int iz = vt % Gm::BZ, iy = (vt / Gm::BZ) % Gm::BY, ix = vt / (Gm::BZ * Gm::BY);
-    hb[j] = ((ix + 1) * Gm::HY + (iy + 1)) * Gm::HZ + (iz + 1);
-  }
-  // fragments of step g: F[0..1] A hi (i), F[2..3] A lo, F[4..5] B hi (j), F[6..7] B lo
-  auto frags = [&](int g, bf16x8 (&F)[1][8]) {
-    const int c = g / 27, tap = g - c * 27;
-    const uint8_t* a = astages + (g % Gm::NA) * Gm::ABYTES;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int row = wr * 64 + i * 32 + r;
-      const int off = row * 32 + ((h ^ swzA16(row)) << 4);
-      F[0][i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(a + off));
-      F[0][2 + i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(a + 4096 + off));
-    }
-    const int dx = tap / 9 - 1, dy = (tap / 3) % 3 - 1, dz = tap % 3 - 1;
-    const int toff = (dx * Gm::HY + dy) * Gm::HZ + dz;
-    const uint8_t* bb = bricks + (c & 1) * Gm::BBYTES;
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int row = hb[j] + toff;
-      const int sw = swzB16(row);
-      F[0][4 + j] = __builtin_bit_cast(bf16x8,
-                                       *reinterpret_cast<const uint4*>(bb + row * 64 + ((h ^ sw) << 4)));
-      F[0][6 + j] = __builtin_bit_cast(
-          bf16x8, *reinterpret_cast<const uint4*>(bb + row * 64 + (((2 + h) ^ sw) << 4)));
-    }
-  };
-
-  f32x16 acc[2][2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
-
-  // Issue bookkeeping, pieces per wave (A step: 1, brick: QB), issued in
-  // order "A(g + 3), then brick" at the top of step g.  At the top of step g
-  // we need A(g + 1) (issued at the top of g - 2) and the brick it reads; in
-  // flight may stay what was issued after it: the bricks of the top of g - 2
-  // and everything of the top of g - 1 (vmcnt counts in issue order).
-  // The prologue counts as tops -3 (brick 0, A 0), -2 (A 1), -1 (A 2, brick 1).
-  const bool b1 = nch > 1;
-  issue_brick(0, 0);
-  issue_a(0);
-  if (N > 1) issue_a(1);
-  if (N > 2) issue_a(2);
-  if (b1) issue_brick(1, 1);
-  int bk2 = 0;                                          // bricks, top of g - 2
-  int bk1 = b1 ? Gm::QB : 0;                            // bricks, top of g - 1
-  int all1 = (N > 2 ? 1 : 0) + bk1;                     // all pieces, top of g - 1
-  wait_vm((N > 1 ? 1 : 0) + all1);                      // brick 0 and A(0) landed
-  __builtin_amdgcn_s_barrier();
-  bf16x8 F0[1][8], F1[1][8];
-  frags(0, F0);
-  auto step = [&](int g, bf16x8 (&Fc)[1][8], bf16x8 (&Fn)[1][8]) {
-    // A(g + 1) and its brick landed; this wave's fragment reads of step g done
-    wait_vm(bk2 + all1);
-    __builtin_amdgcn_s_waitcnt(0xC07F);
-    __builtin_amdgcn_s_barrier();
-    int iss = 0, brk = 0;
-    if (g + 3 < N) {
-      issue_a(g + 3);
-      iss = 1;
-    }
-    const int c = g / 27;
-    if (g == c * 27 && c >= 1 && c + 1 < nch) {  // chunk c started: prefetch chunk c + 1
-      issue_brick(c + 1, (c + 1) & 1);
-      brk = Gm::QB;
-    }
-    bk2 = bk1;
-    bk1 = brk;
-    all1 = iss + brk;
-    if (g + 1 < N) frags(g + 1, Fn);
-    glds_mfma<16>(Fc, acc);
-  };
-  int g = 0;
-  for (; g + 2 <= N; g += 2) {
-    step(g, F0, F1);
-    step(g + 1, F1, F0);
-  }
-  if (g < N) step(g, F0, F1);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-
-  float* __restrict__ yb = y + (size_t)b * M * V;
-  float biasv[2][16];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) load_bias16(bias, m0 + wr * 64 + i * 32, h, M, biasv[i]);
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int vt = wc * 64 + j * 32 + r;
-    const int iz = vt % Gm::BZ, iy = (vt / Gm::BZ) % Gm::BY, ix = vt / (Gm::BZ * Gm::BY);
-    const int v = (x0 + ix) * R2 + (y0 + iy) * R + (z0 + iz);
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int m = m0 + wr * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
-        nt_st(acc[i][j][e] + biasv[i][e], yb + (size_t)m * V + v);
-      }
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Forward / backward-data, PING-PONG form of the LDS-DMA kernel above (same
-// 128 x 256 tile, 32-channel K-steps, three LDS stages, same A / B pieces).
-// There both waves of a SIMD read fragments, issue LDS-DMA and run MFMAs in
-// the same interval and meet at one barrier per step, so their matrix and
-// memory work add up (measured: no-MFMA 0.36 ms + MFMA-only 0.28 ms ~ 0.67 ms
-// as built).  Here waves 0-3 (group 0, one per SIMD, m rows 0-63) and waves
-// 4-7 (group 1, m rows 64-127) run half a step apart: in every phase one wave
-// of each SIMD issues its 24 MFMAs from registers while its partner reads the
-// next step's fragments and issues its LDS-DMA pieces, and the roles swap at
-// the phase barrier (MI355X_MICROARCH.md "Two waves per SIMD").
-//   phase 2t:   group 0 reads stage t, issues its pieces of step t + 2;
-//               group 1 computes step t - 1
-//   phase 2t+1: group 0 computes step t;
-//               group 1 reads stage t, issues its pieces of step t + 2
-// Stage t's buffer is last read in phase 2t+1, refilled (step t + 3) from
-// phase 2t+2 on; a wave's share of step t lands before the barrier that
-// opens phase 2t (counted vmcnt).  Same accumulation order per output as the
-// LDS-DMA kernel (bit-identical results).
-// ---------------------------------------------------------------------------
-template <int KT>
-__global__ void __launch_bounds__(512)
-    conv3_igemm_pp_kernel(const uint16_t* __restrict__ xh, const uint16_t* __restrict__ xl,
-                          const uint16_t* __restrict__ wh, const uint16_t* __restrict__ wl,
-                          const uint16_t* __restrict__ zrow, const float* __restrict__ bias,
-                          float* __restrict__ y, int K, int M, int R,
-                          const uint32_t* __restrict__ tmask, int mmode) {
-  constexpr int GN = kGN, NST = 3;
-  using G = GK<KT, GN>;
-  static_assert(G::NW == 8 && G::APW + G::BPW == 6, "ping-pong form: 8 waves, 6 pieces each");
-  __shared__ __attribute__((aligned(16))) uint8_t lds[NST * G::STAGE];
-  const int V = R * R * R, R2 = R * R;
-  int id = (int)blockIdx.x;
-  {
-    const int nwg = (int)gridDim.x, q = nwg / 8, rr = nwg % 8, xcd = id % 8;
-    id = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + id / 8;
-  }
-  const int nmt = M / kGM, nvt = V / GN;
-  const int m0 = (id % nmt) * kGM;
-  id /= nmt;
-  const int v0 = (id % nvt) * GN;
-  const int b = id / nvt;
-  const int t = threadIdx.x, lane = t & 63;
-  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int grp = w >> 2;                 // 0: waves 0-3, 1: waves 4-7
-  const int wr = grp, wc = w & 3, r = lane & 31, h = lane >> 5;
-  const uint32_t kAll = 0x7FFFFFFu;
-  uint32_t mask = kAll;
-  if (mmode != 0) {
-    const uint32_t mm = __builtin_amdgcn_readfirstlane(tmask[(size_t)b * (V >> 8) + (v0 >> 8)]);
-    mask = mmode == 1 ? (mm & kAll) : ((mm >> 31) ? kAll : 0u);
-  }
-  const int na = __builtin_popcount(mask);
-  const int nsteps = na * (K / KT);
-  const int first = mask != 0u ? __builtin_ctz(mask) : 0;
-  // (ichunk, itap) of the step last issued (iseq); issue() advances one step
-  int iseq = 0, ichunk = 0, itap = first;
-  const size_t bV = (size_t)b * V;
-  const int prow = lane / G::CPR, pch = lane % G::CPR;
-  const uint16_t* abase[G::APW];
-#pragma unroll
-  for (int q = 0; q < G::APW; ++q) {
-    const int I = G::APW * w + q;
-    const int row = (I % G::API) * G::RPP + prow;
-    abase[q] = ((I / G::API) ? wl : wh) + (size_t)(m0 + row) * 2 * K + ((pch ^ G::swz(row)) << 3);
-  }
-  const uint16_t* bbase[G::BPW];
-  const uint16_t* zbase[G::BPW];
-  int bxyz[G::BPW];
-#pragma unroll
-  for (int q = 0; q < G::BPW; ++q) {
-    const int I = G::BPW * w + q;
-    const int row = (I % G::BPI) * G::RPP + prow;
-    const int v = v0 + row;
-    const int cofs = (pch ^ G::swz(row)) << 3;
-    bbase[q] = ((I / G::BPI) ? xl : xh) + (bV + v) * 2 * K + cofs;
-    zbase[q] = zrow + cofs;
-    bxyz[q] = (v / R2) | (((v / R) % R) << 10) | ((v % R) << 20);
-  }
-  // this wave's 6 pieces of step sl (sl = iseq or iseq + 1) into stage buffer buf
-  auto issue = [&](int sl, int buf) {
-    {
-      const bool adv = sl != iseq;
-      const uint32_t rest = mask & ~((2u << itap) - 1u);
-      const int nt = rest != 0u ? __builtin_ctz(rest) : first;
-      ichunk += (adv && rest == 0u) ? 1 : 0;
-      itap = adv ? nt : itap;
-      iseq = sl;
-    }
-    const int c0 = ichunk * KT, tap = itap;
-    const int cof = ((c0 >> 5) << 6) + (c0 & 31);
-    uint8_t* base = lds + buf * G::STAGE;
-    const size_t aofs = (size_t)tap * M * 2 * K + cof;
-#pragma unroll
-    for (int q = 0; q < G::APW; ++q) {
-      const int I = G::APW * w + q;
-      glds16_asm(abase[q] + aofs, lds_addr(base + (I / G::API) * G::A + (I % G::API) * 1024));
-    }
-    const int dx = tap / 9 - 1, dy = (tap / 3) % 3 - 1, dz = tap % 3 - 1;
-    const long long bofs = (long long)(dx * R2 + dy * R + dz) * 2 * K + cof;
-#pragma unroll
-    for (int q = 0; q < G::BPW; ++q) {
-      const int I = G::BPW * w + q;
-      const int x = bxyz[q] & 1023, yy = (bxyz[q] >> 10) & 1023, z = bxyz[q] >> 20;
-      const bool inb = (unsigned)(x + dx) < (unsigned)R && (unsigned)(yy + dy) < (unsigned)R &&
-                       (unsigned)(z + dz) < (unsigned)R;
-      const unsigned long long src = (unsigned long long)(bbase[q] + bofs);
-      const unsigned long long zsrc = (unsigned long long)zbase[q];
-      const unsigned long long msk = 0ull - (unsigned long long)inb;
-      glds16_asm((const void*)((src & msk) | (zsrc & ~msk)),
-                 lds_addr(base + 2 * G::A + (I / G::BPI) * G::B + (I % G::BPI) * 1024));
-    }
-  };
-
-  f32x16 acc[2][2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
-
-  if (nsteps > 0) {
-    bf16x8 F[KT / 16][8];
-    issue(0, 0);
-    if (nsteps > 1) {
-      issue(1, 1);
-      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // step 0 landed (own pieces)
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();
-    for (int p = 0; p <= 2 * nsteps; ++p) {
-      // group 0: memory on even phases (step p / 2), compute on odd (step (p - 1) / 2)
-      // group 1: memory on odd phases (step (p - 1) / 2), compute on even (step p / 2 - 1)
-      const bool mem = ((p & 1) == grp);
-      const int st = grp == 0 ? (p >> 1) : ((p - 1) >> 1);  // the step of this phase's memory work
-      if (mem) {
-        if (st < nsteps) {
-          __builtin_amdgcn_sched_barrier(0);
-          if (st + 2 < nsteps) issue(st + 2, (st + 2) % NST);
-          glds_frags<KT, GN>(lds, st % NST, wr, wc, r, h, F);
-          __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): fragments in registers
-          __builtin_amdgcn_sched_barrier(0);
-        }
-      } else {
-        const int cs = grp == 0 ? ((p - 1) >> 1) : ((p >> 1) - 1);  // the step computed now
-        if (cs >= 0 && cs < nsteps) {
-          __builtin_amdgcn_sched_barrier(0);
-          glds_mfma<KT>(F, acc);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-      }
-      // before a phase 2s (group 0 reads stage s = p / 2 + 1... of the next
-      // even phase): every wave's share of that step has landed
-      if ((p & 1) == 1) {
-        const int s = (p + 1) >> 1;  // the stage group 0 reads next
-        if (s + 1 < nsteps) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      __builtin_amdgcn_s_barrier();
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  float* __restrict__ yb = y + (size_t)b * M * V;
-  float biasv[2][16];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) load_bias16(bias, m0 + wr * 64 + i * 32, h, M, biasv[i]);
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int m = m0 + wr * 64 + i * 32 + (e & 3) + 8 * (e >> 2) + 4 * h;
-        const int v = v0 + wc * 64 + j * 32 + r;
-        nt_st(acc[i][j][e] + biasv[i][e], yb + (size_t)m * V + v);
-      }
-}
-
+// (Measured and removed: a BRICK form -- 256 output voxels a 2x4x32 / 2x8x16
+// brick whose halo sits in LDS once per 16-channel chunk, all 27 taps read from
+// it: 1.25x slower, 12 MFMAs per wave between barriers -- and a PING-PONG form
+// of the LDS-DMA kernel, waves 0-3 and 4-7 half a step apart: 1.5x slower.
+// DESIGN.md section 7; both removed in round 6.)
 
 // ---------------------------------------------------------------------------
 // Weight gradient over the channels-last split operands (the forward's split
@@ -2413,26 +2013,7 @@ extern "C" size_t pcfm_conv3d_igemm_cl_workspace_bytes(int b, int cin, int cout,
   return S == 1 ? 1 : (size_t)S * b * cout * r * r * r * sizeof(float);
 }
 
-// Ping-pong form of the LDS-DMA kernel (opt-in, PCFM_CONV_PP=1: measured
-// 1.5x slower -- the memory phase, not the matrix work, sets each step)
-static bool conv_pp() {
-  static const bool on = [] {
-    const char* e = getenv("PCFM_CONV_PP");
-    return e != nullptr && e[0] == '1';
-  }();
-  return on;
-}
 
-// Halo-brick form for r = 32 / 16 (opt-in, PCFM_CONV_BRICK=1: measured 1.25x
-// slower -- 12 MFMAs per wave between barriers at 16-channel steps; the
-// per-step cost, not the B fetches, sets its pace)
-static bool conv_brick() {
-  static const bool on = [] {
-    const char* e = getenv("PCFM_CONV_BRICK");
-    return e != nullptr && e[0] == '1';
-  }();
-  return on;
-}
 
 // Slab form of the dense r = 32 / 16 launches (PCFM_CONV_SLAB=0: the LDS-DMA
 // kernel that refetches B per tap)
@@ -2448,16 +2029,6 @@ static bool conv_win() {
   return e == nullptr || e[0] != '0';
 }
 
-static bool list_gn128(long long blocks256) {
-  static const int mode = [] {
-    const char* e = getenv("PCFM_CONV_LIST_GN");
-    // default 256: the 128-entry tiles measured equal (32.24 vs 32.20 ms/step)
-    if (e == nullptr) return 0;
-    if (e[0] == 'a') return 2;  // auto
-    return atoi(e) == 128 ? 1 : 0;
-  }();
-  return mode == 1 || (mode == 2 && blocks256 <= 2LL * kCUs);
-}
 
 static int igemm_cl(const void* xs, const void* wsplit, const float* bias, int b, int cin,
                     int cout, int r, float* y, void* ws, size_t ws_bytes, void* stream,
@@ -2488,46 +2059,11 @@ static int igemm_cl(const void* xs, const void* wsplit, const float* bias, int b
 #ifndef PCFM_CONV_GK
 #define PCFM_CONV_GK 32  // 16: two blocks per CU, measured 1.15-1.18x slower
 #endif
-#ifdef PCFM_CONV_GN128
-    // 128-voxel tiles, two stages, two independent 4-wave blocks per CU
-    if (S == 1 && PCFM_CONV_GK == 32 && cin % 32 == 0) {
-      const long long blocks128 = (long long)(V / 128) * (cout / kGM) * b;
-      hipLaunchKernelGGL((conv3_igemm_glds_kernel<32, 128, 2>), dim3((unsigned)blocks128),
-                         dim3(256), 0, st, xh, xl, wh, wh + kSplitLo, zrow, bias, y, cin, cout, r, 1,
-                         part, tmask, mmode);
-      return check_launch("conv3d_igemm_cl");
-    }
-#endif
     // tile masks apply to unsplit launches only (a split's K range is a fixed
     // share of all 27 taps)
     const int mm = S == 1 && tmask != nullptr ? mmode : 0;
     const int* vl = S == 1 ? vlist : nullptr;  // the list form is unsplit
     const int* vc = S == 1 ? vcount : nullptr;
-    // list form on grids that fill the chip only once with 256-voxel tiles
-    // (r = 16 at B = 8: 256 blocks): 128-entry tiles, two 4-wave blocks per
-    // CU, so a half-empty list still keeps every CU busy (opt-in,
-    // PCFM_CONV_LIST_GN: 256 = never (default), 128 = always, auto)
-    if (vl != nullptr && PCFM_CONV_GK == 32 && cin % 32 == 0 &&
-        list_gn128(glds_blocks)) {
-      const long long blocks128 = (long long)(V / 128) * (cout / kGM) * b;
-      hipLaunchKernelGGL((conv3_igemm_glds_kernel<32, 128, 2>), dim3((unsigned)blocks128),
-                         dim3(256), 0, st, xh, xl, wh, wh + kSplitLo, zrow, bias, y, cin, cout, r, 1,
-                         part, tmask, 0, vl, vc);
-      return check_launch("conv3d_igemm_cl");
-    }
-    if (S == 1 && mm == 0 && vl == nullptr && cin % 16 == 0 && (r == 32 || r == 16) &&
-        conv_brick()) {
-      const int e = r == 32 ? allow_big_lds((const void*)conv3_igemm_brick_kernel<32>)
-                            : allow_big_lds((const void*)conv3_igemm_brick_kernel<16>);
-      if (e) return e;
-      if (r == 32)
-        hipLaunchKernelGGL(conv3_igemm_brick_kernel<32>, dim3((unsigned)glds_blocks), dim3(512),
-                           BrickGeo<32>::LDS, st, xh, wh, zrow, bias, y, cin, cout);
-      else
-        hipLaunchKernelGGL(conv3_igemm_brick_kernel<16>, dim3((unsigned)glds_blocks), dim3(512),
-                           BrickGeo<16>::LDS, st, xh, wh, zrow, bias, y, cin, cout);
-      return check_launch("conv3d_igemm_cl");
-    }
     if (S == 1 && mm == 0 && vl == nullptr && cin % 64 == 0 && (r == 32 || r == 16) &&
         conv_slab()) {  // cin % 64: an even number of 32-channel chunks (the step loop's pairs)
       const int e = r == 32 ? allow_big_lds((const void*)conv3_igemm_slab_kernel<32>)
@@ -2553,11 +2089,6 @@ static int igemm_cl(const void* xs, const void* wsplit, const float* bias, int b
         hipLaunchKernelGGL(conv3_ksum_kernel, dim3((unsigned)ceil_div(total4, 256)), dim3(256), 0,
                            st, (const float*)part, bias, S, cout, V, total4, y);
       }
-      return check_launch("conv3d_igemm_cl");
-    }
-    if (S == 1 && PCFM_CONV_GK == 32 && cin % 32 == 0 && vl == nullptr && conv_pp()) {
-      hipLaunchKernelGGL(conv3_igemm_pp_kernel<32>, dim3((unsigned)glds_blocks), dim3(512), 0, st,
-                         xh, xl, wh, wh + kSplitLo, zrow, bias, y, cin, cout, r, tmask, mm);
       return check_launch("conv3d_igemm_cl");
     }
     if (PCFM_CONV_GK == 16 || cin % 32 != 0)

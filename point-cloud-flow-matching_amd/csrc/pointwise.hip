@@ -692,238 +692,6 @@ __global__ void __launch_bounds__(kSW * 64)
 }
 #endif
 
-// ---------------------------------------------------------------------------
-// Persistent LDS-DMA form of the 256-row tile (Mpad == 256, N % 4 == 0): one
-// 512-thread block per CU walks the (batch, 128-point) tiles blockIdx.x,
-// blockIdx.x + gridDim.x, ...; its K-steps form ONE sequence across tiles, fed
-// by a ring of three LDS stages that global_load_lds_dwordx4 fills two steps
-// ahead (cdna_hip_programming.md section 5) -- the weight slice (256 rows x 32
-// channels, bf16 hi and lo, 16-B chunks XOR-swizzled on the source side so the
-// ds_read_b128 fragment reads are conflict-free, as conv3_igemm_glds_kernel)
-// and the x slice as it lies in memory (32 channel rows x 128 points fp32,
-// 16-B chunks of row k xor 8 (k >> 3 & 1): the two lane halves of a fragment
-// read hit disjoint banks).  No VGPR staging and one barrier per step: each
-// wave reads its B fragments straight from the fp32 rows (8 ds_read_b32, one
-// address + immediates) and splits them to bf16 hi / lo in registers with the
-// rounding of store_split, and the MFMAs run in pw_gemm256_kernel's order, so
-// the results are bit-identical to it.  Points >= N read the tile's last four
-// points (never stored, never in the statistics); channels >= K read channel
-// K - 1 against zero weight rows.
-// ---------------------------------------------------------------------------
-constexpr int kPgTN = 128;            // points per tile
-constexpr int kPgStages = 3;          // ring depth (weights and x each)
-constexpr int kPgA = 256 * kKT * 2;   // one weight image slice (hi or lo): 16 KiB
-constexpr int kPgAS = 2 * kPgA;       // weight stage (hi + lo): 32 KiB
-constexpr int kPgX = kKT * kPgTN * 4; // x stage, fp32: 16 KiB
-constexpr int kPgXBase = kPgStages * kPgAS;
-
-__device__ __forceinline__ int pg_swzA(int row) { return (row >> 2) & 3; }
-
-// LDS-DMA of 16 B per lane from sbase + voff into lds + 16 lane (M0 set and
-// restored inside the statement; hipcc does not see the load, completion is
-// counted by hand)
-__device__ __forceinline__ void pg_glds(const void* sbase, uint32_t voff, uint32_t lds) {
-  unsigned keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(voff), "s"(sbase), "s"(lds)
-      : "memory");
-}
-
-__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2, 2)))
-    pw_glds256_kernel(const Parts x, const uint16_t* __restrict__ wh,
-                      const uint16_t* __restrict__ wl, const float* __restrict__ bias,
-                      int bias_bstride, const Parts y, int K, int M, int N, int Kpad, int nb,
-                      float2* __restrict__ stats) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[kPgStages * (kPgAS + kPgX)];
-  const int ntp = (N + kPgTN - 1) / kPgTN, ntiles = nb * ntp;
-  const int G = (int)gridDim.x, blk = (int)blockIdx.x;
-  const int nsteps = Kpad / kKT;
-  const int mytiles = blk < ntiles ? (ntiles - blk + G - 1) / G : 0;
-  const int total = mytiles * nsteps;
-  if (total == 0) return;
-  const int t = threadIdx.x, lane = t & 63;
-  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
-  const int wr = w >> 1, wc = w & 1, r = lane & 31, h = lane >> 5;
-  const uint32_t lds0 = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)lds;
-
-  // weight pieces I = 4 w + q (image I / 16, rows (I % 16) * 16 + lane / 4):
-  // byte offsets in the image at K-step 0
-  uint32_t aoff[4];
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int I = 4 * w + q, row = (I % 16) * 16 + lane / 4;
-    aoff[q] = (uint32_t)(row * Kpad * 2 + (((lane & 3) ^ pg_swzA(row)) << 4));
-  }
-  // x pieces J = 2 w + q: channel row 2 J + lane / 32, logical 16-B chunk
-  // (lane & 31) ^ (8 when the row's bit 3 is set)
-  int xrow[2], xpt[2];
-#pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const int row = 2 * (2 * w + q) + lane / 32;
-    xrow[q] = row;
-    xpt[q] = 4 * ((lane & 31) ^ (((row >> 3) & 1) << 3));
-  }
-
-  // The weights and x of step k go to slot k % 3 of their own rings; x is
-  // read one step earlier (fragment prefetch), so it is issued one step
-  // further ahead: step g issues weights g + 2 and x g + 3.
-  int ia = 0;                    // next weight step to issue (its K-step = ia % nsteps)
-  int ix_tile = blk, ix_s = 0;   // next x step to issue
-  int ix = 0;
-  auto issue_a = [&]() {
-    const int c0 = (ia % nsteps) * kKT;
-    const uint32_t base = lds0 + (ia % kPgStages) * kPgAS;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int I = 4 * w + q;
-      const uint16_t* img = (I / 16) ? wl : wh;
-      pg_glds(img + c0, aoff[q], base + (I / 16) * kPgA + (I % 16) * 1024);
-    }
-    ++ia;
-  };
-  auto issue_x = [&]() {
-    const int bb = ix_tile / ntp, p0 = (ix_tile - bb * ntp) * kPgTN;
-    const int c0 = ix_s * kKT;
-    const uint32_t base = lds0 + kPgXBase + (ix % kPgStages) * kPgX;
-    // the 32 channels of a step lie in one part (parts are 32-aligned)
-    const int cb = __builtin_amdgcn_readfirstlane(min(c0, K - 1));
-    const float* xr = x.row(bb, cb, N);
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-      const int J = 2 * w + q;
-      const int c = min(c0 + xrow[q], K - 1);
-      const int p = min(p0 + xpt[q], N - 4);
-      pg_glds(xr, (uint32_t)(((c - cb) * N + p) * 4), base + J * 1024);
-    }
-    ++ix;
-    if (++ix_s == nsteps) {
-      ix_s = 0;
-      ix_tile += G;
-    }
-  };
-
-  f32x16 acc[2][2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
-
-  // this lane's B-fragment address in an x stage: channel row 8 h (+ 16 kk +
-  // jj), point n = wc 64 + j 32 + r in physical chunk (n >> 2) ^ 8 h
-  uint32_t xoff[2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int n = wc * 64 + j * 32 + r;
-    xoff[j] = (uint32_t)(8 * h * kPgTN * 4 + ((((n >> 2) ^ (8 * h)) << 4) | ((n & 3) * 4)));
-  }
-
-  // B rows double-buffered across steps: after the barrier of step g the
-  // waves read step g + 1's x values while step g's MFMAs run.  (Both operands
-  // double-buffered spill at 256 registers: 240 us at 8 x 256 x 256 x 20000.)
-  struct Frags {
-    float x[2][2][8];  // [kk][j][8 channels]
-  };
-  auto read_x = [&](int k, Frags& F) {
-    const uint8_t* base = lds + kPgXBase + (k % kPgStages) * kPgX;
-#pragma unroll
-    for (int kk = 0; kk < kKT / 16; ++kk)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const float* xp = reinterpret_cast<const float*>(base + xoff[j] + kk * 16 * kPgTN * 4);
-#pragma unroll
-        for (int jj = 0; jj < 8; ++jj) F.x[kk][j][jj] = xp[jj * kPgTN];
-      }
-  };
-  auto mfma_step = [&](int k, const Frags& F) {
-    const uint8_t* base = lds + (k % kPgStages) * kPgAS;
-#pragma unroll
-    for (int kk = 0; kk < kKT / 16; ++kk) {
-      const int kc = 2 * kk + h;
-      bf16x8 ah[2], al[2], bh[2], bl[2];
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int row = wr * 64 + i * 32 + r;
-        const int off = row * (kKT * 2) + ((kc ^ pg_swzA(row)) << 4);
-        ah[i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(base + off));
-        al[i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(base + kPgA + off));
-      }
-#pragma unroll
-      for (int j = 0; j < 2; ++j) bh[j] = split8(F.x[kk][j], bl[j]);
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
-        }
-    }
-  };
-
-  int tile = blk, s = 0;
-  // step g: wait for the pieces issued two steps before (weights g, x g + 1)
-  // -- the previous step's (weights g + 1, x g + 2) stay in flight, and
-  // epilogue stores issued after them only make the wait longer -- then the
-  // barrier makes everyone's visible and ends every wave's reads of weights
-  // g - 1 and x g, whose slots this step refills.
-  auto step = [&](int g, const Frags& Fc, Frags& Fn) {
-    if (g + 2 < total)
-      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    else if (g + 1 < total)
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    if (g + 2 < total) issue_a();
-    if (g + 3 < total) issue_x();
-    if (g + 1 < total) read_x(g + 1, Fn);
-    mfma_step(g, Fc);
-    if (++s == nsteps) {
-      const int bb = tile / ntp, p0 = (tile - bb * ntp) * kPgTN;
-      pw256_epilogue(acc, y, bias != nullptr ? bias + bb * bias_bstride : nullptr, bb, nb, M, N,
-                     0, p0, wr, wc, r, h, stats);
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-          for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.0f;
-      s = 0;
-      tile += G;
-    }
-  };
-
-  // prologue: x 0, then weights 0 + x 1 (step 0's wait), then weights 1 + x 2
-  issue_x();
-  issue_a();
-  if (total > 1) issue_x();
-  if (total > 1) issue_a();
-  if (total > 2) issue_x();
-  // x 0 landed (the last one or two groups may stay in flight)
-  if (total > 2)
-    asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
-  else if (total > 1)
-    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-  else
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  Frags F0, F1;
-  read_x(0, F0);
-  int g = 0;
-  for (; g + 1 < total; g += 2) {
-    step(g, F0, F1);
-    step(g + 1, F1, F0);
-  }
-  if (g < total) step(g, F0, F1);
-  // every issued piece was waited for (the last step waits vmcnt(0))
-}
-
 // dW partials: grid = (ceil(Cout/128) * ceil(Cin/128), S); K-steps of 32
 // points (a step never crosses a batch element).  part [S][Cout][Cin].
 #ifdef PCFM_PW_WG_WAVES
@@ -1258,30 +1026,19 @@ extern "C" int pcfm_pointwise_prep_weight(const float* w, int cout, int cin, int
 // The forward GEMM's kernel for a shape: ONE decision, used by the launcher
 // and by pcfm_pointwise_bnstats_groups(), so a caller is never told that a
 // shape writes BatchNorm statistics when the kernel that runs does not.
-enum class PwPath { Stream128, StreamM, Glds256, Tile256, Tile128, Tile64 };
+// (Measured and removed in round 6, with their A/B final: the 128-row streaming
+// kernel in 128-row slices for M > 128 -- correct, slower: 256->256 forward 98.9
+// vs 88.9 us, profiles/r05_ab_pw_stream_m.jsonl -- and the persistent LDS-DMA
+// 256-row form -- bit-identical, 106.6 vs 94.0 us, profiles/r05_ab_pw_glds256.jsonl.)
+enum class PwPath { Stream128, Tile256, Tile128, Tile64 };
 
 static PwPath pw_path(int b, int cin, int cout, int n) {
   const int Mpad = pw_mpad(cout), Kpad = pad_to(cin, kKT);
   const long long big = (long long)ceil_div(n, 128) * (Mpad / 128) * b;
 #ifndef PCFM_PW_NOSTREAM
   if (Mpad == 128 && Kpad <= 256 && cin % 32 == 0 && cout % 32 == 0) return PwPath::Stream128;
-  // M > 128 as 128-row slices of the streaming kernel: opt-in measurement form
-  // (PCFM_PW_STREAM_M=1; re-measured in round 5 with its missing statistics
-  // epilogue reported -- see DESIGN.md section 5)
-  const char* sm = std::getenv("PCFM_PW_STREAM_M");
-  if (sm != nullptr && sm[0] == '1' && Mpad % 128 == 0 && Kpad <= 256 && cin % 32 == 0 &&
-      cout % 32 == 0)
-    return PwPath::StreamM;
 #endif
 #ifndef PCFM_PW_NO256
-#ifndef PCFM_PW_NOGLDS
-  // PCFM_PW_GLDS=1 selects the persistent LDS-DMA form (same results, bit for
-  // bit: tests/test_gpu_pointwise.py); measured slower than the register-staged
-  // tile, so it is opt-in
-  const char* ge = std::getenv("PCFM_PW_GLDS");
-  if (Mpad == 256 && n % 4 == 0 && big / 2 >= 2 * kCUs && ge != nullptr && ge[0] == '1')
-    return PwPath::Glds256;
-#endif
   if (Mpad % 256 == 0 && big / 2 >= 2 * kCUs) return PwPath::Tile256;
 #endif
   return big >= 2 * kCUs ? PwPath::Tile128 : PwPath::Tile64;
@@ -1294,7 +1051,7 @@ static bool pw_path_has_stats(PwPath p) {
     const char* e = std::getenv("PCFM_PW_STREAM_STATS");
     return PCFM_PW_STREAM_PF < 2 && (e == nullptr || e[0] != '0');
   }
-  return p == PwPath::Tile256 || p == PwPath::Glds256;
+  return p == PwPath::Tile256;
 }
 static int pw_stats_group(PwPath p) { return p == PwPath::Stream128 ? 32 : 64; }
 
@@ -1310,7 +1067,7 @@ static int pw_gemm_launch(const Parts& x, const void* wsplit, const float* bias,
   PCFM_CHECK_ARG(stats == nullptr || pw_path_has_stats(path),
                  "pointwise_gemm: BatchNorm statistics requested for a shape whose kernel has "
                  "no statistics epilogue (b=%d cin=%d cout=%d n=%d)", b, cin, cout, n);
-  if (path == PwPath::Stream128 || path == PwPath::StreamM) {
+  if (path == PwPath::Stream128) {
     const uint16_t* wl_img = wh + total;
     const long long tiles = (long long)b * ceil_div(n, 32);
     const size_t lds = (size_t)2 * 128 * (Kpad + 8) * sizeof(uint16_t);
@@ -1340,12 +1097,6 @@ static int pw_gemm_launch(const Parts& x, const void* wsplit, const float* bias,
       set_error("pointwise_gemm: launch failed");
       return (int)le;
     }
-    return check_launch("pointwise_gemm");
-  }
-  if (path == PwPath::Glds256) {
-    const int tiles = b * ceil_div(n, kPgTN);
-    hipLaunchKernelGGL(pw_glds256_kernel, dim3(std::min(tiles, kCUs)), dim3(512), 0, st, x, wh,
-                       wh + total, bias, bias_bstride, y, cin, cout, n, Kpad, b, stats);
     return check_launch("pointwise_gemm");
   }
   if (path == PwPath::Tile256) {

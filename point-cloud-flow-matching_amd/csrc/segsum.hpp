@@ -392,25 +392,6 @@ constexpr int kItems = PCFM_SEG_ITEMS;  // target items per work unit
 constexpr int kInFlight = 16;    // feature-row loads issued back to back per wave
 constexpr int kUnitWaves = 4;    // waves (independent units) per block
 
-// 2 x 2-column tiles of the trilinear scatter (seg_unit_gather_quad_kernel below)
-constexpr int kQuadMaxR = 16;
-constexpr int kQuadTV = 4 * kQuadMaxR;  // voxels per quad tile (at most)
-
-__host__ __device__ inline int seg_quad_tiles(int r) { return (r / 2) * (r / 2); }
-
-// source keys [lo, hi) of range g (x = x0 - 1 + g, y in [y0 - 1, y0 + 1]) of a quad tile
-__device__ __forceinline__ void seg_quad_range(int r, int tile, int g, int& lo, int& hi) {
-  const int hr = r >> 1, tx = tile / hr;
-  const int x0 = 2 * tx, y0 = 2 * (tile - tx * hr);
-  const int xq = x0 - 1 + g;
-  if (xq < 0 || xq >= r) {
-    lo = hi = 0;
-    return;
-  }
-  lo = (xq * r + max(y0 - 1, 0)) * r;
-  hi = (xq * r + min(y0 + 2, r)) * r;
-}
-
 template <int TAPS>
 constexpr int seg_ranges() { return TAPS == 8 ? 4 : 1; }
 
@@ -437,8 +418,7 @@ __device__ __forceinline__ int seg_range_bound(const int* sb, int v0, int V, int
 template <int TAPS>
 __global__ void __launch_bounds__(1024)
     seg_units_kernel(const int* __restrict__ start, int V, int r, int tiles, int umax,
-                     int4* __restrict__ units, int2* __restrict__ tinfo, int* __restrict__ nunits,
-                     int quad = 0) {
+                     int4* __restrict__ units, int2* __restrict__ tinfo, int* __restrict__ nunits) {
   __shared__ int wsum[16];
   constexpr int NR = seg_ranges<TAPS>();
   const int b = blockIdx.x;
@@ -448,14 +428,7 @@ __global__ void __launch_bounds__(1024)
   for (int t0 = 0; t0 < tiles; t0 += 1024) {
     const int tile = t0 + t;
     int T = 0, P = 0;
-    if (tile < tiles && quad) {  // 2 x 2-column tiles (seg_unit_gather_quad_kernel)
-      for (int g = 0; g < 3; ++g) {
-        int lo, hi;
-        seg_quad_range(r, tile, g, lo, hi);
-        T += sb[hi] - sb[lo];
-      }
-      P = max(1, (T + kItems - 1) / kItems);
-    } else if (tile < tiles) {
+    if (tile < tiles) {
       const int v0 = tile * kTV;
 #pragma unroll
       for (int g = 0; g < NR; ++g) {
@@ -696,196 +669,6 @@ __global__ void __launch_bounds__(256)
   }
 }
 
-// --------------------------------------------------------------------------
-// 2 x 2-column tiles for the trilinear scatter (TAPS == 8, even r <= 16; the
-// devoxelization backward at the r = 16 / 8 stages).  A kTV tile is a z-run of
-// ONE column (x, y) and pulls the four source columns (x - dx, y - dy): every
-// sorted row is read by four tiles (~4x the rows from L2 / HBM).  A quad tile
-// is the full z-range of the four columns (x0 + {0, 1}, y0 + {0, 1}), x0 and
-// y0 even: its sources are the 3 x 3 columns x0 - 1 .. x0 + 1, y0 - 1 .. y0 + 1,
-// i.e. three sorted ranges (the y-rows of one x are consecutive keys), and a
-// row is read by 2.25 tiles on average (1 or 2 in x times 1 or 2 in y).  Each
-// row adds its 8 taps into the tile's 4 r voxels in the wave's LDS tile; runs
-// of rows in one cell are accumulated in registers (8 accumulators) and added
-// when the cell changes.  Same unit / partial-tile machinery as above.
-// --------------------------------------------------------------------------
-
-// grid = (ceil(umax / kUnitWaves), ceil(C/64), B), kUnitWaves * 64 threads.
-__global__ void __launch_bounds__(kUnitWaves * 64)
-    seg_unit_gather_quad_kernel(const float* __restrict__ xs, const int* __restrict__ skey,
-                                const float* __restrict__ ws8, const int* __restrict__ start,
-                                const int4* __restrict__ units, const int* __restrict__ nunits,
-                                int C, int n, int V, int r, int umax, int tiles, int slots,
-                                float* __restrict__ out, float* __restrict__ partial) {
-  __shared__ float lds[kUnitWaves][kQuadTV * 65];
-  int bx, by, bz;
-  {  // XCD-contiguous deal, as seg_unit_gather_kernel
-    const int gx = (int)gridDim.x, gy = (int)gridDim.y;
-    const int tot = gx * gy * (int)gridDim.z;
-    int id = (int)(blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z));
-    const int q = tot / 8, rr = tot % 8, xcd = id % 8;
-    id = (xcd < rr ? xcd * (q + 1) : rr * (q + 1) + (xcd - rr) * q) + id / 8;
-    bx = id % gx;
-    by = (id / gx) % gy;
-    bz = id / (gx * gy);
-  }
-  const int b = bz, c0 = by * 64;
-  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  const int nu = nunits[b];
-  const int u = bx * kUnitWaves + w;
-  if (u >= nu) return;  // wave-uniform; no block barrier below
-  const int4 un = units[(size_t)b * umax + u];
-  const int tile = un.x, part = un.y, parts = un.z, T = un.w;
-  const int hr = r >> 1, txi = tile / hr;
-  const int x0 = 2 * txi, y0 = 2 * (tile - txi * hr), TV = 4 * r, r2 = r * r;
-  const int c = c0 + lane;
-  const bool cok = c < C;
-  const int* __restrict__ sb = start + (size_t)b * (V + 1);
-  const int* __restrict__ kb = skey + (size_t)b * n;
-  const float* __restrict__ xb = xs + (size_t)b * n * C + (cok ? c : 0);
-  const float* __restrict__ wb = ws8 + (size_t)b * n * 8;
-
-  int bnd = 0;
-  if (lane < 6) {
-    int lo, hi;
-    seg_quad_range(r, tile, lane >> 1, lo, hi);
-    bnd = sb[(lane & 1) ? hi : lo];
-  }
-  int rs[3], pre[4];
-  pre[0] = 0;
-#pragma unroll
-  for (int g = 0; g < 3; ++g) {
-    rs[g] = __builtin_amdgcn_readlane(bnd, 2 * g);
-    pre[g + 1] = pre[g] + __builtin_amdgcn_readlane(bnd, 2 * g + 1) - rs[g];
-  }
-  const int i0 = (int)((long long)T * part / parts);
-  const int i1 = (int)((long long)T * (part + 1) / parts);
-
-  float* tl = lds[w];
-  for (int e = lane; e < TV * 65; e += 64) tl[e] = 0.0f;
-
-  // run state: the cell's key and its place relative to the tile, packed as
-  // ((x - x0 + 1) << 10) | ((y - y0 + 1) << 8) | z (wave-uniform)
-  int cur = -1, ccode = 0;
-  float a[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) a[k] = 0.0f;
-  auto flush = [&]() {
-    if (cur < 0) return;
-    const int tx0 = (ccode >> 10) - 1, ty0 = ((ccode >> 8) & 3) - 1, zq = ccode & 255;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {  // tap k = 4 dx + 2 dy + dz -> voxel (x + dx, y + dy, z + dz)
-      const int tx = tx0 + (k >> 2), ty = ty0 + ((k >> 1) & 1), z = zq + (k & 1);
-      if ((unsigned)tx < 2u && (unsigned)ty < 2u && z < r) {
-        float* d = tl + ((tx * 2 + ty) * r + z) * 65 + lane;
-        *d = *d + a[k];
-      }
-    }
-  };
-
-  for (int base = i0; base < i1; base += 64) {
-    const int m = min(64, i1 - base);
-    const int it = base + lane;
-    int pos = 0, key = -1, code = 0;
-    float wv[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) wv[k] = 0.0f;
-    if (lane < m) {
-      const int g = (it >= pre[1] ? 1 : 0) + (it >= pre[2] ? 1 : 0);
-      pos = (g == 0 ? rs[0] : g == 1 ? rs[1] : rs[2]) + it - (g == 0 ? 0 : g == 1 ? pre[1] : pre[2]);
-      key = kb[pos];
-      const int xq = key / r2, rem = key - xq * r2, yq = rem / r, zq = rem - yq * r;
-      code = ((xq - x0 + 1) << 10) | ((yq - y0 + 1) << 8) | zq;
-      const float4 wa = *reinterpret_cast<const float4*>(wb + (size_t)pos * 8);
-      const float4 wc = *reinterpret_cast<const float4*>(wb + (size_t)pos * 8 + 4);
-      wv[0] = wa.x;
-      wv[1] = wa.y;
-      wv[2] = wa.z;
-      wv[3] = wa.w;
-      wv[4] = wc.x;
-      wv[5] = wc.y;
-      wv[6] = wc.z;
-      wv[7] = wc.w;
-    }
-    for (int u0 = 0; u0 < m; u0 += kInFlight) {
-      float x[kInFlight];
-      // unconditional: lanes >= m hold pos = 0, a valid row
-#pragma unroll
-      for (int q = 0; q < kInFlight; ++q)
-        x[q] = xb[(size_t)__builtin_amdgcn_readlane(pos, u0 + q) * C];
-      const int cnt = min(kInFlight, m - u0);
-#pragma unroll
-      for (int q = 0; q < kInFlight; ++q) {
-        if (q < cnt) {
-          const int kq = __builtin_amdgcn_readlane(key, u0 + q);
-          if (kq != cur) {
-            flush();
-            cur = kq;
-            ccode = __builtin_amdgcn_readlane(code, u0 + q);
-#pragma unroll
-            for (int k = 0; k < 8; ++k) a[k] = 0.0f;
-          }
-#pragma unroll
-          for (int k = 0; k < 8; ++k) a[k] = a[k] + rl_f(wv[k], u0 + q) * x[q];
-        }
-      }
-    }
-  }
-  flush();
-
-  // tile -> global: voxel vi = (tx 2 + ty) r + z of the tile
-  const int nch = 64 / min(64, TV);  // channels per pass (TV < 64: several)
-  const int vi = lane % TV, cc0 = lane / TV;
-  const int tx = vi / (2 * r), ty = (vi / r) & 1, z = vi - (vi / r) * r;
-  const size_t v = (size_t)(x0 + tx) * r2 + (size_t)(y0 + ty) * r + z;
-  for (int k = 0; k < 64; k += nch) {
-    const int cc = k + cc0, cg = c0 + cc;
-    if (cc0 < nch && cg < C) {  // 64 % TV != 0 (r = 6, 10, ...): the last lanes idle
-      for (int vv = vi; vv < TV; vv += 64) {  // TV > 64 does not occur (r <= 16)
-        const float val = tl[vv * 65 + cc];
-        if (part == 0) {
-          out[((size_t)b * C + cg) * V + v] = val;
-        } else {
-          partial[(((size_t)b * slots + (size_t)(u - tile - 1)) * C + cg) * TV + vv] = val;
-        }
-      }
-    }
-  }
-}
-
-// out += partial quad tiles 1 .. P-1, in unit order; grid = (tiles, ceil(C/64), B).
-__global__ void __launch_bounds__(256)
-    seg_part_sum_quad_kernel(const int2* __restrict__ tinfo, const float* __restrict__ partial,
-                             int C, int V, int r, int tiles, int slots, float* __restrict__ out) {
-  const int b = blockIdx.z, tile = blockIdx.x, c0 = blockIdx.y * 64;
-  const int2 ti = tinfo[(size_t)b * tiles + tile];
-  if (ti.x <= 1) return;
-  const int hr = r >> 1, txi = tile / hr;
-  const int x0 = 2 * txi, y0 = 2 * (tile - txi * hr), TV = 4 * r;
-  for (int e = threadIdx.x; e < 64 * TV; e += 256) {
-    const int cc = e / TV, vi = e - cc * TV;
-    const int cg = c0 + cc;
-    if (cg < C) {
-      const int tx = vi / (2 * r), ty = (vi / r) & 1, z = vi - (vi / r) * r;
-      const size_t o = ((size_t)b * C + cg) * V + (size_t)(x0 + tx) * r * r + (size_t)(y0 + ty) * r + z;
-      const float* pp = partial + (((size_t)b * slots + ti.y) * C + cg) * TV + vi;
-      const size_t ps = (size_t)C * TV;  // one partial tile
-      float sum = out[o];
-      int p = 0;
-      for (; p + 8 <= ti.x - 1; p += 8) {
-        float x[8];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) x[q] = pp[(size_t)(p + q) * ps];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) sum = sum + x[q];
-      }
-      for (; p < ti.x - 1; ++p) sum = sum + pp[(size_t)p * ps];
-      out[o] = sum;
-    }
-  }
-}
-
 }  // namespace
 
 // --------------------------------------------------------------------------
@@ -896,22 +679,10 @@ __global__ void __launch_bounds__(256)
 // kItems of range items (an item lies in at most 2 tiles per stencil column).
 inline int seg_tiles(int V) { return (V + kTV - 1) / kTV; }
 
-// The trilinear scatter takes 2 x 2-column tiles at even r <= 16 when
-// PCFM_DEVOX_QUAD=1 (opt-in: measured slower than the one-column tiles, see
-// DESIGN.md section 5 -- the gather is issue-bound, not HBM-bound)
-inline int seg_cube_root(int V) {
-  int r = 0;
-  while ((long long)(r + 1) * (r + 1) * (r + 1) <= V) ++r;
-  return r;
-}
-inline bool seg_quad(int taps, int V) {
-  // read per call (cheap) so a test can compare both forms in one process; a
-  // plan and its applies must see the same setting
-  const char* e = std::getenv("PCFM_DEVOX_QUAD");
-  const bool on = e != nullptr && e[0] == '1';
-  const int r = seg_cube_root(V);
-  return on && taps == 8 && r * r * r == V && r % 2 == 0 && r >= 2 && r <= kQuadMaxR;
-}
+// (Round 5 built 2 x 2-column tiles for the trilinear scatter -- a row read by
+// 2.25 tiles instead of 4 -- bit-identical to the column tiles and slower:
+// the gather is issue-bound; profiles/r05_ab_devox_quad.jsonl.  Removed in
+// round 6.)
 inline int seg_umax(int n, int V, int taps) {
   return seg_tiles(V) + (int)(((long long)(taps == 8 ? 8 : 1) * n + kItems - 1) / kItems) + 1;
 }
@@ -950,12 +721,7 @@ inline size_t seg_plan_bytes(int B, int n, int V, int taps) {
 }
 inline size_t seg_apply_bytes(int B, int C, int n, int V, int taps) {
   const int umax = seg_umax(n, V, taps), tiles = seg_tiles(V);
-  size_t part = (size_t)B * (umax - tiles) * std::max(C, 1) * kTV * 4;
-  if (taps == 8) {  // room for the quad tiles' partials too (4 r voxels each)
-    const int r = seg_cube_root(V);
-    if (r * r * r == V && r % 2 == 0 && r <= kQuadMaxR)
-      part = std::max(part, (size_t)B * (umax - seg_quad_tiles(r)) * std::max(C, 1) * 4 * r * 4);
-  }
+  const size_t part = (size_t)B * (umax - tiles) * std::max(C, 1) * kTV * 4;
   return align256((size_t)B * n * std::max(C, 1) * 4) + align256(part);
 }
 inline size_t seg_ws_bytes(int B, int C, int n, int V, int taps) {
@@ -1013,10 +779,9 @@ inline int seg_plan_build(const int* key, long long key_bstride, bool avg, const
                      key, key_bstride, n, V, seg_sort_span(V), w.start, cnt_out,
                      avg ? w.vinv : nullptr, w.rank);
 #endif
-  const bool quad = seg_quad(TAPS, V);
-  const int tiles = quad ? seg_quad_tiles(r) : seg_tiles(V), umax = seg_umax(n, V, TAPS);
+  const int tiles = seg_tiles(V), umax = seg_umax(n, V, TAPS);
   hipLaunchKernelGGL(seg_units_kernel<TAPS>, dim3(B), dim3(1024), 0, st, w.start, V, r, tiles,
-                     umax, w.units, w.tinfo, w.nunits, quad ? 1 : 0);
+                     umax, w.units, w.tinfo, w.nunits);
   if (n > 0)
     hipLaunchKernelGGL(seg_plan_rows_kernel, dim3(ceil_div(n, 256), B), dim3(256), 0, st, w.rank,
                        key, key_bstride, TAPS == 8 ? tapw : nullptr, n, w.skey, w.ws8);
@@ -1036,15 +801,6 @@ inline int seg_apply(const float* in, const SegPlan& w, bool avg, int r, int B, 
                        dim3(256), 0, st, in, w.rank, nullptr, 0LL, nullptr, C, n, aw.xs, nullptr,
                        nullptr);
   const int gx = ceil_div(umax, kUnitWaves);
-  if (seg_quad(TAPS, V)) {
-    const int qt = seg_quad_tiles(r), qslots = umax - qt;
-    hipLaunchKernelGGL(seg_unit_gather_quad_kernel, dim3(gx, ceil_div(C, 64), B),
-                       dim3(kUnitWaves * 64), 0, st, aw.xs, w.skey, w.ws8, w.start, w.units,
-                       w.nunits, C, n, V, r, umax, qt, qslots, out, aw.partial);
-    hipLaunchKernelGGL(seg_part_sum_quad_kernel, dim3(qt, ceil_div(C, 64), B), dim3(256), 0, st,
-                       w.tinfo, aw.partial, C, V, r, qt, qslots, out);
-    return PCFM_OK;
-  }
   hipLaunchKernelGGL(seg_unit_gather_kernel<TAPS>, dim3(gx, ceil_div(C, 64), B),
                      dim3(kUnitWaves * 64), 0, st, aw.xs, w.skey, w.ws8, w.start,
                      avg ? w.vinv : nullptr, w.units, w.nunits, C, n, V, r, umax, slots, out,

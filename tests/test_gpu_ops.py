@@ -509,30 +509,3 @@ def test_emd_rowpass_form_matches_split_form(tmp_path, report):
                          "rowpass_ms": res["rowpass"]["approxmatch_ms_b8_n2048"],
                          "rowpass_unfused_ms": res["unfused"]["approxmatch_ms_b8_n2048"],
                          "max_rel_diff_f32": worst})
-
-
-@pytest.mark.parametrize("b,c,n,r", [(8, 256, 20000, 16), (8, 256, 20000, 8), (2, 64, 5000, 2),
-                                     (3, 100, 3000, 6), (2, 128, 20000, 32)])
-def test_devox_backward_quad_tiles_match_column_tiles(monkeypatch, b, c, n, r):
-    """The devoxelization backward on 2 x 2-column tiles (segsum.hpp
-    seg_unit_gather_quad_kernel, even r <= 16, opt-in PCFM_DEVOX_QUAD=1) against
-    the one-column tiles (the default): the same sums in another order (1e-5), each form
-    deterministic.  r = 2 puts ~600 points in a cell (crowded tiles, many
-    partial units); r = 6 a ragged channel group; r = 32 takes the column
-    tiles in both runs."""
-    from pcfm import ops
-    g = torch.Generator(device=DEV).manual_seed(b * c + r)
-    pts = torch.rand(b, 3, n, device=DEV, generator=g) * (r - 1)
-    pts[:, :, : n // 8] = pts[:, :, : n // 8].round()
-    pts[:, :, -1] = r - 1
-    grid = torch.randn(b, c, r ** 3, device=DEV, generator=g)
-    _, inds, wgts = ops.trilinear_devoxelize_forward(r, True, pts, grid)
-    gy = torch.randn(b, c, n, device=DEV, generator=g)
-    monkeypatch.setenv("PCFM_DEVOX_QUAD", "0")
-    ref = ops.trilinear_devoxelize_backward(gy, inds, wgts, r)
-    monkeypatch.setenv("PCFM_DEVOX_QUAD", "1")
-    q1 = ops.trilinear_devoxelize_backward(gy, inds, wgts, r)
-    q2 = ops.trilinear_devoxelize_backward(gy, inds, wgts, r)
-    assert torch.equal(q1, q2)
-    scale = float(ref.abs().max())
-    torch.testing.assert_close(q1, ref, rtol=1e-5, atol=1e-6 * scale)
