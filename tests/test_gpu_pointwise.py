@@ -184,8 +184,23 @@ def test_pointwise_256_row_shapes(ops, b, cin, cout, n):
     y = ops.pointwise_forward(x, w, bias)
     fs = ops.pointwise_forward_bnstats(x, w, bias)
     assert fs is not None or cout != 256
-    if fs is not None:
+    if fs is not None:  # per (channel, 64-point group): the group's mean and centred sum of squares
         assert torch.equal(fs[0], y)
+        st = fs[1]
+        ng = st.shape[1] // b
+        G = (n + ng - 1) // ng
+        yd = torch.nn.functional.pad(y.double(), (0, ng * G - n)).view(b, cout, ng, G)
+        cnt = torch.full((ng,), float(G), device="cuda", dtype=torch.float64)
+        cnt[-1] = n - (ng - 1) * G
+        mean = yd.sum(-1) / cnt
+        valid = (torch.arange(G, device="cuda")[None, :]
+                 + G * torch.arange(ng, device="cuda")[:, None]) < n
+        m2 = (((yd - mean[..., None]) ** 2) * valid).sum(-1)
+        ref = torch.stack([mean, m2], -1).permute(1, 0, 2, 3).reshape(cout, b * ng, 2)
+        scale = y.double().abs().max()
+        assert torch.allclose(st[..., 0].double(), ref[..., 0], rtol=1e-5, atol=1e-6 * scale)
+        assert torch.allclose(st[..., 1].double(), ref[..., 1], rtol=1e-4,
+                              atol=1e-5 * scale ** 2 * G)
     dx = ops.pointwise_backward_data(gy, w)
     x64, w64 = x[:1].double().cpu(), w[:, :, 0].double().cpu()
     y64 = torch.einsum("oc,bcn->bon", w64, x64) + bias.double().cpu()[:, None]

@@ -29,6 +29,7 @@ def timeit(fn, it=20):
 
 
 res = {"tag": sys.argv[1] if len(sys.argv) > 1 else os.environ.get("PCFM_LIB", "main")}
+OUT = {}
 g = torch.Generator(device="cuda").manual_seed(0)
 b = 8
 for c, r in ((128, 32), (256, 16), (256, 8)):
@@ -43,6 +44,15 @@ for c, r in ((128, 32), (256, 16), (256, 8)):
     y = ops.conv3d_igemm_split(xs, img_f, None, b, c, c, r, "f")
     ref = torch.nn.functional.conv3d(x, w, padding=1)
     err = float((y - ref).abs().max() / ref.abs().max())
+    # the weight gradient (small) and a 1/64 sample of the forward output
+    OUT[f"C{c}R{r}"] = (y.flatten()[::64].cpu(), ops.conv3d_wgrad_split(xs, gys, b, c, c, r).cpu())
     res[f"C{c}R{r}"] = {"fwd_ms": tf, "wgrad_ms": tw, "fwd_TF_fp32eq": flops / tf / 1e9,
                         "wgrad_TF_fp32eq": flops / tw / 1e9, "fwd_rel_err": err}
+save = os.environ.get("CONV_SAVE")  # outputs for a bitwise comparison across variants
+if save:
+    if os.path.exists(save):
+        ref = torch.load(save, weights_only=True)
+        res["bit_equal_to_saved"] = all(torch.equal(a, c) for k in OUT for a, c in zip(OUT[k], ref[k]))
+    else:
+        torch.save(OUT, save)
 print(json.dumps(res), flush=True)
