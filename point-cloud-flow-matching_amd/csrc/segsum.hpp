@@ -37,12 +37,20 @@ namespace pcfm {
 
 inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
-// Step 1 for the scatters: the stable radix sort of sort.hip (rocPRIM).  Same
-// outputs as seg_sort_kernel (start, cnt_out, vinv, rank), workspace from
-// seg_sort_stable_ws.
-size_t seg_sort_stable_ws(int B, int n, int V);
-int seg_sort_stable(const int* key, long long key_bstride, int B, int n, int V, int* start,
-                    int* cnt_out, float* vinv, int* rank, void* ws, hipStream_t st);
+// Key shift of a scatter's sort.  The trilinear stencil (TAPS == 8) reaches
+// from a point's base cell q to q + dx r^2 + dy r + dz (dx, dy, dz in {0, 1}),
+// so a point whose base cell lies below the volume (coordinates outside
+// [0, r - 1]: a negative linear index) can still have corners inside it, and
+// the forward reads them (trilinear_devox.cu:64-105).  Its sort key is q + koff
+// with koff = r^2 + r + 1, over V + koff keys: every point with a corner in
+// [0, V) is kept.  (Keys >= V have every corner >= V: dropped.)
+inline int seg_koff(int V, int taps) {
+  if (taps != 8) return 0;
+  int r = 1;
+  while ((long long)r * r * r < V) ++r;
+  return r * r + r + 1;
+}
+inline int seg_keys(int V, int taps) { return V + seg_koff(V, taps); }
 
 namespace {  // kernels get internal linkage: this header is included by several .hip files
 
@@ -71,6 +79,8 @@ namespace {  // kernels get internal linkage: this header is included by several
 //   vinv[b, v]      (float)(1.0 / (double)cnt) (optional, vox.cu:66)
 //   rank[b, i]      start[key_i] + rank within the key; -1 when the key is
 //                   outside [0, V) (the item contributes nothing)
+// Keys are key[i] + koff (seg_koff; V then counts the shifted key range and
+// cnt_out / vinv are not asked for).
 // --------------------------------------------------------------------------
 constexpr int kSortWaves = 16;
 constexpr int kSortChunk = 2048;   // keys per pass: 16 waves x 2048 ints = 128 KiB of LDS
@@ -92,7 +102,7 @@ inline size_t seg_sort_lds(int V) {
 __global__ void __launch_bounds__(1024)
     seg_sort_kernel(const int* __restrict__ key, long long key_bstride, int n, int V, int span,
                     int* __restrict__ start, int* __restrict__ cnt_out, float* __restrict__ vinv,
-                    int* __restrict__ rank) {
+                    int* __restrict__ rank, int koff = 0) {
   extern __shared__ int hw[];  // [kSortWaves][len]
   __shared__ int wsum[kSortWaves];
   const int p = blockIdx.x, b = blockIdx.y;
@@ -117,7 +127,7 @@ __global__ void __launch_bounds__(1024)
 #pragma unroll
       for (int q = 0; q < kSortBatch; ++q) {
         const int i = i0 + 64 * q + lane;
-        kk[q] = i < i_hi ? kb[i] : -1;
+        kk[q] = i < i_hi ? kb[i] + koff : -1;
       }
 #pragma unroll
       for (int q = 0; q < kSortBatch; ++q) {
@@ -192,7 +202,7 @@ __global__ void __launch_bounds__(1024)
 #pragma unroll
       for (int q = 0; q < kSortBatch; ++q) {
         const int i = j0 + 64 * q + lane;
-        kq[q] = i < i_hi ? kb[i] : -1;
+        kq[q] = i < i_hi ? kb[i] + koff : -1;
       }
 #pragma unroll
       for (int q = 0; q < kSortBatch; ++q) {
@@ -395,19 +405,25 @@ constexpr int kUnitWaves = 4;    // waves (independent units) per block
 template <int TAPS>
 constexpr int seg_ranges() { return TAPS == 8 ? 4 : 1; }
 
+// seg_koff on the device
+template <int TAPS>
+__device__ __forceinline__ int seg_koff_r(int r) { return TAPS == 8 ? r * r + r + 1 : 0; }
+
 // Range g of tile v0: lanes 2g / 2g+1 return the sorted positions [lo, hi).
+// sb: the batch element's start row over the V + koff shifted keys.
 template <int TAPS>
 __device__ __forceinline__ int seg_range_bound(const int* sb, int v0, int V, int r, int lane) {
   int bnd = 0;
   if (lane < 2 * seg_ranges<TAPS>()) {
     const int g = lane >> 1;
+    const int koff = seg_koff_r<TAPS>(r);
     int lo = v0, hi = v0 + kTV;
     if constexpr (TAPS == 8) {
       const int off = (g >> 1) * r * r + (g & 1) * r;
       lo = v0 - off - 1;
       hi = v0 + kTV - off;
     }
-    bnd = sb[min(max((lane & 1) ? hi : lo, 0), V)];
+    bnd = sb[min(max(((lane & 1) ? hi : lo) + koff, 0), V + koff)];
   }
   return bnd;
 }
@@ -423,7 +439,8 @@ __global__ void __launch_bounds__(1024)
   constexpr int NR = seg_ranges<TAPS>();
   const int b = blockIdx.x;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int* sb = start + (size_t)b * (V + 1);
+  const int koff = seg_koff_r<TAPS>(r), VK = V + koff;
+  const int* sb = start + (size_t)b * (VK + 1);
   int carry = 0;
   for (int t0 = 0; t0 < tiles; t0 += 1024) {
     const int tile = t0 + t;
@@ -438,7 +455,7 @@ __global__ void __launch_bounds__(1024)
           lo = v0 - off - 1;
           hi = v0 + kTV - off;
         }
-        T += sb[min(max(hi, 0), V)] - sb[min(max(lo, 0), V)];
+        T += sb[min(max(hi + koff, 0), VK)] - sb[min(max(lo + koff, 0), VK)];
       }
       P = max(1, (T + kItems - 1) / kItems);
     }
@@ -538,7 +555,7 @@ __global__ void __launch_bounds__(kUnitWaves * 64)
   const int v0 = tile * kTV;
   const int c = c0 + lane;
   const bool cok = c < C;
-  const int* __restrict__ sb = start + (size_t)b * (V + 1);
+  const int* __restrict__ sb = start + (size_t)b * (V + seg_koff_r<TAPS>(r) + 1);
   const int* __restrict__ kb = skey + (size_t)b * n;
   const float* __restrict__ xb = xs + (size_t)b * n * C + (cok ? c : 0);
   const float* __restrict__ wb = TAPS == 8 ? ws8 + (size_t)b * n * 8 : nullptr;
@@ -692,7 +709,7 @@ inline int seg_umax(int n, int V, int taps) {
 // gather, partial sums).  The plan depends only on the keys, so scatters over
 // the same points share it (include/pcfm.h, "segment plans").
 struct SegPlan {
-  int* start;      // B*(V+1)
+  int* start;      // B*(VK+1), VK = seg_keys(V, taps)
   float* vinv;     // B*V (per-voxel 1/cnt)
   int* rank;       // B*n
   int* skey;       // B*n
@@ -700,7 +717,6 @@ struct SegPlan {
   int4* units;     // B*umax
   int2* tinfo;     // B*tiles
   int* nunits;     // B
-  void* sort;      // seg_sort_stable workspace
 };
 struct SegApplyWs {
   float* xs;       // B*n*C
@@ -709,14 +725,13 @@ struct SegApplyWs {
 
 inline size_t seg_plan_bytes(int B, int n, int V, int taps) {
   const int umax = seg_umax(n, V, taps), tiles = seg_tiles(V);
-  size_t s = align256((size_t)B * (V + 1) * 4);
+  size_t s = align256((size_t)B * (seg_keys(V, taps) + 1) * 4);
   s += align256((size_t)B * V * 4);
   s += 2 * align256((size_t)B * n * 4);
   if (taps == 8) s += align256((size_t)B * n * 8 * 4);
   s += align256((size_t)B * umax * 16);
   s += align256((size_t)B * tiles * 8);
   s += align256((size_t)B * 4);
-  s += align256(seg_sort_stable_ws(B, n, V));
   return s;
 }
 inline size_t seg_apply_bytes(int B, int C, int n, int V, int taps) {
@@ -740,7 +755,7 @@ inline SegPlan seg_plan_carve(void* mem, int B, int n, int V, int taps) {
   const int umax = seg_umax(n, V, taps), tiles = seg_tiles(V);
   SegCarver c{(char*)mem};
   SegPlan w;
-  w.start = (int*)c.take((size_t)B * (V + 1) * 4);
+  w.start = (int*)c.take((size_t)B * (seg_keys(V, taps) + 1) * 4);
   w.vinv = (float*)c.take((size_t)B * V * 4);
   w.rank = (int*)c.take((size_t)B * n * 4);
   w.skey = (int*)c.take((size_t)B * n * 4);
@@ -748,7 +763,6 @@ inline SegPlan seg_plan_carve(void* mem, int B, int n, int V, int taps) {
   w.units = (int4*)c.take((size_t)B * umax * 16);
   w.tinfo = (int2*)c.take((size_t)B * tiles * 8);
   w.nunits = (int*)c.take((size_t)B * 4);
-  w.sort = c.take(seg_sort_stable_ws(B, n, V));
   return w;
 }
 inline SegApplyWs seg_apply_carve(void* mem, int B, int C, int n, int V, int taps) {
@@ -768,17 +782,16 @@ template <int TAPS>
 inline int seg_plan_build(const int* key, long long key_bstride, bool avg, const float* tapw,
                           int r, int B, int n, int V, int* cnt_out, const SegPlan& w,
                           hipStream_t st) {
-#ifdef PCFM_SORT_ROCPRIM
-  int e = seg_sort_stable(key, key_bstride, B, n, V, w.start, cnt_out, avg ? w.vinv : nullptr,
-                          w.rank, w.sort, st);
-  if (e) return e;
-#else
+  // (A rocPRIM radix sort of the composite keys, kept opt-in through round 5
+  // at ~70 us per sort against this kernel's 23 us, was removed in round 6.)
+  const int koff = seg_koff(V, TAPS), VK = V + koff;
+  PCFM_CHECK_ARG(koff == 0 || (cnt_out == nullptr && !avg),
+                 "segment plan: counts of a shifted-key sort");
   int e = allow_big_lds((const void*)seg_sort_kernel);
   if (e) return e;
-  hipLaunchKernelGGL(seg_sort_kernel, dim3(seg_sort_parts(V), B), dim3(1024), seg_sort_lds(V), st,
-                     key, key_bstride, n, V, seg_sort_span(V), w.start, cnt_out,
-                     avg ? w.vinv : nullptr, w.rank);
-#endif
+  hipLaunchKernelGGL(seg_sort_kernel, dim3(seg_sort_parts(VK), B), dim3(1024), seg_sort_lds(VK),
+                     st, key, key_bstride, n, VK, seg_sort_span(VK), w.start, cnt_out,
+                     avg ? w.vinv : nullptr, w.rank, koff);
   const int tiles = seg_tiles(V), umax = seg_umax(n, V, TAPS);
   hipLaunchKernelGGL(seg_units_kernel<TAPS>, dim3(B), dim3(1024), 0, st, w.start, V, r, tiles,
                      umax, w.units, w.tinfo, w.nunits);
