@@ -260,15 +260,18 @@ def cpu_baseline(args, cfg_kwargs):
     dt = time.perf_counter() - t0
     pts = cfg.batch_size * cfg.num_points
     # the same step at the box's CPU share (16 threads: OMP_NUM_THREADS there), which
-    # ran faster than the full core count in round 4 -- stated beside it, not instead
-    alt = None
+    # ran faster than the full core count in rounds 4-5; the FASTER of the two thread
+    # counts is the headline baseline, the other is stated beside it
+    runs = [{"cores": threads, "value": pts / dt, "seconds_per_step": dt}]
     if threads > 16:
         torch.set_num_threads(16)
         t0 = time.perf_counter()
         tr.step(batch, epoch=201)
         dt16 = time.perf_counter() - t0
         torch.set_num_threads(threads)
-        alt = {"cores": 16, "value": pts / dt16, "seconds_per_step": dt16}
+        runs.append({"cores": 16, "value": pts / dt16, "seconds_per_step": dt16})
+    best = max(runs, key=lambda d: d["value"])
+    other = [d for d in runs if d is not best]
     n = cfg.num_points
     g = torch.Generator().manual_seed(0)
     a, b = torch.rand(1, n, 3, generator=g), torch.rand(1, n, 3, generator=g)
@@ -277,13 +280,15 @@ def cpu_baseline(args, cfg_kwargs):
     _ = d2.min(dim=2).values.mean(dim=1) + d2.min(dim=1).values.mean(dim=1)
     cd = time.perf_counter() - t1
     del d2
-    return {"value": pts / dt, "unit": "points/s", "cores": threads, "kind": "port",
+    return {"value": best["value"], "unit": "points/s", "cores": best["cores"], "kind": "port",
             "host_cpu": host,
             "sample": f"1 timed train step (after a B=1, N=2048 warm-up) at B={cfg.batch_size}, "
                       f"N={n}, {cfg.pf_backbone} backbone, fp32 torch CPU, per-point FiLM, "
-                      f"pcfm.cpu_ops voxel ops, {threads} threads; {dt:.2f} s/step",
-            "seconds_per_step": dt,
-            "at_16_threads": alt,
+                      f"pcfm.cpu_ops voxel ops, the faster of "
+                      f"{' / '.join(str(d['cores']) for d in runs)} threads: {best['cores']} "
+                      f"({best['seconds_per_step']:.2f} s/step)",
+            "seconds_per_step": best["seconds_per_step"],
+            "other_thread_counts": other,
             "chamfer_cdist_fwd_ms": {"shape": f"1x{n}x{n}", "ms": cd * 1e3,
                                      "c2_equivalent_ms": cd * 1e3 * cfg_kwargs["batch_size"]}}
 

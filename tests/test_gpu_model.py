@@ -149,6 +149,17 @@ def test_hybrid_gpu_matches_reference(golden, report, mode, perturbed):
         q = rep["grads_elementwise_quantiles"]
         med, p99, mx = (1e-4, 5e-3, 5e-2) if mode == "exact_fp32" else (1e-3, 5e-2, 2e-1)
         assert q[0.5] < med and q[0.99] < p99 and e_el < mx, (q, e_el, w_el)
+        # per parameter where the ReLU-mask sensitivity does not reach: the head
+        # (measured <= 1.9e-6 in both modes, profiles/r05_hybrid_grads_elementwise.json)
+        # and the ContextNet parameters outside its PVConv stages (<= 1.5e-4 exact,
+        # 2.5e-3 bf16x3) -- a wrong gradient confined to a few of them fails here
+        head = {k: v for k, v in per.items() if k.startswith("head.")}
+        rest = {k: v for k, v in per.items() if k.startswith("ctx_net.")
+                and ".stages." not in k and not k.endswith(_NOISE_BIAS)}
+        assert len(head) > 30 and len(rest) > 8, (len(head), len(rest))
+        assert max(head.values()) < 1e-4, sorted(head.items(), key=lambda kv: -kv[1])[:3]
+        bound = 1e-3 if mode == "exact_fp32" else 1e-2
+        assert max(rest.values()) < bound, sorted(rest.items(), key=lambda kv: -kv[1])[:3]
     if mode == "exact_fp32":
         assert e_v < 1e-5 and e_loss < 1e-5 and e_g < 1e-3 and e_se < 2e-3, (e_v, e_loss, e_g,
                                                                              e_se, worst)
