@@ -56,7 +56,7 @@ VOXEL_OPS = ("avg_voxelize_fwd", "avg_voxelize_bwd", "trilinear_devoxelize_fwd",
 BF16X3_PEAK_TF = BF16_DENSE_TF / 3  # fp32-equivalent peak of the 3-product split
 H100_DERIVED_PTS = 1.88e6       # 25 s/epoch at <= 293 steps/epoch (derived)
 # HBM bytes per launch of the voxel ops from rocprofv3 PMC passes (tools/op_traffic.py)
-TRAFFIC_FILE = os.path.join(REPO, "profiles", "r05_traffic.json")
+TRAFFIC_FILE = os.path.join(REPO, "profiles", "r06_traffic.json")
 
 
 def measured_traffic(op, batch, points):
@@ -77,7 +77,7 @@ def measured_traffic(op, batch, points):
 
 # MFMA-pipe busy fractions of the conv kernels (rocprofv3 SQ_VALU_MFMA_BUSY_CYCLES
 # over GRBM_GUI_ACTIVE, tools/kernel_pmc.py at the C2 stage shapes)
-KERNEL_PMC_FILE = os.path.join(REPO, "profiles", "r05_kernel_pmc.json")
+KERNEL_PMC_FILE = os.path.join(REPO, "profiles", "r06_kernel_pmc.json")
 # dense fwd / bwd-data: the slab form at r = 32 / 16, the LDS-DMA form at r = 8
 CONV_KERNEL = {"conv3d_fwd": ("conv3_igemm_slab_kernel", "conv3_igemm_glds_kernel"),
                "conv3d_bwd_data": ("conv3_igemm_slab_kernel", "conv3_igemm_glds_kernel"),
@@ -484,7 +484,7 @@ def main():
                 traffic = measured_traffic(op, cfg.batch_size, cfg.num_points)
                 return {"kernel": op, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
                         "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                        "traffic_unit": "bytes per launch (PMC, profiles/r05_traffic.json)"
+                        "traffic_unit": "bytes per launch (PMC, profiles/r06_traffic.json)"
                         if traffic else None,
                         "algorithmic_bytes_per_launch": d["amount"] / d["launches"],
                         "avg_launch_ms": d["ms"] / d["launches"]}
@@ -499,13 +499,13 @@ def main():
             return {"kernel": op, "bound": "mfma", "achieved": achieved, "peak": BF16X3_PEAK_TF,
                     "unit": "TFLOP/s", "frac": achieved / BF16X3_PEAK_TF, "traffic": traffic,
                     "traffic_unit": "HBM bytes per launch (PMC FETCH_SIZE + WRITE_SIZE, "
-                                    "profiles/r05_traffic.json)" if traffic else None,
+                                    "profiles/r06_traffic.json)" if traffic else None,
                     "note": "achieved = algorithmic fp32 conv FLOPs / time; each is 3 bf16 "
                             "MFMA products, so peak = dense bf16 2500 TF / 3; raw bf16 MFMA "
                             f"utilisation = {3 * achieved / BF16_DENSE_TF:.3f}",
                     "mfma_busy_frac": committed_mfma_busy(op),
                     "mfma_busy_source": "SQ_VALU_MFMA_BUSY_CYCLES / (1024 * GRBM_GUI_ACTIVE / 8), "
-                                        "profiles/r05_kernel_pmc.json (time-weighted "
+                                        "profiles/r06_kernel_pmc.json (time-weighted "
                                         "over the slab and LDS-DMA forms)",
                     "algorithmic_flops_per_launch": d["amount"] / d["launches"],
                     "avg_launch_ms": d["ms"] / d["launches"]}
