@@ -61,12 +61,15 @@ __global__ void __launch_bounds__(256)
 //     tile holds an occupied voxel;
 //   cmask [b][V / 64]: bit p < 9 = some voxel of the 64-voxel chunk shifted by
 //     (dx, dy, dz), p = 3 (dx + 1) + dy + 1, dz = -1..1, is occupied, i.e. the
-//     weight gradient's (pair, chunk) step has a nonzero X operand.
+//     weight gradient's (pair, chunk) step has a nonzero X operand;
+//   kmask [b][V / 16]: bit t < 27 = some voxel of the 16-voxel group shifted by
+//     tap t is occupied, i.e. the weight gradient's 16-voxel K-slice of tap t
+//     has a nonzero X operand (the rest of its products are exact zeros).
 // grid = (V / 256, b), 256 threads (a thread = a voxel, a wave = a chunk).
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(256)
     conv3_occupancy_kernel(const int* __restrict__ cnt, int R, uint32_t* __restrict__ tmask,
-                           uint32_t* __restrict__ cmask) {
+                           uint32_t* __restrict__ cmask, uint32_t* __restrict__ kmask) {
   __shared__ uint32_t sm;
   const int V = R * R * R, R2 = R * R;
   const int b = blockIdx.y, t = threadIdx.x;
@@ -84,6 +87,10 @@ __global__ void __launch_bounds__(256)
       pairs |= 1u << (tap / 3);
     }
   }
+  uint32_t k16 = taps;  // 16-voxel group OR of the tap bits
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1) k16 |= __shfl_xor(k16, o);
+  if ((t & 15) == 0) kmask[(size_t)b * (V / 16) + v / 16] = k16;
   if (c[v] > 0) taps |= 1u << 31;
   if (t == 0) sm = 0;
   __syncthreads();
@@ -1586,11 +1593,17 @@ __global__ void __launch_bounds__(64)
 // the step, kW3Q / 4 per 16-voxel K-slice behind sched_barriers, instead of in
 // one burst at the step's start: 2.09 vs 2.04 ms/step, same box -- the issue
 // burst is not what holds the MFMA pipe at 0.56 busy.)
+// kmask (with lists; conv3_occupancy_kernel): a wave skips the 16-voxel
+// K-slices whose X rows for its tap are all empty -- products that are exact
+// zeros, so the partials keep their bits.  The block's mask words are staged
+// in LDS behind the two buffers before the first DMA (a global load inside the
+// loop would be waited for with vmcnt(0), draining the DMA pieces in flight).
 __global__ void __launch_bounds__(kW3Threads)
     conv3_wgrad3_kernel(const uint16_t* __restrict__ xh, const uint16_t* __restrict__ xl,
                         const uint16_t* __restrict__ gh, const uint16_t* __restrict__ gl,
                         int B, int cin, int cout, int R, int S, float* __restrict__ part,
-                        const int* __restrict__ lists, const int* __restrict__ counts, int cap) {
+                        const int* __restrict__ lists, const int* __restrict__ counts, int cap,
+                        const uint32_t* __restrict__ kmask) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   // 12 waves = 3 per SIMD at 168 VGPRs each: the CU's whole register file, so
   // no other kernel's wave shares a CU with this block
@@ -1678,6 +1691,17 @@ __global__ void __launch_bounds__(kW3Threads)
 
   auto chunk_of = [&](int st) { return lst != nullptr ? lst[st] : sp + st * S; };
   const int lgR = 31 - __builtin_clz(R);  // R is a power of two here
+  // the 4 K-slice mask words of every listed chunk (kmask: with lists only)
+  uint32_t* kms = reinterpret_cast<uint32_t*>(lds + 2 * kW3Buf);
+  const bool skip = kmask != nullptr && lst != nullptr;
+  if (skip) {
+    for (int i = t; i < 4 * nst; i += kW3Threads) {
+      const int c = lst[i >> 2];
+      kms[i] = kmask[(size_t)(c / cpb) * (V / 16) + (size_t)(c % cpb) * (kWV / 16) + (i & 3)];
+    }
+    __syncthreads();
+  }
+  const int mytap = pair * 3 + (dz + 1);
   int cnext = nst > 0 ? chunk_of(0) : 0;
   if (nst > 0) issue(cnext / cpb, (cnext % cpb) * kWV, lds);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1696,8 +1720,16 @@ __global__ void __launch_bounds__(kW3Threads)
     const uint8_t* iAl = cur + kW3AImg;
     const uint8_t* iBh = cur + 2 * kW3AImg;
     const uint8_t* iBl = iBh + kW3BImg;
+    uint32_t kw = 0xFu;  // K-slices of this step with a nonzero X operand (bit kk)
+    if (skip) {
+      const uint4 q = *reinterpret_cast<const uint4*>(kms + 4 * st);
+      kw = ((q.x >> mytap) & 1u) | (((q.y >> mytap) & 1u) << 1) | (((q.z >> mytap) & 1u) << 2) |
+           (((q.w >> mytap) & 1u) << 3);
+      kw = __builtin_amdgcn_readfirstlane(kw);
+    }
 #pragma unroll
     for (int kk = 0; kk < kWV / 16; ++kk) {
+      if (!((kw >> kk) & 1u)) continue;  // wave-uniform: exact-zero products skipped
       // validity of this lane's 8 voxels for tap (dx, dy, dz)
       const int vk = v0 + kk * 16 + 8 * h;
       const int xq = vk >> (2 * lgR), yq = (vk >> lgR) & (R - 1), z0 = vk & (R - 1);
@@ -2148,7 +2180,7 @@ extern "C" int pcfm_conv3d_igemm_cl_occ(const void* xs, const void* wsplit, cons
 extern "C" size_t pcfm_conv3d_occupancy_bytes(int b, int r) {
   const long long v = (long long)r * r * r;
   if (b <= 0 || r <= 0 || v % 256 != 0) return 0;
-  return (size_t)b * (v / 256 + v / 64) * sizeof(uint32_t);
+  return (size_t)b * (v / 256 + v / 64 + v / 16) * sizeof(uint32_t);
 }
 
 extern "C" int pcfm_conv3d_occupancy(const int* cnt, int b, int r, unsigned* masks,
@@ -2157,7 +2189,8 @@ extern "C" int pcfm_conv3d_occupancy(const int* cnt, int b, int r, unsigned* mas
                  "conv3d_occupancy: bad shape b=%d r=%d (r^3 %% 256 == 0)", b, r);
   const int V = r * r * r;
   hipLaunchKernelGGL(conv3_occupancy_kernel, dim3(V / 256, b), dim3(256), 0, (hipStream_t)stream,
-                     cnt, r, (uint32_t*)masks, (uint32_t*)masks + (size_t)b * (V / 256));
+                     cnt, r, (uint32_t*)masks, (uint32_t*)masks + (size_t)b * (V / 256),
+                     (uint32_t*)masks + (size_t)b * (V / 256 + V / 64));
   return check_launch("conv3d_occupancy");
 }
 
@@ -2218,7 +2251,7 @@ static int wgrad_cap(int b, int r, int S) {
 
 static int wgrad_cl(const void* xs, const void* gys, int b, int cin, int cout, int r,
                     const uint32_t* cmask, float* grad_w, void* ws, size_t ws_bytes,
-                    void* stream) {
+                    void* stream, const uint32_t* kmask = nullptr) {
   PCFM_CHECK_ARG(b > 0 && conv3_shape_ok(b, cin, cout, r) && cin % kMT == 0,
                  "conv3d_wgrad_cl: unsupported shape b=%d cin=%d cout=%d r=%d", b, cin, cout, r);
   const size_t need = wgrad_partial_bytes(b, cin, cout, r);
@@ -2244,9 +2277,12 @@ static int wgrad_cl(const void* xs, const void* gys, int b, int cin, int cout, i
       hipLaunchKernelGGL(conv3_wgrad_lists_kernel, dim3(9, S), dim3(64), 0, st, cmask,
                          b * (V / kWV), S, cap, lists, counts);
     }
-    hipLaunchKernelGGL(conv3_wgrad3_kernel, dim3(tiles / 3 * S), dim3(kW3Threads), 2 * kW3Buf, st,
+    const size_t lds = 2 * (size_t)kW3Buf + (kmask != nullptr ? (size_t)cap * 16 : 0);
+    PCFM_CHECK_ARG(lds <= (size_t)kLdsBytesMax, "conv3d_wgrad_cl_occ: %d listed chunks per split "
+                   "exceed the LDS", cap);
+    hipLaunchKernelGGL(conv3_wgrad3_kernel, dim3(tiles / 3 * S), dim3(kW3Threads), lds, st,
                        xh, xh + kSplitLo, gh, gh + kSplitLo, b, cin, cout, r,
-                       S, (float*)ws, lists, counts, cap);
+                       S, (float*)ws, lists, counts, cap, kmask);
   } else {
     hipLaunchKernelGGL(conv3_wgrad_cl_kernel, dim3(tiles * S), dim3(256), 0, st, xh,
                        xh + kSplitLo, gh, gh + kSplitLo, b, cin, cout, r, S,
@@ -2278,5 +2314,8 @@ extern "C" int pcfm_conv3d_wgrad_cl_occ(const void* xs, const void* gys, int b, 
   const int V = r * r * r;
   // the chunk masks follow the tile masks in pcfm_conv3d_occupancy's buffer
   const uint32_t* cmask = (const uint32_t*)masks + (size_t)b * (V / 256);
-  return wgrad_cl(xs, gys, b, cin, cout, r, cmask, grad_w, ws, ws_bytes, stream);
+  // the K-slice masks follow the chunk masks (PCFM_WGRAD_KSKIP=0: none, A/B knob)
+  const char* ks = std::getenv("PCFM_WGRAD_KSKIP");
+  const uint32_t* kmask = (ks != nullptr && ks[0] == '0') ? nullptr : cmask + (size_t)b * (V / 64);
+  return wgrad_cl(xs, gys, b, cin, cout, r, cmask, grad_w, ws, ws_bytes, stream, kmask);
 }
