@@ -323,7 +323,9 @@ int pcfm_conv3d_wgrad_cl(const void* xs, const void* gys, int b, int cin, int co
  * (> 0 = occupied) writes masks (pcfm_conv3d_occupancy_bytes(b, r); 0 =
  * unsupported: r^3 % 256 != 0): per 256-voxel tile the taps whose shifted tile
  * holds an occupied voxel (bits 0-26) and whether the tile holds one (bit 31);
- * then per 64-voxel chunk the (dx, dy) pairs whose shifted rows hold one. */
+ * then per 64-voxel chunk the (dx, dy) pairs whose shifted rows hold one;
+ * then per 16-voxel group the taps at which some voxel of the group has an
+ * occupied neighbour (bits 0-26). */
 size_t pcfm_conv3d_occupancy_bytes(int b, int r);
 int pcfm_conv3d_occupancy(const int* cnt, int b, int r, unsigned* masks, void* stream);
 /* pcfm_conv3d_igemm_cl skipping exact-zero work: mode 1 (forward over a
