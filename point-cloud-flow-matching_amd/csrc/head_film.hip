@@ -136,7 +136,7 @@ __device__ __forceinline__ float dsilu(float x) {
   return s * (1.0f + x * (1.0f - s));
 }
 
-// grid = (ceil(n / 256), B), 256 threads.
+// grid = (ceil(n / rpb), B), 256 threads; a block owns rpb rows.
 template <int NV, bool FILM>
 __global__ void __launch_bounds__(256)
     film_fwd_kernel(const uint16_t* __restrict__ h16, const float* __restrict__ uprev,
@@ -144,11 +144,11 @@ __global__ void __launch_bounds__(256)
                     const float* __restrict__ beta, const uint16_t* __restrict__ sp1,
                     const uint16_t* __restrict__ shift, const float* __restrict__ hbias, int n,
                     float eps, float* __restrict__ u, uint16_t* __restrict__ a,
-                    float* __restrict__ mean_o, float* __restrict__ rstd_o) {
+                    float* __restrict__ mean_o, float* __restrict__ rstd_o, int rpb) {
   constexpr int W = 256 * NV;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int b = blockIdx.y;
-  const int i0 = blockIdx.x * kRowsPerBlock, i1 = min(n, i0 + kRowsPerBlock);
+  const int i0 = blockIdx.x * rpb, i1 = min(n, i0 + rpb);
   float gm[NV][4], bt[NV][4], sp[NV][4], sh[NV][4], hb[NV][4];
   const bool has_hb = hbias != nullptr;
   if (has_hb) ld_f32<NV>(hbias + (size_t)b * W, lane, hb);
@@ -374,6 +374,14 @@ __global__ void __launch_bounds__(64)
   out[c] = s;
 }
 
+// rows per forward block (env PCFM_FILM_FWD_ROWS, a multiple of 4, default
+// 32; read per call: A/B runs)
+int film_fwd_rows() {
+  const char* e = getenv("PCFM_FILM_FWD_ROWS");
+  const int v = e != nullptr ? atoi(e) : 32;
+  return v >= 4 && v % 4 == 0 ? v : 32;
+}
+
 bool film_ok(int b, int n, int w) {
   return b > 0 && n > 0 && (w == 256 || w == 512) &&
          (long long)b * n * w < (1LL << 40);
@@ -384,7 +392,13 @@ int launch_fwd(const void* h16, const float* uprev, const void* gprev, const flo
                const float* beta, const void* sp1, const void* shift, const float* hbias, int b,
                int n, int w, float eps, float* u, void* a, float* mean, float* rstd,
                hipStream_t st) {
-  const dim3 grid(ceil_div(n, kRowsPerBlock), b), blk(256);
+  // 32 rows per block (8 per wave): at 256 the B = 8, N = 20000 pass had 632
+  // blocks, 2.5 waves per SIMD with one row each in flight -- 0.175 -> 0.154 ms
+  // per 512-wide launch, 5.6 -> 6.4 TB/s (profiles/r06_ab_film_rows.jsonl).
+  // The backward stays at 256 (its partials are per block; 64 / 128 rows and
+  // two rows in flight per wave measured slower there).
+  const int rpb = film_fwd_rows();
+  const dim3 grid(ceil_div(n, rpb), b), blk(256);
   const uint16_t* H = (const uint16_t*)h16;
   const uint16_t* G = (const uint16_t*)gprev;
   const uint16_t* S1 = (const uint16_t*)sp1;
@@ -393,11 +407,11 @@ int launch_fwd(const void* h16, const float* uprev, const void* gprev, const flo
   switch (w) {
     case 256:
       hipLaunchKernelGGL((film_fwd_kernel<1, FILM>), grid, blk, 0, st, H, uprev, G, gamma, beta,
-                         S1, SH, hbias, n, eps, u, A, mean, rstd);
+                         S1, SH, hbias, n, eps, u, A, mean, rstd, rpb);
       break;
     default:
       hipLaunchKernelGGL((film_fwd_kernel<2, FILM>), grid, blk, 0, st, H, uprev, G, gamma, beta,
-                         S1, SH, hbias, n, eps, u, A, mean, rstd);
+                         S1, SH, hbias, n, eps, u, A, mean, rstd, rpb);
   }
   return check_launch(FILM ? "head_film_fwd" : "head_silu_fwd");
 }
