@@ -205,11 +205,13 @@ __device__ __forceinline__ void xpose_reduce_stage(float* v, bool upper) {
 }
 
 // Epilogue of a 256 (m) x 128 (point) tile held as 8 waves of 64 x 64
-// (pw_gemm256_kernel, pw_glds256_kernel): y = acc + bias, streamed stores, and
-// with stats the per-(channel, 64-point group) BatchNorm statistics (see
-// pw_gemm256_kernel).  nb = batch elements (the stats row length is nb * groups).
+// (pw_gemm256_kernel): y = acc + bias, streamed stores, and with stats the
+// per-(channel, 64-point group) BatchNorm statistics (see pw_gemm256_kernel).
+// nb = batch elements (the stats row length is nb * groups).  sbias: the tile's
+// 256 bias values (rows m0 + i, clamped to M - 1), staged in LDS by the kernel
+// at its start -- read here without a global load's latency at the end.
 __device__ __forceinline__ void pw256_epilogue(const f32x16 (&acc)[2][2], const Parts& y,
-                                               const float* __restrict__ bias, int b, int nb,
+                                               const float* __restrict__ sbias, int b, int nb,
                                                int M, int N, int m0, int p0, int wr, int wc,
                                                int r, int h, float2* __restrict__ stats) {
   const int pw0 = p0 + wc * 64;  // this wave's 64 points
@@ -217,16 +219,9 @@ __device__ __forceinline__ void pw256_epilogue(const f32x16 (&acc)[2][2], const 
   for (int i = 0; i < 2; ++i) {
     const int mg = m0 + wr * 64 + i * 32;
     float* __restrict__ yr = y.row(b, min(mg, M - 1), N);
-    // bias rows at wave-uniform addresses (scalar loads: the persistent kernel
-    // keeps LDS-DMA pieces in flight here, which a vector load's wait would drain)
     float bv[16];
 #pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const int m0e = mg + (e & 3) + 8 * (e >> 2);
-      const float b0 = bias != nullptr ? bias[min(m0e, M - 1)] : 0.0f;
-      const float b1 = bias != nullptr ? bias[min(m0e + 4, M - 1)] : 0.0f;
-      bv[e] = h ? b1 : b0;
-    }
+    for (int e = 0; e < 16; ++e) bv[e] = sbias[mg - m0 + (e & 3) + 8 * (e >> 2) + 4 * h];
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -285,8 +280,11 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))
   constexpr int TM = 256, TN = 128;
   constexpr int A_ELEMS = TM * kLDR, B_ELEMS = TN * kLDR;
   __shared__ __attribute__((aligned(16))) uint16_t lds[2 * A_ELEMS + 2 * B_ELEMS];
+  __shared__ float sbias[TM];
   const int b = blockIdx.z, m0 = blockIdx.y * TM, p0 = blockIdx.x * TN;
   const int t = threadIdx.x, lane = t & 63;
+  // the tile's bias rows, visible after the first barrier below
+  if (t < TM) sbias[t] = bias != nullptr ? bias[b * bias_bstride + min(m0 + t, M - 1)] : 0.0f;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);
   const int wr = w >> 1, wc = w & 1, r = lane & 31, h = lane >> 5;
   constexpr int CPT = kKT * TN / 512;  // 8 channels per thread per K-step
@@ -411,7 +409,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4, 4))
     if (s + 1 < nsteps) store(s + 1, rb);
     __syncthreads();
   }
-  pw256_epilogue(acc, y, bias != nullptr ? bias + b * bias_bstride : nullptr, b, (int)gridDim.z,
+  pw256_epilogue(acc, y, sbias, b, (int)gridDim.z,
                  M, N, m0, p0, wr, wc, r, h, stats);
 }
 
