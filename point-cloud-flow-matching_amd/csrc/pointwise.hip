@@ -484,6 +484,11 @@ __global__ void __launch_bounds__(kSW * 64)
   // every slice streams all point tiles; slices of a tile share its x reads
   // in L2 -- blocks (x, y) and (x, y') sit on one XCD when gridDim.x % 8 == 0)
   const int m0 = (int)blockIdx.y * 128;
+  // one bias shared by the batch: the slice's 128 rows staged in LDS with the
+  // weights, so a tile's epilogue does not wait on global loads
+  __shared__ float sbias[128];
+  const bool lbias = bias != nullptr && bias_bstride == 0;
+  if (lbias && t < 128) sbias[t] = bias[min(m0 + t, M - 1)];
   for (int e = t; e < 2 * 128 * cpr; e += kSW * 64) {  // weight image -> LDS, 16-B pieces
     const int img = e / (128 * cpr), rem = e - img * 128 * cpr;
     const int row = rem / cpr, pc = rem - row * cpr;
@@ -645,8 +650,13 @@ __global__ void __launch_bounds__(kSW * 64)
         // addresses out of the tile loop)
         float bv[16];
         const float* bl = bias != nullptr ? uniform_ptr(bias + bo + mg) + 4 * h : nullptr;
+        if (lbias) {  // block-uniform
 #pragma unroll
-        for (int e = 0; e < 16; ++e) bv[e] = bl != nullptr ? bl[(e & 3) + 8 * (e >> 2)] : 0.0f;
+          for (int e = 0; e < 16; ++e) bv[e] = sbias[32 * i + (e & 3) + 8 * (e >> 2) + 4 * h];
+        } else {
+#pragma unroll
+          for (int e = 0; e < 16; ++e) bv[e] = bl != nullptr ? bl[(e & 3) + 8 * (e >> 2)] : 0.0f;
+        }
         if (p < N) {
 #pragma unroll
           for (int e = 0; e < 16; ++e) out_store(yl + ((e & 3) + 8 * (e >> 2)) * N, acc[i][e] + bv[e]);

@@ -25,4 +25,12 @@ for n in (8192, 12288, 16384, 18432, 20000, 20480, 24576):
     d = timeit(lambda: ops.pointwise_backward_data(x, w))
     res[str(n)] = {"blocks": blocks, "rounds": blocks / 512.0, "fwd_ms": f, "bwd_data_ms": d,
                    "fwd_TBps": 2 * x.numel() * 4 / f / 1e9}
+# the M <= 128 streaming form (pw_stream128) at N = 20000, with a shared bias
+for ci, co in ((128, 128), (256, 128), (64, 128)):
+    w2 = torch.randn(co, ci, 1, device="cuda", generator=g) * ci ** -0.5
+    b2 = torch.randn(co, device="cuda", generator=g)
+    x = torch.randn(b, ci, 20000, device="cuda", generator=g)
+    dy = torch.randn(b, co, 20000, device="cuda", generator=g)
+    res[f"s{ci}to{co}"] = {"fwd_ms": timeit(lambda: ops.pointwise_forward(x, w2, b2)),
+                           "bwd_data_ms": timeit(lambda: ops.pointwise_backward_data(dy, w2))}
 print(json.dumps(res), flush=True)
