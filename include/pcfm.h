@@ -339,9 +339,10 @@ int pcfm_conv3d_igemm_cl_occ(const void* xs, const void* wsplit, const float* bi
 /* Chunk lists of a voxelized grid (the same counts cnt i32 [b][r^3]; a chunk =
  * 32 consecutive voxels): list 0 = the chunks holding an occupied voxel, list 1
  * = the chunks holding a voxel with an occupied voxel in its 3x3x3
- * neighbourhood; entries are chunk indices (b r^3 + v) / 32, ascending, and
- * the device-side counts lead the buffer (pcfm_conv3d_vlist_bytes; 0 =
- * unsupported: r^3 % 256 != 0 or b r^3 >= 2^31). */
+ * neighbourhood; entries are chunk indices (b r^3 + v) / 32, ascending; list 2
+ * = the occupied voxels themselves, b r^3 + v, ascending.  The device-side
+ * counts lead the buffer (pcfm_conv3d_vlist_bytes; 0 = unsupported:
+ * r^3 % 256 != 0 or b r^3 >= 2^31). */
 size_t pcfm_conv3d_vlist_bytes(int b, int r);
 int pcfm_conv3d_vlist(const int* cnt, int b, int r, int* lists, void* stream);
 /* pcfm_conv3d_igemm_cl computed in the chunks of list `which` only (its GEMM
@@ -349,7 +350,9 @@ int pcfm_conv3d_vlist(const int* cnt, int b, int r, int* lists, void* stream);
  * (forward over a voxelized input x: elsewhere the output is exactly the bias,
  * written as such -- bit-identical to pcfm_conv3d_igemm_cl everywhere), which 0
  * (backward-data into a voxelized grid, bias NULL: equal to
- * pcfm_conv3d_igemm_cl at every occupied voxel, 0 in the unlisted chunks).  Shapes without
+ * pcfm_conv3d_igemm_cl at every occupied voxel, 0 at every other voxel --
+ * computed over list 2, voxel by voxel; PCFM_LIST_VOX=0: over the chunks of
+ * list 0, 0 in the unlisted chunks).  Shapes without
  * the list form (split-K grids, r = 8 at the C2 sizes) run the dense GEMM.
  * Fully writes y; same workspace as pcfm_conv3d_igemm_cl. */
 int pcfm_conv3d_igemm_cl_list(const void* xs, const void* wsplit, const float* bias, int b,

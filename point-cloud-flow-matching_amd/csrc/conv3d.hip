@@ -114,8 +114,9 @@ __global__ void __launch_bounds__(256)
 // its bias: its input is 0 there).  Whole chunks keep the GEMM's B-row fetches
 // and output stores 128-B runs (voxel-granular lists measured slower: short
 // scattered runs).  Entries are global chunk indices (b V + v) / 32, ascending
-// (deterministic).  Buffer: int32 counts[2] | pad to 64 | per-tile counts /
-// offsets [2][tiles] | list 0 [B V / 32] | list 1 [B V / 32].
+// (deterministic).  List 2: the occupied voxels themselves, global voxel
+// indices b V + v, ascending (the backward-data's voxel-granular form).
+// Buffer layout: pcfm_conv3d_vlist_bytes.
 // ---------------------------------------------------------------------------
 constexpr int kChunk = 32;
 
@@ -147,15 +148,20 @@ __device__ __forceinline__ void chunk_flags(const int* __restrict__ cnt, long lo
 // grid = B V / 256 tiles (8 chunks each), 256 threads: per-tile chunk counts
 __global__ void __launch_bounds__(256)
     conv3_vlist_count_kernel(const int* __restrict__ cnt, int R, int tiles,
-                             int* __restrict__ tcount) {
+                             int* __restrict__ tcount, int* __restrict__ tcount2) {
   __shared__ int ws[2][8];
+  __shared__ int wv[4];
   const int t = threadIdx.x;
+  const long long g = (long long)blockIdx.x * 256 + t;
   bool occ, act;
-  chunk_flags(cnt, (long long)blockIdx.x * 256 + t, R, occ, act);
+  chunk_flags(cnt, g, R, occ, act);
   if ((t & 31) == 0) {
     ws[0][t >> 5] = occ ? 1 : 0;
     ws[1][t >> 5] = act ? 1 : 0;
   }
+  // occupied voxels (list 2): per-wave ballot counts
+  const int n2 = __popcll(__ballot(cnt[g] > 0));
+  if ((t & 63) == 0) wv[t >> 6] = n2;
   __syncthreads();
   if (t < 2) {
     int n = 0;
@@ -163,15 +169,17 @@ __global__ void __launch_bounds__(256)
     for (int q = 0; q < 8; ++q) n += ws[t][q];
     tcount[t * tiles + blockIdx.x] = n;
   }
+  if (t == 2) tcount2[blockIdx.x] = ((wv[0] + wv[1]) + wv[2]) + wv[3];
 }
 
 // one block: exclusive scans of the two per-tile count rows (in place) and
 // the totals
 __global__ void __launch_bounds__(1024)
-    conv3_vlist_scan_kernel(int* __restrict__ tcount, int tiles, int* __restrict__ counts) {
+    conv3_vlist_scan_kernel(int* __restrict__ tcount, int tiles, int* __restrict__ counts,
+                            int rows) {
   __shared__ int wsum[16];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  for (int k = 0; k < 2; ++k) {
+  for (int k = 0; k < rows; ++k) {
     int* row = tcount + (size_t)k * tiles;
     int carry = 0;
     for (int t0 = 0; t0 < tiles; t0 += 1024) {
@@ -203,16 +211,28 @@ __global__ void __launch_bounds__(1024)
 __global__ void __launch_bounds__(256)
     conv3_vlist_write_kernel(const int* __restrict__ cnt, int R, int tiles,
                              const int* __restrict__ toff, int* __restrict__ list0,
-                             int* __restrict__ list1) {
+                             int* __restrict__ list1, const int* __restrict__ toff2,
+                             int* __restrict__ list2) {
   __shared__ int ws[2][8];
+  __shared__ int wv[4];
   const int t = threadIdx.x;
+  const long long g = (long long)blockIdx.x * 256 + t;
   bool occ, act;
-  chunk_flags(cnt, (long long)blockIdx.x * 256 + t, R, occ, act);
+  chunk_flags(cnt, g, R, occ, act);
   if ((t & 31) == 0) {
     ws[0][t >> 5] = occ ? 1 : 0;
     ws[1][t >> 5] = act ? 1 : 0;
   }
+  const bool o2 = cnt[g] > 0;
+  const unsigned long long m2 = __ballot(o2);
+  if ((t & 63) == 0) wv[t >> 6] = __popcll(m2);
   __syncthreads();
+  if (o2) {  // list 2: the occupied voxels in voxel order
+    int p2 = toff2[blockIdx.x];
+    for (int u = 0; u < (t >> 6); ++u) p2 += wv[u];
+    p2 += __builtin_amdgcn_mbcnt_hi((unsigned)(m2 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m2, 0u));
+    list2[p2] = (int)g;
+  }
   if ((t & 31) == 0) {
     const int q = t >> 5, chunk = blockIdx.x * 8 + q;
     int p0 = toff[blockIdx.x], p1 = toff[tiles + blockIdx.x];
@@ -230,12 +250,13 @@ __global__ void __launch_bounds__(256)
 // grid = B V / 256, 256 threads.
 __global__ void __launch_bounds__(256)
     conv3_fill_unlisted_kernel(const int* __restrict__ cnt, int R, int M, int which,
-                               const float* __restrict__ bias, float* __restrict__ y) {
+                               const float* __restrict__ bias, float* __restrict__ y, int vox) {
   const int V = R * R * R;
   const long long g = (long long)blockIdx.x * 256 + threadIdx.x;
   bool occ, act;
   chunk_flags(cnt, g, R, occ, act);
-  if (which == 0 ? occ : act) return;
+  // vox (which 0 over the voxel list): every voxel without a point
+  if (vox ? cnt[g] > 0 : (which == 0 ? occ : act)) return;
   const int b = (int)(g / V), v = (int)(g % V);
   float* __restrict__ yb = y + (size_t)b * M * V + v;
   for (int m = 0; m < M; ++m)
@@ -572,20 +593,21 @@ __global__ void __launch_bounds__(GN * 2)  // GK<KT, GN>::NW = GN / 32 waves
                             float* __restrict__ y, int K, int M, int R, int S,
                             float* __restrict__ part, const uint32_t* __restrict__ tmask,
                             int mmode, const int* __restrict__ vlist = nullptr,
-                            const int* __restrict__ vcount = nullptr) {
+                            const int* __restrict__ vcount = nullptr, int lg = 5) {
   using G = GK<KT, GN>;
   __shared__ __attribute__((aligned(16))) uint8_t lds[NST * G::STAGE];
   const int V = R * R * R, R2 = R * R;
   const int nmt = M / kGM, nvt = V / GN;
-  // Chunk-list form (S == 1, conv3_vlist_*): the block's GN output voxels are
-  // the CPT listed 32-voxel chunks [lt CPT, lt CPT + CPT) -- global chunk
-  // indices (b V + v) / 32 whose result is wanted, ascending -- instead of a
-  // contiguous range; the B rows of every tap are their neighbours (a padding
-  // entry reads zero rows and stores nothing).  Only the first nmt x
-  // ceil(count / CPT) blocks (device-side count) work, dealt to the XCDs as
-  // the dense grid is; the rest leave at once, before any barrier.
+  // List form (S == 1, conv3_vlist_*): the block's GN output voxels are the
+  // CPT listed runs of 2^lg voxels [lt CPT, lt CPT + CPT) -- global run
+  // indices (b V + v) >> lg whose result is wanted, ascending: 32-voxel chunks
+  // (lg 5) or single voxels (lg 0) -- instead of a contiguous range; the B rows
+  // of every tap are their neighbours (a padding entry reads zero rows and
+  // stores nothing).  Only the first nmt x ceil(count / CPT) blocks
+  // (device-side count) work, dealt to the XCDs as the dense grid is; the rest
+  // leave at once, before any barrier.
   const bool lmode = vlist != nullptr;
-  constexpr int CPT = GN / kChunk;
+  const int CPT = GN >> lg, lmask = (1 << lg) - 1;
   int lcount = 0;
   int nwg = (int)gridDim.x, id = (int)blockIdx.x;
   if (lmode) {
@@ -657,8 +679,8 @@ __global__ void __launch_bounds__(GN * 2)  // GK<KT, GN>::NW = GN / 32 waves
     const int row = (I % G::BPI) * G::RPP + prow;
     long long gv = (long long)bV + v0 + row;  // global row b V + v, -1: padding
     if (lmode) {
-      const int e = lt * CPT + row / kChunk;
-      gv = e < lcount ? (long long)vlist[e] * kChunk + row % kChunk : -1;
+      const int e = lt * CPT + (row >> lg);
+      gv = e < lcount ? ((long long)vlist[e] << lg) + (row & lmask) : -1;
     }
     const int v = gv >= 0 ? (int)(gv % V) : 0;
     const int cofs = (pch ^ G::swz(row)) << 3;
@@ -882,8 +904,8 @@ __global__ void __launch_bounds__(GN * 2)  // GK<KT, GN>::NW = GN / 32 waves
   for (int j = 0; j < 2; ++j) {
     const int col = wc * 64 + j * 32 + r;
     if (lmode) {
-      const int e = lt * CPT + col / kChunk;
-      const long long g = e < lcount ? (long long)vlist[e] * kChunk + col % kChunk : -1;
+      const int e = lt * CPT + (col >> lg);
+      const long long g = e < lcount ? ((long long)vlist[e] << lg) + (col & lmask) : -1;
       ycol[j] = g >= 0 ? y + (size_t)(g / V) * M * V + (size_t)(g % V) : nullptr;
     } else {
       ycol[j] = yb + v0 + col;
@@ -2065,7 +2087,7 @@ static bool conv_win() {
 static int igemm_cl(const void* xs, const void* wsplit, const float* bias, int b, int cin,
                     int cout, int r, float* y, void* ws, size_t ws_bytes, void* stream,
                     const uint32_t* tmask, int mmode, const int* vlist = nullptr,
-                    const int* vcount = nullptr) {
+                    const int* vcount = nullptr, int lg = 5) {
   PCFM_CHECK_ARG(conv3_shape_ok(b, cin, cout, r),
                  "conv3d_igemm_cl: unsupported shape b=%d cin=%d cout=%d r=%d", b, cin, cout, r);
   if (b == 0) return PCFM_OK;
@@ -2126,11 +2148,11 @@ static int igemm_cl(const void* xs, const void* wsplit, const float* bias, int b
     if (PCFM_CONV_GK == 16 || cin % 32 != 0)
       hipLaunchKernelGGL(conv3_igemm_glds_kernel<16>, dim3((unsigned)glds_blocks), dim3(512), 0,
                          st, xh, xl, wh, wh + kSplitLo, zrow, bias, y, cin, cout, r, S, part, tmask,
-                         mm, vl, vc);
+                         mm, vl, vc, lg);
     else
       hipLaunchKernelGGL(conv3_igemm_glds_kernel<32>, dim3((unsigned)glds_blocks), dim3(512), 0,
                          st, xh, xl, wh, wh + kSplitLo, zrow, bias, y, cin, cout, r, S, part, tmask,
-                         mm, vl, vc);
+                         mm, vl, vc, lg);
     if (S > 1) {
       const long long total4 = (long long)b * cout * V / 4;
       hipLaunchKernelGGL(conv3_ksum_kernel, dim3((unsigned)ceil_div(total4, 256)), dim3(256), 0,
@@ -2194,11 +2216,14 @@ extern "C" int pcfm_conv3d_occupancy(const int* cnt, int b, int r, unsigned* mas
   return check_launch("conv3d_occupancy");
 }
 
+// Buffer: int32 counts[3] | pad to 64 | per-tile counts / offsets [2][tiles] |
+// list 0 [B V / 32] | list 1 [B V / 32] | per-tile counts / offsets of list 2
+// [tiles] | list 2 [B V] (the occupied voxels, global indices b V + v).
 extern "C" size_t pcfm_conv3d_vlist_bytes(int b, int r) {
   const long long v = (long long)r * r * r;
   if (b <= 0 || r <= 0 || v % 256 != 0 || (long long)b * v >= (1LL << 31)) return 0;
   const long long tiles = (long long)b * v / 256;
-  return (size_t)(64 + 2 * tiles + 2 * (long long)b * v / kChunk) * sizeof(int);
+  return (size_t)(64 + 3 * tiles + 2 * (long long)b * v / kChunk + (long long)b * v) * sizeof(int);
 }
 
 extern "C" int pcfm_conv3d_vlist(const int* cnt, int b, int r, int* lists, void* stream) {
@@ -2208,11 +2233,26 @@ extern "C" int pcfm_conv3d_vlist(const int* cnt, int b, int r, int* lists, void*
   hipStream_t st = (hipStream_t)stream;
   int* tc = lists + 64;
   int* l0 = tc + 2 * tiles;
-  hipLaunchKernelGGL(conv3_vlist_count_kernel, dim3(tiles), dim3(256), 0, st, cnt, r, tiles, tc);
-  hipLaunchKernelGGL(conv3_vlist_scan_kernel, dim3(1), dim3(1024), 0, st, tc, tiles, lists);
+  int* tc2 = l0 + 2 * ((size_t)b * V / kChunk);
+  int* l2 = tc2 + tiles;
+  hipLaunchKernelGGL(conv3_vlist_count_kernel, dim3(tiles), dim3(256), 0, st, cnt, r, tiles, tc,
+                     tc2);
+  hipLaunchKernelGGL(conv3_vlist_scan_kernel, dim3(1), dim3(1024), 0, st, tc, tiles, lists, 2);
+  hipLaunchKernelGGL(conv3_vlist_scan_kernel, dim3(1), dim3(1024), 0, st, tc2, tiles, lists + 2,
+                     1);
   hipLaunchKernelGGL(conv3_vlist_write_kernel, dim3(tiles), dim3(256), 0, st, cnt, r, tiles, tc,
-                     l0, l0 + (size_t)b * V / kChunk);
+                     l0, l0 + (size_t)b * V / kChunk, (const int*)tc2, l2);
   return check_launch("conv3d_vlist");
+}
+
+// The backward-data list form (which 0) over single occupied voxels (list 2)
+// instead of 32-voxel chunks (env PCFM_LIST_VOX=0: the chunk list; read per
+// call: A/B runs).  At the C2 stages an occupied chunk holds 27 % (r = 32) /
+// 36 % (r = 16) occupied voxels, so the chunk form computed ~3x the products
+// the voxelization backward reads back.
+static bool list_vox() {
+  const char* e = getenv("PCFM_LIST_VOX");
+  return e == nullptr || e[0] != '0';
 }
 
 extern "C" int pcfm_conv3d_igemm_cl_list(const void* xs, const void* wsplit, const float* bias,
@@ -2227,7 +2267,6 @@ extern "C" int pcfm_conv3d_igemm_cl_list(const void* xs, const void* wsplit, con
                  "conv3d_igemm_cl_list: unsupported shape b=%d cin=%d cout=%d r=%d", b, cin, cout,
                  r);
   const int V = r * r * r, tiles = b * (V / 256);
-  const int* l = lists + 64 + 2 * tiles + (size_t)which * b * V / kChunk;
 #ifndef PCFM_CONV_NOGLDS
   const bool listed = glds_ok(cout, r) && glds_splits(b, cin, cout, r) == 1;
 #else
@@ -2235,13 +2274,16 @@ extern "C" int pcfm_conv3d_igemm_cl_list(const void* xs, const void* wsplit, con
 #endif
   if (!listed)  // no list form for this shape: the dense GEMM (every voxel)
     return igemm_cl(xs, wsplit, bias, b, cin, cout, r, y, ws, ws_bytes, stream, nullptr, 0);
+  const bool vox = which == 0 && list_vox();
+  const int* l = vox ? lists + 64 + 3 * tiles + 2 * ((size_t)b * V / kChunk)
+                     : lists + 64 + 2 * tiles + (size_t)which * b * V / kChunk;
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(conv3_fill_unlisted_kernel, dim3(tiles), dim3(256), 0, st, cnt, r, cout,
-                     which, bias, y);
+                     which, bias, y, vox ? 1 : 0);
   const int e = check_launch("conv3d_igemm_cl_list");
   if (e) return e;
   return igemm_cl(xs, wsplit, bias, b, cin, cout, r, y, ws, ws_bytes, stream, nullptr, 0, l,
-                  lists + which);
+                  vox ? lists + 2 : lists + which, vox ? 0 : 5);
 }
 
 static int wgrad_cap(int b, int r, int S) {

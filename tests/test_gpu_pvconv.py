@@ -287,7 +287,8 @@ def test_conv_voxel_lists(ops, b, r, n, surface):
     """pcfm_conv3d_vlist against torch: list 0 = the 32-voxel chunks holding an
     occupied voxel, list 1 = the chunks holding a voxel with an occupied voxel in
     its 3x3x3 neighbourhood, both as ascending global chunk indices
-    (b r^3 + v) / 32, with the device-side counts first."""
+    (b r^3 + v) / 32; list 2 = the occupied voxels, ascending b r^3 + v; the
+    device-side counts first."""
     _, cnt, _ = _voxelized(ops, b, 8, r, n, 3 * r, surface)
     lists = ops.conv3d_vlists(cnt, r)
     assert lists is not None
@@ -297,13 +298,16 @@ def test_conv_voxel_lists(ops, b, r, n, surface):
     want0 = torch.nonzero(occ.view(-1, 32).amax(1) > 0).view(-1).int()
     want1 = torch.nonzero(act.reshape(-1, 32).any(1)).view(-1).int()
     tiles = b * v // 256
-    counts = lists[:2].tolist()
-    assert counts == [want0.numel(), want1.numel()]
+    want2 = torch.nonzero(occ.view(-1) > 0).view(-1).int()
+    counts = lists[:3].tolist()
+    assert counts == [want0.numel(), want1.numel(), want2.numel()]
     nch = b * v // 32
     l0 = lists[64 + 2 * tiles: 64 + 2 * tiles + nch]
     l1 = lists[64 + 2 * tiles + nch: 64 + 2 * tiles + 2 * nch]
+    l2 = lists[64 + 3 * tiles + 2 * nch: 64 + 3 * tiles + 2 * nch + b * v]
     assert torch.equal(l0[: counts[0]], want0)
     assert torch.equal(l1[: counts[1]], want1)
+    assert torch.equal(l2[: counts[2]], want2)
 
 
 @pytest.mark.parametrize("b,cin,cout,r,surface", [(4, 128, 128, 32, False),
@@ -311,7 +315,7 @@ def test_conv_voxel_lists(ops, b, r, n, surface):
                                                   (4, 128, 128, 32, True),
                                                   (8, 256, 256, 16, False),
                                                   (4, 256, 256, 8, False)])
-def test_conv_voxel_list_gemm_is_exact(ops, b, cin, cout, r, surface, report):
+def test_conv_voxel_list_gemm_is_exact(ops, monkeypatch, b, cin, cout, r, surface, report):
     """The voxel-list form of PVConv's first conv: the forward bit-identical to
     the dense GEMM at every voxel (bias where no occupied voxel is near), the
     backward-data bit-identical at every occupied voxel and 0 in chunks without one
@@ -332,14 +336,19 @@ def test_conv_voxel_list_gemm_is_exact(ops, b, cin, cout, r, surface, report):
     gys = ops.conv3d_split(dy)
     imgt = ops.conv3d_prep_weight(w, True)
     dx0 = ops.conv3d_igemm_split(gys, imgt, None, b, cout, cin, r, "conv3d_bwd_data")
-    dx1 = ops.conv3d_igemm_split(gys, imgt, None, b, cout, cin, r, "conv3d_bwd_data",
-                                 occ_mode=2, vlists=lists, cnt=cnt)
     occupied = (cnt.view(b, 1, -1) > 0).expand(b, cin, r ** 3)
-    assert torch.equal(dx0.view(b, cin, -1)[occupied], dx1.view(b, cin, -1)[occupied])
-    # at the other voxels: 0 in the chunks without an occupied voxel, the dense
-    # value in the others (and everywhere on shapes without the list form)
-    rest1, rest0 = dx1.view(b, cin, -1)[~occupied], dx0.view(b, cin, -1)[~occupied]
-    assert bool(((rest1 == 0) | (rest1 == rest0)).all())
+    # the voxel-list form (default) and the chunk-list form (PCFM_LIST_VOX=0)
+    for vox in ("1", "0"):
+        monkeypatch.setenv("PCFM_LIST_VOX", vox)
+        dx1 = ops.conv3d_igemm_split(gys, imgt, None, b, cout, cin, r, "conv3d_bwd_data",
+                                     occ_mode=2, vlists=lists, cnt=cnt)
+        assert torch.equal(dx0.view(b, cin, -1)[occupied], dx1.view(b, cin, -1)[occupied]), vox
+        # at the other voxels: 0 (voxel list: everywhere; chunk list: in the chunks
+        # without an occupied voxel), else the dense value (and everywhere on
+        # shapes without the list form)
+        rest1, rest0 = dx1.view(b, cin, -1)[~occupied], dx0.view(b, cin, -1)[~occupied]
+        assert bool(((rest1 == 0) | (rest1 == rest0)).all()), vox
+    monkeypatch.delenv("PCFM_LIST_VOX")
     report(f"conv_voxel_lists_b{b}_c{cin}_r{r}{'_surface' if surface else ''}",
            {"occupied_fraction": float((cnt > 0).float().mean()),
             "listed_fwd_chunk_fraction": int(lists[1]) * 32 / float(b * r ** 3),
