@@ -336,24 +336,25 @@ int pcfm_conv3d_occupancy(const int* cnt, int b, int r, unsigned* masks, void* s
 int pcfm_conv3d_igemm_cl_occ(const void* xs, const void* wsplit, const float* bias, int b,
                              int cin, int cout, int r, const unsigned* masks, int mode, float* y,
                              void* ws, size_t ws_bytes, void* stream);
-/* Chunk lists of a voxelized grid (the same counts cnt i32 [b][r^3]; a chunk =
- * 32 consecutive voxels): list 0 = the chunks holding an occupied voxel, list 1
- * = the chunks holding a voxel with an occupied voxel in its 3x3x3
- * neighbourhood; entries are chunk indices (b r^3 + v) / 32, ascending; list 2
- * = the occupied voxels themselves, b r^3 + v, ascending.  The device-side
- * counts lead the buffer (pcfm_conv3d_vlist_bytes; 0 = unsupported:
- * r^3 % 256 != 0 or b r^3 >= 2^31). */
+/* Chunk and voxel lists of a voxelized grid (the same counts cnt i32 [b][r^3];
+ * a chunk = 32 consecutive voxels): list 0 = the chunks holding an occupied
+ * voxel, list 1 = the chunks holding a voxel with an occupied voxel in its
+ * 3x3x3 neighbourhood, as chunk indices (b r^3 + v) / 32; lists 2 / 3 = the
+ * occupied / neighbourhood-occupied voxels themselves, b r^3 + v; all
+ * ascending.  The four device-side counts lead the buffer
+ * (pcfm_conv3d_vlist_bytes; 0 = unsupported: r^3 % 256 != 0 or b r^3 >= 2^31). */
 size_t pcfm_conv3d_vlist_bytes(int b, int r);
 int pcfm_conv3d_vlist(const int* cnt, int b, int r, int* lists, void* stream);
-/* pcfm_conv3d_igemm_cl computed in the chunks of list `which` only (its GEMM
- * tiles are 8 listed chunks, their B rows the chunks' neighbours): which 1
- * (forward over a voxelized input x: elsewhere the output is exactly the bias,
- * written as such -- bit-identical to pcfm_conv3d_igemm_cl everywhere), which 0
- * (backward-data into a voxelized grid, bias NULL: equal to
- * pcfm_conv3d_igemm_cl at every occupied voxel, 0 at every other voxel --
- * computed over list 2, voxel by voxel; PCFM_LIST_VOX=0: over the chunks of
- * list 0, 0 in the unlisted chunks).  Shapes without
- * the list form (split-K grids, r = 8 at the C2 sizes) run the dense GEMM.
+/* pcfm_conv3d_igemm_cl computed at the listed voxels only (GEMM tiles of 256
+ * listed voxels, their B rows the voxels' neighbours): which 1 (forward over a
+ * voxelized input x, list 3: elsewhere the output is exactly the bias, written
+ * as such -- bit-identical to pcfm_conv3d_igemm_cl everywhere), which 0
+ * (backward-data into a voxelized grid, bias NULL, list 2: equal to
+ * pcfm_conv3d_igemm_cl at every occupied voxel, 0 at every other voxel).  Env
+ * PCFM_LIST_VOX (bit 0: which 0, bit 1: which 1; default 3) -- a cleared bit
+ * runs that direction over the chunk list (0 / 1) instead: 8 chunks per tile,
+ * the same values at the voxels the contract names.  Shapes without the list
+ * form (split-K grids, r = 8 at the C2 sizes) run the dense GEMM.
  * Fully writes y; same workspace as pcfm_conv3d_igemm_cl. */
 int pcfm_conv3d_igemm_cl_list(const void* xs, const void* wsplit, const float* bias, int b,
                               int cin, int cout, int r, const int* cnt, const int* lists,

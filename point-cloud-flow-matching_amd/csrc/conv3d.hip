@@ -114,8 +114,8 @@ __global__ void __launch_bounds__(256)
 // its bias: its input is 0 there).  Whole chunks keep the GEMM's B-row fetches
 // and output stores 128-B runs (voxel-granular lists measured slower: short
 // scattered runs).  Entries are global chunk indices (b V + v) / 32, ascending
-// (deterministic).  List 2: the occupied voxels themselves, global voxel
-// indices b V + v, ascending (the backward-data's voxel-granular form).
+// (deterministic).  Lists 2 / 3: the occupied / active voxels themselves,
+// global voxel indices b V + v, ascending (the voxel-granular forms).
 // Buffer layout: pcfm_conv3d_vlist_bytes.
 // ---------------------------------------------------------------------------
 constexpr int kChunk = 32;
@@ -134,42 +134,53 @@ __device__ __forceinline__ void vlist_flags(const int* __restrict__ c, int v, in
   }
 }
 
-// chunk flags of this thread's chunk (32 consecutive lanes = one chunk)
+// chunk flags of this thread's chunk (32 consecutive lanes = one chunk); o, a:
+// the thread's own voxel's flags
 __device__ __forceinline__ void chunk_flags(const int* __restrict__ cnt, long long g, int R,
-                                            bool& occ, bool& act) {
+                                            bool& occ, bool& act, bool& o, bool& a) {
   const int V = R * R * R;
-  bool o, a;
   vlist_flags(cnt + (g / V) * V, (int)(g % V), R, o, a);
   const int sh = threadIdx.x & 32;
   occ = ((__ballot(o) >> sh) & 0xFFFFFFFFull) != 0ull;
   act = ((__ballot(a) >> sh) & 0xFFFFFFFFull) != 0ull;
 }
+__device__ __forceinline__ void chunk_flags(const int* __restrict__ cnt, long long g, int R,
+                                            bool& occ, bool& act) {
+  bool o, a;
+  chunk_flags(cnt, g, R, occ, act, o, a);
+}
 
 // grid = B V / 256 tiles (8 chunks each), 256 threads: per-tile chunk counts
+// (lists 0, 1 -> tcount[2][tiles]) and voxel counts (lists 2, 3 -> tcount2[2][tiles])
 __global__ void __launch_bounds__(256)
     conv3_vlist_count_kernel(const int* __restrict__ cnt, int R, int tiles,
                              int* __restrict__ tcount, int* __restrict__ tcount2) {
   __shared__ int ws[2][8];
-  __shared__ int wv[4];
+  __shared__ int wv[2][4];
   const int t = threadIdx.x;
   const long long g = (long long)blockIdx.x * 256 + t;
-  bool occ, act;
-  chunk_flags(cnt, g, R, occ, act);
+  bool occ, act, o, a;
+  chunk_flags(cnt, g, R, occ, act, o, a);
   if ((t & 31) == 0) {
     ws[0][t >> 5] = occ ? 1 : 0;
     ws[1][t >> 5] = act ? 1 : 0;
   }
-  // occupied voxels (list 2): per-wave ballot counts
-  const int n2 = __popcll(__ballot(cnt[g] > 0));
-  if ((t & 63) == 0) wv[t >> 6] = n2;
+  // occupied / active voxels (lists 2, 3): per-wave ballot counts
+  const int n2 = __popcll(__ballot(o)), n3 = __popcll(__ballot(a));
+  if ((t & 63) == 0) {
+    wv[0][t >> 6] = n2;
+    wv[1][t >> 6] = n3;
+  }
   __syncthreads();
   if (t < 2) {
     int n = 0;
 #pragma unroll
     for (int q = 0; q < 8; ++q) n += ws[t][q];
     tcount[t * tiles + blockIdx.x] = n;
+  } else if (t < 4) {
+    const int k = t - 2;
+    tcount2[k * tiles + blockIdx.x] = ((wv[k][0] + wv[k][1]) + wv[k][2]) + wv[k][3];
   }
-  if (t == 2) tcount2[blockIdx.x] = ((wv[0] + wv[1]) + wv[2]) + wv[3];
 }
 
 // one block: exclusive scans of the two per-tile count rows (in place) and
@@ -207,31 +218,41 @@ __global__ void __launch_bounds__(1024)
   }
 }
 
-// grid = tiles, 256 threads: each tile writes its listed chunks at its offsets
+// grid = tiles, 256 threads: each tile writes its listed chunks and voxels at
+// its offsets
 __global__ void __launch_bounds__(256)
     conv3_vlist_write_kernel(const int* __restrict__ cnt, int R, int tiles,
                              const int* __restrict__ toff, int* __restrict__ list0,
                              int* __restrict__ list1, const int* __restrict__ toff2,
-                             int* __restrict__ list2) {
+                             int* __restrict__ list2, int* __restrict__ list3) {
   __shared__ int ws[2][8];
-  __shared__ int wv[4];
+  __shared__ int wv[2][4];
   const int t = threadIdx.x;
   const long long g = (long long)blockIdx.x * 256 + t;
-  bool occ, act;
-  chunk_flags(cnt, g, R, occ, act);
+  bool occ, act, o, a;
+  chunk_flags(cnt, g, R, occ, act, o, a);
   if ((t & 31) == 0) {
     ws[0][t >> 5] = occ ? 1 : 0;
     ws[1][t >> 5] = act ? 1 : 0;
   }
-  const bool o2 = cnt[g] > 0;
-  const unsigned long long m2 = __ballot(o2);
-  if ((t & 63) == 0) wv[t >> 6] = __popcll(m2);
+  const unsigned long long m2 = __ballot(o), m3 = __ballot(a);
+  if ((t & 63) == 0) {
+    wv[0][t >> 6] = __popcll(m2);
+    wv[1][t >> 6] = __popcll(m3);
+  }
   __syncthreads();
-  if (o2) {  // list 2: the occupied voxels in voxel order
-    int p2 = toff2[blockIdx.x];
-    for (int u = 0; u < (t >> 6); ++u) p2 += wv[u];
-    p2 += __builtin_amdgcn_mbcnt_hi((unsigned)(m2 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m2, 0u));
-    list2[p2] = (int)g;
+  // lists 2 / 3: the occupied / active voxels in voxel order
+  if (o) {
+    int p = toff2[blockIdx.x];
+    for (int u = 0; u < (t >> 6); ++u) p += wv[0][u];
+    p += __builtin_amdgcn_mbcnt_hi((unsigned)(m2 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m2, 0u));
+    list2[p] = (int)g;
+  }
+  if (a) {
+    int p = toff2[tiles + blockIdx.x];
+    for (int u = 0; u < (t >> 6); ++u) p += wv[1][u];
+    p += __builtin_amdgcn_mbcnt_hi((unsigned)(m3 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m3, 0u));
+    list3[p] = (int)g;
   }
   if ((t & 31) == 0) {
     const int q = t >> 5, chunk = blockIdx.x * 8 + q;
@@ -253,10 +274,10 @@ __global__ void __launch_bounds__(256)
                                const float* __restrict__ bias, float* __restrict__ y, int vox) {
   const int V = R * R * R;
   const long long g = (long long)blockIdx.x * 256 + threadIdx.x;
-  bool occ, act;
-  chunk_flags(cnt, g, R, occ, act);
-  // vox (which 0 over the voxel list): every voxel without a point
-  if (vox ? cnt[g] > 0 : (which == 0 ? occ : act)) return;
+  bool occ, act, o, a;
+  chunk_flags(cnt, g, R, occ, act, o, a);
+  // vox (over the voxel lists 2 / 3): every voxel not in the list
+  if (which == 0 ? (vox ? o : occ) : (vox ? a : act)) return;
   const int b = (int)(g / V), v = (int)(g % V);
   float* __restrict__ yb = y + (size_t)b * M * V + v;
   for (int m = 0; m < M; ++m)
@@ -2216,14 +2237,16 @@ extern "C" int pcfm_conv3d_occupancy(const int* cnt, int b, int r, unsigned* mas
   return check_launch("conv3d_occupancy");
 }
 
-// Buffer: int32 counts[3] | pad to 64 | per-tile counts / offsets [2][tiles] |
-// list 0 [B V / 32] | list 1 [B V / 32] | per-tile counts / offsets of list 2
-// [tiles] | list 2 [B V] (the occupied voxels, global indices b V + v).
+// Buffer: int32 counts[4] | pad to 64 | per-tile counts / offsets [2][tiles] |
+// list 0 [B V / 32] | list 1 [B V / 32] | per-tile counts / offsets of lists 2, 3
+// [2][tiles] | list 2 [B V] (the occupied voxels, global indices b V + v) |
+// list 3 [B V] (the voxels with an occupied voxel in their 3x3x3 neighbourhood).
 extern "C" size_t pcfm_conv3d_vlist_bytes(int b, int r) {
   const long long v = (long long)r * r * r;
   if (b <= 0 || r <= 0 || v % 256 != 0 || (long long)b * v >= (1LL << 31)) return 0;
   const long long tiles = (long long)b * v / 256;
-  return (size_t)(64 + 3 * tiles + 2 * (long long)b * v / kChunk + (long long)b * v) * sizeof(int);
+  return (size_t)(64 + 4 * tiles + 2 * (long long)b * v / kChunk + 2 * (long long)b * v) *
+         sizeof(int);
 }
 
 extern "C" int pcfm_conv3d_vlist(const int* cnt, int b, int r, int* lists, void* stream) {
@@ -2234,25 +2257,25 @@ extern "C" int pcfm_conv3d_vlist(const int* cnt, int b, int r, int* lists, void*
   int* tc = lists + 64;
   int* l0 = tc + 2 * tiles;
   int* tc2 = l0 + 2 * ((size_t)b * V / kChunk);
-  int* l2 = tc2 + tiles;
+  int* l2 = tc2 + 2 * tiles;
   hipLaunchKernelGGL(conv3_vlist_count_kernel, dim3(tiles), dim3(256), 0, st, cnt, r, tiles, tc,
                      tc2);
   hipLaunchKernelGGL(conv3_vlist_scan_kernel, dim3(1), dim3(1024), 0, st, tc, tiles, lists, 2);
   hipLaunchKernelGGL(conv3_vlist_scan_kernel, dim3(1), dim3(1024), 0, st, tc2, tiles, lists + 2,
-                     1);
+                     2);
   hipLaunchKernelGGL(conv3_vlist_write_kernel, dim3(tiles), dim3(256), 0, st, cnt, r, tiles, tc,
-                     l0, l0 + (size_t)b * V / kChunk, (const int*)tc2, l2);
+                     l0, l0 + (size_t)b * V / kChunk, (const int*)tc2, l2, l2 + (size_t)b * V);
   return check_launch("conv3d_vlist");
 }
 
-// The backward-data list form (which 0) over single occupied voxels (list 2)
-// instead of 32-voxel chunks (env PCFM_LIST_VOX=0: the chunk list; read per
-// call: A/B runs).  At the C2 stages an occupied chunk holds 27 % (r = 32) /
-// 36 % (r = 16) occupied voxels, so the chunk form computed ~3x the products
-// the voxelization backward reads back.
-static bool list_vox() {
+// The list forms over single voxels (lists 2 / 3) instead of 32-voxel chunks
+// (lists 0 / 1): env PCFM_LIST_VOX bit 0 = backward-data (which 0), bit 1 =
+// forward (which 1); default 3; read per call (A/B runs).  At the C2 stages an
+// occupied chunk holds 27 % (r = 32) / 36 % (r = 16) occupied voxels, and a
+// listed forward chunk 49 % / 61 % active voxels.
+static int list_vox() {
   const char* e = getenv("PCFM_LIST_VOX");
-  return e == nullptr || e[0] != '0';
+  return e == nullptr ? 3 : (atoi(e) & 3);
 }
 
 extern "C" int pcfm_conv3d_igemm_cl_list(const void* xs, const void* wsplit, const float* bias,
@@ -2274,8 +2297,9 @@ extern "C" int pcfm_conv3d_igemm_cl_list(const void* xs, const void* wsplit, con
 #endif
   if (!listed)  // no list form for this shape: the dense GEMM (every voxel)
     return igemm_cl(xs, wsplit, bias, b, cin, cout, r, y, ws, ws_bytes, stream, nullptr, 0);
-  const bool vox = which == 0 && list_vox();
-  const int* l = vox ? lists + 64 + 3 * tiles + 2 * ((size_t)b * V / kChunk)
+  const bool vox = (list_vox() >> which) & 1;
+  const int* l = vox ? lists + 64 + 4 * tiles + 2 * ((size_t)b * V / kChunk) +
+                           (size_t)which * b * V
                      : lists + 64 + 2 * tiles + (size_t)which * b * V / kChunk;
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(conv3_fill_unlisted_kernel, dim3(tiles), dim3(256), 0, st, cnt, r, cout,
@@ -2283,7 +2307,7 @@ extern "C" int pcfm_conv3d_igemm_cl_list(const void* xs, const void* wsplit, con
   const int e = check_launch("conv3d_igemm_cl_list");
   if (e) return e;
   return igemm_cl(xs, wsplit, bias, b, cin, cout, r, y, ws, ws_bytes, stream, nullptr, 0, l,
-                  vox ? lists + 2 : lists + which, vox ? 0 : 5);
+                  vox ? lists + 2 + which : lists + which, vox ? 0 : 5);
 }
 
 static int wgrad_cap(int b, int r, int S) {

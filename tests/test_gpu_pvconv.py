@@ -299,15 +299,18 @@ def test_conv_voxel_lists(ops, b, r, n, surface):
     want1 = torch.nonzero(act.reshape(-1, 32).any(1)).view(-1).int()
     tiles = b * v // 256
     want2 = torch.nonzero(occ.view(-1) > 0).view(-1).int()
-    counts = lists[:3].tolist()
-    assert counts == [want0.numel(), want1.numel(), want2.numel()]
+    want3 = torch.nonzero(act.reshape(-1)).view(-1).int()
+    counts = lists[:4].tolist()
+    assert counts == [want0.numel(), want1.numel(), want2.numel(), want3.numel()]
     nch = b * v // 32
     l0 = lists[64 + 2 * tiles: 64 + 2 * tiles + nch]
     l1 = lists[64 + 2 * tiles + nch: 64 + 2 * tiles + 2 * nch]
-    l2 = lists[64 + 3 * tiles + 2 * nch: 64 + 3 * tiles + 2 * nch + b * v]
+    l2 = lists[64 + 4 * tiles + 2 * nch: 64 + 4 * tiles + 2 * nch + b * v]
+    l3 = lists[64 + 4 * tiles + 2 * nch + b * v: 64 + 4 * tiles + 2 * nch + 2 * b * v]
     assert torch.equal(l0[: counts[0]], want0)
     assert torch.equal(l1[: counts[1]], want1)
     assert torch.equal(l2[: counts[2]], want2)
+    assert torch.equal(l3[: counts[3]], want3)
 
 
 @pytest.mark.parametrize("b,cin,cout,r,surface", [(4, 128, 128, 32, False),
@@ -329,9 +332,12 @@ def test_conv_voxel_list_gemm_is_exact(ops, monkeypatch, b, cin, cout, r, surfac
     bias = torch.randn(cout, device="cuda", generator=g)
     img = ops.conv3d_prep_weight(w, False)
     y0 = ops.conv3d_igemm_split(xs, img, bias, b, cin, cout, r, "conv3d_fwd")
-    y1 = ops.conv3d_igemm_split(xs, img, bias, b, cin, cout, r, "conv3d_fwd", occ_mode=1,
-                                vlists=lists, cnt=cnt)
-    assert torch.equal(y0, y1)
+    for vox in ("3", "0"):  # voxel list 3 (default), chunk list 1
+        monkeypatch.setenv("PCFM_LIST_VOX", vox)
+        y1 = ops.conv3d_igemm_split(xs, img, bias, b, cin, cout, r, "conv3d_fwd", occ_mode=1,
+                                    vlists=lists, cnt=cnt)
+        assert torch.equal(y0, y1), vox
+    monkeypatch.delenv("PCFM_LIST_VOX")
     dy = torch.randn(b, cout, r, r, r, device="cuda", generator=g)
     gys = ops.conv3d_split(dy)
     imgt = ops.conv3d_prep_weight(w, True)
