@@ -224,7 +224,8 @@ __global__ void __launch_bounds__(256)
     conv3_vlist_write_kernel(const int* __restrict__ cnt, int R, int tiles,
                              const int* __restrict__ toff, int* __restrict__ list0,
                              int* __restrict__ list1, const int* __restrict__ toff2,
-                             int* __restrict__ list2, int* __restrict__ list3) {
+                             int* __restrict__ list2, int* __restrict__ list3,
+                             uint32_t* __restrict__ bits2, uint32_t* __restrict__ bits3) {
   __shared__ int ws[2][8];
   __shared__ int wv[2][4];
   const int t = threadIdx.x;
@@ -239,6 +240,10 @@ __global__ void __launch_bounds__(256)
   if ((t & 63) == 0) {
     wv[0][t >> 6] = __popcll(m2);
     wv[1][t >> 6] = __popcll(m3);
+  }
+  if ((t & 31) == 0) {  // the lists' voxel bitmaps (bit g & 31 of word g >> 5)
+    bits2[g >> 5] = (uint32_t)(m2 >> (t & 32));
+    bits3[g >> 5] = (uint32_t)(m3 >> (t & 32));
   }
   __syncthreads();
   // lists 2 / 3: the occupied / active voxels in voxel order
@@ -271,13 +276,17 @@ __global__ void __launch_bounds__(256)
 // grid = B V / 256, 256 threads.
 __global__ void __launch_bounds__(256)
     conv3_fill_unlisted_kernel(const int* __restrict__ cnt, int R, int M, int which,
-                               const float* __restrict__ bias, float* __restrict__ y, int vox) {
+                               const float* __restrict__ bias, float* __restrict__ y,
+                               const uint32_t* __restrict__ vbits) {
   const int V = R * R * R;
   const long long g = (long long)blockIdx.x * 256 + threadIdx.x;
-  bool occ, act, o, a;
-  chunk_flags(cnt, g, R, occ, act, o, a);
-  // vox (over the voxel lists 2 / 3): every voxel not in the list
-  if (which == 0 ? (vox ? o : occ) : (vox ? a : act)) return;
+  if (vbits != nullptr) {  // over a voxel list (2 / 3): every voxel not in it
+    if ((vbits[g >> 5] >> (g & 31)) & 1u) return;
+  } else {
+    bool occ, act;
+    chunk_flags(cnt, g, R, occ, act);
+    if (which == 0 ? occ : act) return;
+  }
   const int b = (int)(g / V), v = (int)(g % V);
   float* __restrict__ yb = y + (size_t)b * M * V + v;
   for (int m = 0; m < M; ++m)
@@ -2240,12 +2249,13 @@ extern "C" int pcfm_conv3d_occupancy(const int* cnt, int b, int r, unsigned* mas
 // Buffer: int32 counts[4] | pad to 64 | per-tile counts / offsets [2][tiles] |
 // list 0 [B V / 32] | list 1 [B V / 32] | per-tile counts / offsets of lists 2, 3
 // [2][tiles] | list 2 [B V] (the occupied voxels, global indices b V + v) |
-// list 3 [B V] (the voxels with an occupied voxel in their 3x3x3 neighbourhood).
+// list 3 [B V] (the voxels with an occupied voxel in their 3x3x3 neighbourhood)
+// | bitmaps of lists 2, 3 [2][B V / 32] (bit v & 31 of word v >> 5).
 extern "C" size_t pcfm_conv3d_vlist_bytes(int b, int r) {
   const long long v = (long long)r * r * r;
   if (b <= 0 || r <= 0 || v % 256 != 0 || (long long)b * v >= (1LL << 31)) return 0;
   const long long tiles = (long long)b * v / 256;
-  return (size_t)(64 + 4 * tiles + 2 * (long long)b * v / kChunk + 2 * (long long)b * v) *
+  return (size_t)(64 + 4 * tiles + 4 * (long long)b * v / kChunk + 2 * (long long)b * v) *
          sizeof(int);
 }
 
@@ -2263,8 +2273,10 @@ extern "C" int pcfm_conv3d_vlist(const int* cnt, int b, int r, int* lists, void*
   hipLaunchKernelGGL(conv3_vlist_scan_kernel, dim3(1), dim3(1024), 0, st, tc, tiles, lists, 2);
   hipLaunchKernelGGL(conv3_vlist_scan_kernel, dim3(1), dim3(1024), 0, st, tc2, tiles, lists + 2,
                      2);
+  uint32_t* bits = (uint32_t*)(l2 + 2 * (size_t)b * V);
   hipLaunchKernelGGL(conv3_vlist_write_kernel, dim3(tiles), dim3(256), 0, st, cnt, r, tiles, tc,
-                     l0, l0 + (size_t)b * V / kChunk, (const int*)tc2, l2, l2 + (size_t)b * V);
+                     l0, l0 + (size_t)b * V / kChunk, (const int*)tc2, l2, l2 + (size_t)b * V,
+                     bits, bits + (size_t)b * V / kChunk);
   return check_launch("conv3d_vlist");
 }
 
@@ -2302,8 +2314,13 @@ extern "C" int pcfm_conv3d_igemm_cl_list(const void* xs, const void* wsplit, con
                            (size_t)which * b * V
                      : lists + 64 + 2 * tiles + (size_t)which * b * V / kChunk;
   hipStream_t st = (hipStream_t)stream;
+  const uint32_t* vbits =
+      vox ? (const uint32_t*)(lists + 64 + 4 * tiles + 2 * ((size_t)b * V / kChunk) +
+                              2 * (size_t)b * V) +
+                (size_t)which * b * V / kChunk
+          : nullptr;
   hipLaunchKernelGGL(conv3_fill_unlisted_kernel, dim3(tiles), dim3(256), 0, st, cnt, r, cout,
-                     which, bias, y, vox ? 1 : 0);
+                     which, bias, y, vbits);
   const int e = check_launch("conv3d_igemm_cl_list");
   if (e) return e;
   return igemm_cl(xs, wsplit, bias, b, cin, cout, r, y, ws, ws_bytes, stream, nullptr, 0, l,
