@@ -42,6 +42,15 @@ def test_workspace_queries():
         q("pcfm_emd_workspace_bytes", 2, 100, 100, 8)
     assert q("pcfm_emd_workspace_bytes", 2, 100, 100, 3) == 0
     assert q("pcfm_avg_voxelize_fwd_workspace_bytes", -1, 1, 1, 2) == 0
+    # occupancy masks: tile / pair-chunk / 16-voxel words; voxel lists: counts,
+    # per-tile offsets of the chunk and voxel lists, lists 0-3 and the voxel
+    # lists' bitmaps (include/pcfm.h)
+    b, r = 2, 32
+    v = r ** 3
+    assert q("pcfm_conv3d_occupancy_bytes", b, r) == 4 * b * (v // 256 + v // 64 + v // 16)
+    tiles = b * v // 256
+    assert q("pcfm_conv3d_vlist_bytes", b, r) == 4 * (64 + 4 * tiles + 4 * b * v // 32 + 2 * b * v)
+    assert q("pcfm_conv3d_vlist_bytes", b, 6) == 0  # r^3 % 256 != 0
 
 
 def test_invalid_arguments_rejected_on_host():
