@@ -623,7 +623,8 @@ __global__ void __launch_bounds__(GN * 2)  // GK<KT, GN>::NW = GN / 32 waves
                             float* __restrict__ y, int K, int M, int R, int S,
                             float* __restrict__ part, const uint32_t* __restrict__ tmask,
                             int mmode, const int* __restrict__ vlist = nullptr,
-                            const int* __restrict__ vcount = nullptr, int lg = 5) {
+                            const int* __restrict__ vcount = nullptr, int lg = 5,
+                            const uint32_t* __restrict__ obits = nullptr) {
   using G = GK<KT, GN>;
   __shared__ __attribute__((aligned(16))) uint8_t lds[NST * G::STAGE];
   const int V = R * R * R, R2 = R * R;
@@ -725,6 +726,19 @@ __global__ void __launch_bounds__(GN * 2)  // GK<KT, GN>::NW = GN / 32 waves
 #pragma unroll
     for (int t = 0; t < 27; ++t)
       m |= (((ax >> (t / 9)) & (ay >> ((t / 3) % 3)) & (az >> (t % 3))) & 1u) << t;
+    // obits (the forward over a voxelized input): a neighbour without a point
+    // has an all-zero row, so it is read from the zero row instead (same bits:
+    // zeros either way) -- the gather then fetches only occupied rows
+    if (obits != nullptr && gv >= 0) {
+      uint32_t keep = 0u;
+#pragma unroll
+      for (int t = 0; t < 27; ++t) {
+        const long long gn = gv + (t / 9 - 1) * R2 + ((t / 3) % 3 - 1) * R + (t % 3 - 1);
+        const uint32_t word = ((m >> t) & 1u) ? obits[gn >> 5] : 0u;
+        keep |= ((word >> (gn & 31)) & 1u) << t;
+      }
+      m = keep;
+    }
     bval[q] = gv >= 0 ? m : 0u;
   }
 
@@ -2117,7 +2131,7 @@ static bool conv_win() {
 static int igemm_cl(const void* xs, const void* wsplit, const float* bias, int b, int cin,
                     int cout, int r, float* y, void* ws, size_t ws_bytes, void* stream,
                     const uint32_t* tmask, int mmode, const int* vlist = nullptr,
-                    const int* vcount = nullptr, int lg = 5) {
+                    const int* vcount = nullptr, int lg = 5, const uint32_t* obits = nullptr) {
   PCFM_CHECK_ARG(conv3_shape_ok(b, cin, cout, r),
                  "conv3d_igemm_cl: unsupported shape b=%d cin=%d cout=%d r=%d", b, cin, cout, r);
   if (b == 0) return PCFM_OK;
@@ -2178,11 +2192,11 @@ static int igemm_cl(const void* xs, const void* wsplit, const float* bias, int b
     if (PCFM_CONV_GK == 16 || cin % 32 != 0)
       hipLaunchKernelGGL(conv3_igemm_glds_kernel<16>, dim3((unsigned)glds_blocks), dim3(512), 0,
                          st, xh, xl, wh, wh + kSplitLo, zrow, bias, y, cin, cout, r, S, part, tmask,
-                         mm, vl, vc, lg);
+                         mm, vl, vc, lg, S == 1 ? obits : nullptr);
     else
       hipLaunchKernelGGL(conv3_igemm_glds_kernel<32>, dim3((unsigned)glds_blocks), dim3(512), 0,
                          st, xh, xl, wh, wh + kSplitLo, zrow, bias, y, cin, cout, r, S, part, tmask,
-                         mm, vl, vc, lg);
+                         mm, vl, vc, lg, S == 1 ? obits : nullptr);
     if (S > 1) {
       const long long total4 = (long long)b * cout * V / 4;
       hipLaunchKernelGGL(conv3_ksum_kernel, dim3((unsigned)ceil_div(total4, 256)), dim3(256), 0,
@@ -2323,8 +2337,16 @@ extern "C" int pcfm_conv3d_igemm_cl_list(const void* xs, const void* wsplit, con
                      which, bias, y, vbits);
   const int e = check_launch("conv3d_igemm_cl_list");
   if (e) return e;
+  // the forward reads occupied neighbour rows only (list 2's bitmap; env
+  // PCFM_LIST_ZROW=0: every in-volume row, A/B)
+  const char* zr = getenv("PCFM_LIST_ZROW");
+  const uint32_t* obits =
+      which == 1 && (zr == nullptr || zr[0] != '0')
+          ? (const uint32_t*)(lists + 64 + 4 * tiles + 2 * ((size_t)b * V / kChunk) +
+                              2 * (size_t)b * V)
+          : nullptr;
   return igemm_cl(xs, wsplit, bias, b, cin, cout, r, y, ws, ws_bytes, stream, nullptr, 0, l,
-                  vox ? lists + 2 + which : lists + which, vox ? 0 : 5);
+                  vox ? lists + 2 + which : lists + which, vox ? 0 : 5, obits);
 }
 
 static int wgrad_cap(int b, int r, int S) {
