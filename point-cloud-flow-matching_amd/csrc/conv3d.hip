@@ -2128,10 +2128,28 @@ static bool conv_win() {
 }
 
 
+// List-form tile in voxels, per direction (env PCFM_LIST_GN_FWD / _BWD = 256 or
+// 128, read per call: A/B runs).  The backward-data's list (the occupied
+// voxels, 12 % at r = 32, 21 % at r = 16) fills only ~120 / ~110 blocks of
+// 256 voxels -- half the CUs idle -- so it takes 128-voxel tiles: 0.89 -> 0.70
+// ms/step; the forward's longer list (30 % / 50 %) is slower on them (1.17 ->
+// 1.34), profiles/r06_ab_list_gn128.jsonl.  PCFM_LIST_NST: 3 / 2 LDS-DMA
+// stages at 128 (2: two blocks per CU; measured slower, 0.85 ms).
+static int list_gn(int which) {
+  const char* e = getenv(which == 0 ? "PCFM_LIST_GN_BWD" : "PCFM_LIST_GN_FWD");
+  if (e != nullptr) return atoi(e) == 128 ? 128 : 256;
+  return which == 0 ? 128 : 256;
+}
+static int list_nst() {
+  const char* e = getenv("PCFM_LIST_NST");
+  return e != nullptr && atoi(e) == 2 ? 2 : 3;
+}
+
 static int igemm_cl(const void* xs, const void* wsplit, const float* bias, int b, int cin,
                     int cout, int r, float* y, void* ws, size_t ws_bytes, void* stream,
                     const uint32_t* tmask, int mmode, const int* vlist = nullptr,
-                    const int* vcount = nullptr, int lg = 5, const uint32_t* obits = nullptr) {
+                    const int* vcount = nullptr, int lg = 5, const uint32_t* obits = nullptr,
+                    int lgn = 256) {
   PCFM_CHECK_ARG(conv3_shape_ok(b, cin, cout, r),
                  "conv3d_igemm_cl: unsupported shape b=%d cin=%d cout=%d r=%d", b, cin, cout, r);
   if (b == 0) return PCFM_OK;
@@ -2187,6 +2205,19 @@ static int igemm_cl(const void* xs, const void* wsplit, const float* bias, int b
         hipLaunchKernelGGL(conv3_ksum_kernel, dim3((unsigned)ceil_div(total4, 256)), dim3(256), 0,
                            st, (const float*)part, bias, S, cout, V, total4, y);
       }
+      return check_launch("conv3d_igemm_cl");
+    }
+    if (vl != nullptr && cin % 32 == 0 && lgn == 128) {
+      // list form on 128-voxel tiles (list_gn): twice the blocks
+      const long long lblocks = (long long)(V / 128) * (cout / kGM) * b;
+      if (list_nst() == 2)
+        hipLaunchKernelGGL((conv3_igemm_glds_kernel<32, 128, 2>), dim3((unsigned)lblocks),
+                           dim3(256), 0, st, xh, xl, wh, wh + kSplitLo, zrow, bias, y, cin, cout,
+                           r, S, part, tmask, mm, vl, vc, lg, obits);
+      else
+        hipLaunchKernelGGL((conv3_igemm_glds_kernel<32, 128, 3>), dim3((unsigned)lblocks),
+                           dim3(256), 0, st, xh, xl, wh, wh + kSplitLo, zrow, bias, y, cin, cout,
+                           r, S, part, tmask, mm, vl, vc, lg, obits);
       return check_launch("conv3d_igemm_cl");
     }
     if (PCFM_CONV_GK == 16 || cin % 32 != 0)
@@ -2346,7 +2377,8 @@ extern "C" int pcfm_conv3d_igemm_cl_list(const void* xs, const void* wsplit, con
                               2 * (size_t)b * V)
           : nullptr;
   return igemm_cl(xs, wsplit, bias, b, cin, cout, r, y, ws, ws_bytes, stream, nullptr, 0, l,
-                  vox ? lists + 2 + which : lists + which, vox ? 0 : 5, obits);
+                  vox ? lists + 2 + which : lists + which, vox ? 0 : 5, obits,
+                  vox ? list_gn(which) : 256);
 }
 
 static int wgrad_cap(int b, int r, int S) {
